@@ -1,0 +1,176 @@
+"""Synthetic inputs for the manifold optical-flow path.
+
+The reference reads a PLY surface and a potentials CSV
+(`S3_compute_v_and_detection_singularity.py:75-89`). Neither ships, so every
+parity case and benchmark runs on generated inputs of the same shapes:
+
+* a geodesic icosphere of frequency ``n`` (V = 10 n^2 + 2 vertices,
+  M = 20 n^2 triangles), optionally with seeded radial jitter, or an open
+  spherical cap cut from one;
+* VTK-like per-vertex normals (normalised sum of unit face normals) and
+  triangle areas (half the cross-product norm), the attributes S3 takes from
+  pyvista (`S3…py:83-84`);
+* a travelling wave ``I_k(x) = sin(kappa * phi(x) - omega * k)``.
+
+All arrays are float64 / int32 unless a caller asks otherwise.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+__all__ = [
+    "icosphere",
+    "spherical_cap",
+    "vertex_normals",
+    "triangle_areas",
+    "travelling_wave",
+    "mesh_for_config",
+    "CONFIG_FREQ",
+]
+
+# frequency n of the configs in SURVEY.md §8d (V = 10 n^2 + 2)
+CONFIG_FREQ = {"C1": 8, "C2": 57, "C3": 128, "C5": 253}
+
+
+def _icosahedron():
+    t = (1.0 + 5.0 ** 0.5) / 2.0
+    v = np.array(
+        [[-1, t, 0], [1, t, 0], [-1, -t, 0], [1, -t, 0],
+         [0, -1, t], [0, 1, t], [0, -1, -t], [0, 1, -t],
+         [t, 0, -1], [t, 0, 1], [-t, 0, -1], [-t, 0, 1]], dtype=np.float64)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    f = np.array(
+        [[0, 11, 5], [0, 5, 1], [0, 1, 7], [0, 7, 10], [0, 10, 11],
+         [1, 5, 9], [5, 11, 4], [11, 10, 2], [10, 7, 6], [7, 1, 8],
+         [3, 9, 4], [3, 4, 2], [3, 2, 6], [3, 6, 8], [3, 8, 9],
+         [4, 9, 5], [2, 4, 11], [6, 2, 10], [8, 6, 7], [9, 8, 1]],
+        dtype=np.int64)
+    return v, f
+
+
+def icosphere(n: int, radius: float = 10.0, jitter: float = 0.0, seed: int = 0):
+    """Geodesic icosphere of frequency ``n`` (class-I subdivision of each face
+    into n^2 triangles, projected to the sphere).
+
+    Returns ``(points (V,3) f64, triangles (M,3) int32)`` with outward,
+    consistently oriented triangles. ``jitter`` scales each radius by
+    ``1 + jitter * U(-1, 1)`` drawn from ``numpy.random.default_rng(seed)``.
+    """
+    if n < 1:
+        raise ValueError("frequency n must be >= 1")
+    cv, cf = _icosahedron()
+    nv = len(cv)
+    # canonical edge ids
+    edges = {}
+    for f in cf:
+        for a, b in ((f[0], f[1]), (f[1], f[2]), (f[2], f[0])):
+            key = (min(a, b), max(a, b))
+            if key not in edges:
+                edges[key] = len(edges)
+    ne = len(edges)
+    n_edge_pts = n - 1
+    n_face_pts = (n - 1) * (n - 2) // 2
+    total = nv + ne * n_edge_pts + len(cf) * n_face_pts
+
+    pts = np.empty((total, 3), dtype=np.float64)
+    pts[:nv] = cv
+    # lattice index -> vertex id, built per face
+    tris = []
+    for fi, (a, b, c) in enumerate(cf):
+        A, Bv, C = cv[a], cv[b], cv[c]
+        idx = -np.ones((n + 1, n + 1), dtype=np.int64)  # idx[i, j]: i along a->b, j along a->c
+
+        def edge_vertex(p, q, s):
+            # s-th interior point (1..n-1) from p towards q
+            key = (min(p, q), max(p, q))
+            eid = edges[key]
+            pos = s if p < q else n - s
+            return nv + eid * n_edge_pts + (pos - 1)
+
+        face_base = nv + ne * n_edge_pts + fi * n_face_pts
+        fcount = 0
+        for i in range(n + 1):
+            for j in range(n + 1 - i):
+                k = n - i - j  # weight of a
+                if i == 0 and j == 0:
+                    vid = a
+                elif i == n:
+                    vid = b
+                elif j == n:
+                    vid = c
+                elif j == 0:
+                    vid = edge_vertex(a, b, i)
+                elif i == 0:
+                    vid = edge_vertex(a, c, j)
+                elif k == 0:
+                    vid = edge_vertex(b, c, j)
+                else:
+                    vid = face_base + fcount
+                    fcount += 1
+                idx[i, j] = vid
+                pts[vid] = (k * A + i * Bv + j * C) / n
+        for i in range(n):
+            for j in range(n - i):
+                tris.append((idx[i, j], idx[i + 1, j], idx[i, j + 1]))
+                if i + j < n - 1:
+                    tris.append((idx[i + 1, j], idx[i + 1, j + 1], idx[i, j + 1]))
+    tri = np.asarray(tris, dtype=np.int64)
+    pts /= np.linalg.norm(pts, axis=1, keepdims=True)
+    r = np.full(total, float(radius))
+    if jitter:
+        rng = np.random.default_rng(seed)
+        r = r * (1.0 + jitter * rng.uniform(-1.0, 1.0, size=total))
+    pts *= r[:, None]
+    return pts, tri.astype(np.int32)
+
+
+def spherical_cap(n: int = 16, radius: float = 10.0, zcut: float = 0.5):
+    """Open cap: the triangles of ``icosphere(n)`` whose three vertices all have
+    z > zcut * radius, re-indexed (the G2 boundary case)."""
+    p, t = icosphere(n, radius)
+    keep_v = p[:, 2] > zcut * radius
+    keep_t = keep_v[t].all(axis=1)
+    t = t[keep_t]
+    used = np.unique(t)
+    remap = -np.ones(len(p), dtype=np.int64)
+    remap[used] = np.arange(len(used))
+    return p[used].copy(), remap[t].astype(np.int32)
+
+
+def vertex_normals(points: np.ndarray, triangles: np.ndarray) -> np.ndarray:
+    """VTK-like point normals: normalised sum of the unit normals of the
+    incident faces."""
+    p = np.asarray(points, dtype=np.float64)
+    t = np.asarray(triangles, dtype=np.int64)
+    fn = np.cross(p[t[:, 1]] - p[t[:, 0]], p[t[:, 2]] - p[t[:, 0]])
+    fn /= np.linalg.norm(fn, axis=1, keepdims=True)
+    vn = np.zeros_like(p)
+    for l in range(3):
+        np.add.at(vn, t[:, l], fn)
+    vn /= np.linalg.norm(vn, axis=1, keepdims=True)
+    return vn
+
+
+def triangle_areas(points: np.ndarray, triangles: np.ndarray) -> np.ndarray:
+    p = np.asarray(points, dtype=np.float64)
+    t = np.asarray(triangles, dtype=np.int64)
+    return 0.5 * np.linalg.norm(
+        np.cross(p[t[:, 1]] - p[t[:, 0]], p[t[:, 2]] - p[t[:, 0]]), axis=1)
+
+
+def travelling_wave(points: np.ndarray, T: int, kappa: float = 3.0,
+                    omega: float = 0.3) -> np.ndarray:
+    """``I[k, x] = sin(kappa * atan2(y, x) - omega * k)``, shape (T, N) f64."""
+    phi = np.arctan2(points[:, 1], points[:, 0])
+    k = np.arange(T, dtype=np.float64)[:, None]
+    return np.sin(kappa * phi[None, :] - omega * k)
+
+
+def mesh_for_config(name: str):
+    """(points, triangles, normals, areas) of a SURVEY.md §8d config mesh.
+
+    C1 has no jitter; the >=32k meshes get 0.5 % radial jitter, seed 0."""
+    n = CONFIG_FREQ[name]
+    jitter = 0.0 if name == "C1" else 0.005
+    p, t = icosphere(n, 10.0, jitter=jitter, seed=0)
+    return p, t, vertex_normals(p, t), triangle_areas(p, t)

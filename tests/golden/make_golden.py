@@ -1,0 +1,113 @@
+"""Capture golden vectors from the reference itself (container-only tool).
+
+Imports ``utils/compute_optical_flow.py`` from ``/root/reference`` (read-only;
+bytecode writing disabled; pyvista, absent here and unused by the hot-path
+functions, replaced by an empty module -- SURVEY.md §8c) and runs it on the
+synthetic inputs of ``mofhip.synth``. Writes small ``.npz`` fixtures next to
+this file. Only data is stored: inputs and the reference's outputs.
+
+Cases:
+  G1 642-vertex icosphere, T=16, lambda=0.01, t_k=range(T): e, grad_w,
+     integral_wi_wj, a2, A_0/f_0 and A_7/f_7 (captured at spsolve), V_k
+  G2 open spherical cap (641 vertices, boundary), T=6
+  G3 G1 with float32 coordinates/normals (pyvista dtype fidelity), T=4
+  G4 compute_velocity_field with processes_num=2 (list order and shape), T=6
+  G5 G1 with t_k = i/512 (S3's t_k = i/SF convention), T=4
+
+Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import scipy.sparse as sp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "manifold-based-optical-flow-method_amd"))
+
+from mofhip import synth  # noqa: E402
+
+REF = "/root/reference"
+
+
+def load_reference():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("pyvista", types.ModuleType("pyvista"))
+    sys.path.insert(0, REF)
+    import importlib
+    mod = importlib.import_module("utils.compute_optical_flow")
+    sys.path.remove(REF)
+    return mod
+
+
+def csr_dict(prefix, m):
+    m = sp.csr_matrix(m)
+    m.sort_indices()
+    return {prefix + "_indptr": m.indptr.astype(np.int32), prefix + "_indices": m.indices.astype(np.int32),
+            prefix + "_data": m.data.astype(np.float64)}
+
+
+def run_case(ref, name, coords, tris, normals, areas, I, t_k, capture_ks=(0,), lam=0.01,
+             processes_num=None):
+    captured = {}
+    orig = ref.spsolve
+
+    def spy(a, f):
+        captured.setdefault("calls", []).append((sp.csr_matrix(a).copy(), np.array(f, copy=True)))
+        return orig(a, f)
+
+    T = len(I)
+    a2, grad_w, e, iw, _ = ref.compute_geometrical_quantities(coords, normals, tris, areas)
+    out = {"coordinates": np.asarray(coords), "normals": np.asarray(normals),
+           "triangles": np.asarray(tris, dtype=np.int32), "areas": np.asarray(areas, dtype=np.float64),
+           "I": np.asarray(I, dtype=np.float64), "t_k": np.asarray(t_k, dtype=np.float64),
+           "lambda_": np.float64(lam), "e": e, "grad_w": grad_w, "integral_wi_wj": iw}
+    out.update(csr_dict("a2", a2))
+    if processes_num is None:
+        ref.spsolve = spy
+        try:
+            V = [ref.worker(k, a2, grad_w, e, iw, tris, t_k, areas, lam, I[k], I[k + 1])
+                 for k in range(T - 1)]
+        finally:
+            ref.spsolve = orig
+        for k in capture_ks:
+            A, f = captured["calls"][k]
+            out.update(csr_dict("A%d" % k, A))
+            out["f%d" % k] = f
+    else:
+        V, _ = ref.compute_velocity_field(processes_num, T, a2, grad_w, e, iw, tris, t_k, areas,
+                                          lam, I, I)
+        out["processes_num"] = np.int64(processes_num)
+    out["V_k"] = np.asarray(V)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, {k: getattr(v, "shape", ()) for k, v in out.items()})
+
+
+def main():
+    ref = load_reference()
+    # G1
+    p, t = synth.icosphere(8, 10.0)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    I = synth.travelling_wave(p, 16)
+    run_case(ref, "G1_ico642", p, t, n, a, I, list(range(16)), capture_ks=(0, 7))
+    # G2
+    pc, tc = synth.spherical_cap(16, 10.0, 0.5)
+    nc, ac = synth.vertex_normals(pc, tc), synth.triangle_areas(pc, tc)
+    Ic = synth.travelling_wave(pc, 6)
+    run_case(ref, "G2_cap641", pc, tc, nc, ac, Ic, list(range(6)), capture_ks=(0,))
+    # G3: float32 points/normals, float64 areas (pyvista/VTK dtypes)
+    p32, n32 = p.astype(np.float32), n.astype(np.float32)
+    a32 = synth.triangle_areas(p32.astype(np.float64), t)
+    run_case(ref, "G3_ico642_f32", p32, t, n32, a32, I[:4], list(range(4)), capture_ks=(0,))
+    # G4: the pool entry point
+    run_case(ref, "G4_pool2", p, t, n, a, I[:6], list(range(6)), processes_num=2)
+    # G5: t_k = i / SF
+    run_case(ref, "G5_dt512", p, t, n, a, I[:4], [i / 512 for i in range(4)], capture_ks=(0,))
+
+
+if __name__ == "__main__":
+    main()
