@@ -1,0 +1,161 @@
+/*
+ * mof.h -- C ABI of libmofhip.so, the MI355X-native manifold optical-flow
+ * solver (per-timestep FEM assembly + preconditioned CG on gfx950).
+ *
+ * Drop-in boundary for utils/compute_optical_flow.py of
+ * SEU-dynamical-models/Manifold-based-optical-flow-method (reference @
+ * 2025-10-31). Each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Every function returns int status: MOF_OK (0) or a negative MOF_E_*;
+ *    mof_last_error() then describes the failure (thread-local string).
+ *  - The caller owns every host buffer; the library owns the device buffers
+ *    behind a mof_mesh handle.
+ *  - One handle lives on one device. Calls on one handle are serialised by the
+ *    caller; different handles may be driven from different host threads
+ *    concurrently (ctypes releases the GIL).
+ *  - Unknown ordering is the reference's planar one: x[i + N*alpha],
+ *    alpha in {0,1} (compute_optical_flow.py:83-84,133-134).
+ *  - Arrays are C-contiguous row-major: xyz/nrm (N,3), tri (M,3), I (T,N),
+ *    e (N,2,3), grad_w (M,3,3), integral_wi_wj (M,2), V (K,2N).
+ */
+#ifndef MOF_H_
+#define MOF_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOF_ABI_VERSION 1
+
+/* status codes */
+#define MOF_OK 0
+#define MOF_E_ARG (-1)        /* invalid argument / shape */
+#define MOF_E_HIP (-2)        /* HIP runtime error (no device, OOM, fault) */
+#define MOF_E_NOCONV (-3)     /* a system did not converge; its V is NaN-filled */
+#define MOF_E_STATE (-4)      /* call out of order (e.g. export before assemble) */
+
+/* mof_mesh_create flags */
+#define MOF_GEOM_F32_POINTS 1u /* xyz holds float32 values: grad_w in float32
+                                  arithmetic, as numpy does for pyvista's
+                                  float32 points (S3…py:79, :238-255) */
+
+/* mof_opts.precision */
+#define MOF_PREC_F64 0         /* fp64 values + vectors, Jacobi-PCG */
+#define MOF_PREC_MIXED 1       /* fp32 inner PCG, fp64 residual refinement */
+
+/* mof_opts.flags */
+#define MOF_IO_DEVICE 1u       /* I, I2 and V_out are device pointers on the
+                                  handle's device (inputs resident in HBM) */
+#define MOF_NO_BLOCK_JACOBI 2u /* scalar Jacobi instead of 2x2 block Jacobi */
+#define MOF_TIME_SPMV 4u       /* bracket every PCG SpMV launch with HIP events
+                                  (fills mof_stats.ms_spmv / spmv_bytes) */
+
+/* mof_csr_export which */
+#define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */
+#define MOF_CSR_A_LAST 1       /* A = a1 + lambda*a2 of the last mof_assemble */
+
+typedef struct mof_mesh mof_mesh;
+
+typedef struct mof_opts {
+    uint32_t struct_size;  /* sizeof(mof_opts) */
+    uint32_t precision;    /* MOF_PREC_* */
+    uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI */
+    int32_t batch;         /* timesteps solved together per launch (0: auto) */
+    int32_t max_iter;      /* PCG iterations per inner solve (0: 10000) */
+    int32_t max_outer;     /* refinement steps, MOF_PREC_MIXED (0: 10) */
+    double rtol;           /* stop at ||f - A V||_2 <= rtol ||f||_2 (0: 1e-8) */
+    double inner_rtol;     /* MOF_PREC_MIXED inner PCG tolerance (0: 1e-4) */
+    void *stream;          /* hipStream_t to run on, NULL: the handle's own */
+} mof_opts;
+
+typedef struct mof_stats {
+    int64_t systems;          /* timesteps solved */
+    int64_t iterations;       /* PCG iterations summed over systems */
+    int32_t max_iterations;   /* largest per-system PCG iteration count */
+    int32_t failed;           /* systems that did not converge (NaN-filled) */
+    int32_t outer_steps;      /* refinement steps of the last batch */
+    int32_t batches;          /* batches launched */
+    double max_rel_residual;  /* max over systems of ||f - A V|| / ||f|| */
+    double ms_assembly;       /* device time, HIP events on the solve stream */
+    double ms_solve;
+    int64_t spmv_launches;    /* MOF_TIME_SPMV: PCG SpMV launches timed */
+    double ms_spmv;           /* MOF_TIME_SPMV: summed SpMV launch time */
+    double spmv_bytes;        /* MOF_TIME_SPMV: summed algorithmic bytes of
+                                 those launches */
+} mof_stats;
+
+typedef struct mof_mesh_info {
+    int32_t N, M;              /* vertices, triangles */
+    int32_t device;
+    int32_t nblocks;           /* vertex 2x2 blocks (= N + 2E on a closed mesh) */
+    int64_t nnz_struct;        /* 4 * nblocks: structural nnz of a2 / A */
+    int64_t sell_blocks;       /* blocks incl. SELL-64 padding */
+    double ms_geometry;        /* one-time device geometry + a2 build */
+    double ms_pattern;         /* one-time host pattern build */
+} mof_mesh_info;
+
+/* Library / device queries. */
+const char *mof_version(void);
+const char *mof_last_error(void);
+int mof_device_count(int32_t *count);
+
+/* Replaces compute_geometrical_quantities(coordinates, normals, triangles,
+ * areas) (compute_optical_flow.py:27-97): builds on `device` the tangent
+ * bases e, the hat-function gradients grad_w, integral_wi_wj, the block
+ * sparsity pattern and the smoothness matrix a2. xyz/nrm (N,3), tri (M,3)
+ * zero-based, area (M,). */
+int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri,
+                    const double *area, int32_t N, int32_t M, int32_t device,
+                    uint32_t flags, mof_mesh **out);
+int mof_mesh_destroy(mof_mesh *mesh);
+int mof_mesh_get_info(const mof_mesh *mesh, mof_mesh_info *info);
+
+/* Host copies of the geometric quantities compute_geometrical_quantities
+ * returns (:97): e (N,2,3), grad_w (M,3,3), integral_wi_wj (M,2). Any pointer
+ * may be NULL. */
+int mof_geometry_export(mof_mesh *mesh, double *e, double *grad_w, double *iw);
+
+/* CSR (2N x 2N, canonical: sorted columns) of a2 (MOF_CSR_A2, the lil matrix
+ * of :49,83-93) or of the last assembled A (MOF_CSR_A_LAST, :144-146).
+ * indptr has 2N+1 entries; indices/data need nnz_struct entries. With
+ * drop_zeros != 0 exact zeros are removed, as lil and csr+csr do in the
+ * reference. *nnz receives the entry count written. */
+int mof_csr_export(mof_mesh *mesh, int32_t which, int32_t drop_zeros,
+                   int32_t *indptr, int32_t *indices, double *data, int64_t *nnz);
+
+/* The assembly half of worker(k, ...) (:100-146) for one timestep: builds
+ * A = a1 + lambda*a2 and f from I0 = I_k[k], I1 = I_k_2[k+1] (host, N each)
+ * and dt = t_k[k+1] - t_k[k]. f (2N,) host, may be NULL; A is kept for
+ * mof_csr_export(MOF_CSR_A_LAST). */
+int mof_assemble(mof_mesh *mesh, const double *I0, const double *I1, double dt,
+                 double lambda, double *f);
+
+/* Replaces compute_velocity_field(processes_num, time_steps, a2, grad_w, e,
+ * integral_wi_wj, triangles, t_k, areas, lambda_, I_k, I_k_2) (:152-194)
+ * for k in [k0, k1), and worker(k, ...) (:100-149) for k1 = k0 + 1:
+ * V_out[k - k0] (2N,) solves (a1_k + lambda a2) V = f_k with I0 = I[k],
+ * I1 = I2[k+1] (I2 == NULL: I2 = I), dt = t_k[k+1] - t_k[k].
+ * I, I2: (T, N) f64; t_k: (T,) host f64; V_out: (k1-k0, 2N) f64.
+ * Host or device pointers per opts->flags. opts may be NULL (defaults).
+ * Systems that do not converge are NaN-filled and MOF_E_NOCONV is returned
+ * after every other system has been solved (spsolve's MatrixRankWarning +
+ * NaN result, scipy linsolve.py:287-289). stats may be NULL. */
+int mof_solve_range(mof_mesh *mesh, const double *I, const double *I2,
+                    const double *t_k, int32_t T, int32_t k0, int32_t k1,
+                    double lambda, const mof_opts *opts, double *V_out,
+                    mof_stats *stats);
+
+/* Measurement helper for bench.py: launches the PCG SpMV kernel `reps` times
+ * back to back on `batch` systems of the last solve's working set, timed with
+ * HIP events on the handle's stream. Returns the mean launch time and the
+ * algorithmic bytes one launch moves. */
+int mof_bench_spmv(mof_mesh *mesh, uint32_t precision, int32_t batch, int32_t reps,
+                   double *ms_per_launch, double *bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOF_H_ */

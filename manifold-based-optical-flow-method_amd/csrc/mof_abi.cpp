@@ -1,0 +1,359 @@
+// mof_abi.cpp -- extern "C" entry points of libmofhip.so (include/mof.h).
+//
+// Host orchestration only: argument checks, device uploads, batching of
+// timesteps, and result copies. All arithmetic runs in the HIP kernels of
+// mof_assemble.hip / mof_pcg.hip.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <new>
+
+#include "mof_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+template <class F>
+int guarded(F &&f) {
+    try {
+        f();
+        return MOF_OK;
+    } catch (const mof::Error &e) {
+        g_err = e.msg;
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_err = "host allocation failed";
+        return MOF_E_HIP;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return MOF_E_ARG;
+    }
+}
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int d) {
+        (void)hipGetDevice(&prev);
+        MOF_HIP(hipSetDevice(d));
+    }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+struct Events {
+    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+    Events() {
+        for (auto &x : e) MOF_HIP(hipEventCreate(&x));
+    }
+    ~Events() {
+        for (auto &x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+    float ms(int a, int b) const {
+        float v = 0.f;
+        (void)hipEventElapsedTime(&v, e[a], e[b]);
+        return v;
+    }
+};
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// SELL block layout -> canonical scalar CSR (2N x 2N).
+void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop_zeros,
+                 int32_t *indptr, int32_t *indices, double *data, int64_t *nnz_out) {
+    const mof::Pattern &P = m->pat;
+    const int32_t N = m->N;
+    int64_t nnz = 0;
+    indptr[0] = 0;
+    for (int32_t r = 0; r < 2 * N; ++r) {
+        const int32_t i = r % N, al = r / N;
+        for (int half = 0; half < 2; ++half) {  // columns j, then j + N
+            for (int32_t p = P.vptr[i], t = 0; p < P.vptr[i + 1]; ++p, ++t) {
+                const int64_t pos = (int64_t)P.sell_off[i >> 6] + (int64_t)t * mof::kSlice + (i & 63);
+                const double v = blk[4 * pos + 2 * al + half];
+                if (drop_zeros && v == 0.0) continue;
+                indices[nnz] = P.vcol[p] + half * N;
+                data[nnz] = v;
+                ++nnz;
+            }
+        }
+        indptr[r + 1] = (int32_t)nnz;
+    }
+    *nnz_out = nnz;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mof_version(void) { return "mofhip 0.1 (gfx950, abi 1)"; }
+
+const char *mof_last_error(void) { return g_err.c_str(); }
+
+int mof_device_count(int32_t *count) {
+    return guarded([&] {
+        MOF_REQUIRE(count, "count is NULL");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        *count = (e == hipSuccess) ? n : 0;
+    });
+}
+
+int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
+                    int32_t N, int32_t M, int32_t device, uint32_t flags, mof_mesh **out) {
+    return guarded([&] {
+        MOF_REQUIRE(out, "out is NULL");
+        *out = nullptr;
+        MOF_REQUIRE(xyz && nrm && tri && area, "NULL input array");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DeviceGuard dg(device);
+        auto *m = new mof_mesh();
+        try {
+            m->N = N;
+            m->M = M;
+            m->device = device;
+            m->flags = flags;
+            double t0 = now_ms();
+            mof::build_pattern(tri, N, M, m->pat);
+            m->ms_pattern = now_ms() - t0;
+            MOF_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+            hipStream_t s = m->stream;
+            const mof::Pattern &P = m->pat;
+            m->tri.alloc(3 * (size_t)M);
+            m->tri.upload(tri, 3 * (size_t)M, s);
+            m->area.alloc(M);
+            m->area.upload(area, M, s);
+            m->vptr.alloc(N + 1);
+            m->vptr.upload(P.vptr.data(), N + 1, s);
+            m->vcol.alloc(P.vcol.size());
+            m->vcol.upload(P.vcol.data(), P.vcol.size(), s);
+            m->cptr.alloc(P.cptr.size());
+            m->cptr.upload(P.cptr.data(), P.cptr.size(), s);
+            m->clist.alloc(P.clist.size());
+            m->clist.upload(P.clist.data(), P.clist.size(), s);
+            m->sell_off.alloc(P.sell_off.size());
+            m->sell_off.upload(P.sell_off.data(), P.sell_off.size(), s);
+            m->sell_col.alloc(P.sell_col.size());
+            m->sell_col.upload(P.sell_col.data(), P.sell_col.size(), s);
+            mof::DevArray<double> dxyz, dnrm;
+            dxyz.alloc(3 * (size_t)N);
+            dxyz.upload(xyz, 3 * (size_t)N, s);
+            dnrm.alloc(3 * (size_t)N);
+            dnrm.upload(nrm, 3 * (size_t)N, s);
+            m->e.alloc(6 * (size_t)N);
+            m->gw.alloc(9 * (size_t)M);
+            m->iw.alloc(2 * (size_t)M);
+            m->a2.alloc(4 * (size_t)P.sell_nb());
+            m->a2.zero(s);
+            Events ev;
+            MOF_HIP(hipEventRecord(ev.e[0], s));
+            mof::launch_geometry(m, dxyz.p, dnrm.p, (flags & MOF_GEOM_F32_POINTS) != 0);
+            mof::launch_a2(m);
+            MOF_HIP(hipEventRecord(ev.e[1], s));
+            MOF_HIP(hipStreamSynchronize(s));
+            m->ms_geometry = ev.ms(0, 1);
+        } catch (...) {
+            mof_mesh_destroy(m);
+            throw;
+        }
+        *out = m;
+    });
+}
+
+int mof_mesh_destroy(mof_mesh *m) {
+    if (!m) return MOF_OK;
+    return guarded([&] {
+        {
+            DeviceGuard dg(m->device);
+            if (m->stream) (void)hipStreamSynchronize(m->stream);
+            if (m->h_sysi) (void)hipHostFree(m->h_sysi);
+            if (m->h_sysd) (void)hipHostFree(m->h_sysd);
+            for (auto e : m->spmv_events) (void)hipEventDestroy(e);
+            if (m->stream) (void)hipStreamDestroy(m->stream);
+            m->stream = nullptr;
+            delete m;  // DevArray destructors free on the current (guarded) device
+        }
+    });
+}
+
+int mof_mesh_get_info(const mof_mesh *m, mof_mesh_info *info) {
+    return guarded([&] {
+        MOF_REQUIRE(m && info, "NULL argument");
+        info->N = m->N;
+        info->M = m->M;
+        info->device = m->device;
+        info->nblocks = m->pat.nblocks();
+        info->nnz_struct = 4 * (int64_t)m->pat.nblocks();
+        info->sell_blocks = m->pat.sell_nb();
+        info->ms_geometry = m->ms_geometry;
+        info->ms_pattern = m->ms_pattern;
+    });
+}
+
+int mof_geometry_export(mof_mesh *m, double *e, double *grad_w, double *iw) {
+    return guarded([&] {
+        MOF_REQUIRE(m, "mesh is NULL");
+        DeviceGuard dg(m->device);
+        hipStream_t s = m->stream;
+        if (e) MOF_HIP(hipMemcpyAsync(e, m->e.p, m->e.bytes(), hipMemcpyDeviceToHost, s));
+        if (grad_w) MOF_HIP(hipMemcpyAsync(grad_w, m->gw.p, m->gw.bytes(), hipMemcpyDeviceToHost, s));
+        if (iw) MOF_HIP(hipMemcpyAsync(iw, m->iw.p, m->iw.bytes(), hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipStreamSynchronize(s));
+    });
+}
+
+int mof_csr_export(mof_mesh *m, int32_t which, int32_t drop_zeros, int32_t *indptr,
+                   int32_t *indices, double *data, int64_t *nnz) {
+    return guarded([&] {
+        MOF_REQUIRE(m && indptr && indices && data && nnz, "NULL argument");
+        MOF_REQUIRE(which == MOF_CSR_A2 || which == MOF_CSR_A_LAST, "unknown matrix id");
+        DeviceGuard dg(m->device);
+        const int64_t snb = m->pat.sell_nb();
+        std::vector<double> blk(4 * (size_t)snb);
+        const double *src = m->a2.p;
+        if (which == MOF_CSR_A_LAST) {
+            if (!m->have_last_A) throw mof::Error{MOF_E_STATE, "no assembled system: call mof_assemble first"};
+            src = m->ws.A64.p;
+        }
+        MOF_HIP(hipMemcpyAsync(blk.data(), src, sizeof(double) * blk.size(), hipMemcpyDeviceToHost,
+                               m->stream));
+        MOF_HIP(hipStreamSynchronize(m->stream));
+        sell_to_csr(m, blk, drop_zeros, indptr, indices, data, nnz);
+    });
+}
+
+int mof_assemble(mof_mesh *m, const double *I0, const double *I1, double dt, double lambda,
+                 double *f) {
+    return guarded([&] {
+        MOF_REQUIRE(m && I0 && I1, "NULL argument");
+        DeviceGuard dg(m->device);
+        hipStream_t s = m->stream;
+        mof::ensure_workspace(m, 1);
+        mof::Workspace &w = m->ws;
+        const int64_t N = m->N;
+        MOF_HIP(hipMemcpyAsync(w.Ibuf.p, I0, sizeof(double) * N, hipMemcpyHostToDevice, s));
+        MOF_HIP(hipMemcpyAsync(w.Ibuf.p + N, I1, sizeof(double) * N, hipMemcpyHostToDevice, s));
+        MOF_HIP(hipMemcpyAsync(w.dt.p, &dt, sizeof(double), hipMemcpyHostToDevice, s));
+        mof::launch_assemble(m, 1, w.Ibuf.p, w.Ibuf.p + N, N, lambda, true, s);
+        m->have_last_A = true;
+        if (f) {
+            std::vector<double> fi(2 * N);
+            MOF_HIP(hipMemcpyAsync(fi.data(), w.rhs.p, sizeof(double) * 2 * N, hipMemcpyDeviceToHost, s));
+            MOF_HIP(hipStreamSynchronize(s));
+            for (int64_t i = 0; i < N; ++i) {
+                f[i] = fi[2 * i];
+                f[N + i] = fi[2 * i + 1];
+            }
+        }
+        MOF_HIP(hipStreamSynchronize(s));
+    });
+}
+
+int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double *t_k, int32_t T,
+                    int32_t k0, int32_t k1, double lambda, const mof_opts *opts, double *V_out,
+                    mof_stats *stats) {
+    int nonconv = 0;
+    int rc = guarded([&] {
+        MOF_REQUIRE(m && I && t_k && V_out, "NULL argument");
+        MOF_REQUIRE(T >= 1 && k0 >= 0 && k0 <= k1 && k1 <= T - 1, "need 0 <= k0 <= k1 <= T-1");
+        mof_opts o{};
+        if (opts) {
+            MOF_REQUIRE(opts->struct_size == 0 || opts->struct_size >= sizeof(mof_opts),
+                        "mof_opts.struct_size too small");
+            o = *opts;
+        }
+        MOF_REQUIRE(o.precision == MOF_PREC_F64 || o.precision == MOF_PREC_MIXED, "unknown precision");
+        mof::SolveParams sp;
+        sp.precision = o.precision;
+        sp.block_jacobi = !(o.flags & MOF_NO_BLOCK_JACOBI);
+        sp.time_spmv = (o.flags & MOF_TIME_SPMV) != 0;
+        mof::SpmvTiming timing;
+        sp.max_iter = o.max_iter > 0 ? o.max_iter : 10000;
+        sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
+        sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
+        sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
+        const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
+        if (!I2) I2 = I;
+        DeviceGuard dg(m->device);
+        hipStream_t s = o.stream ? (hipStream_t)o.stream : m->stream;
+        const int32_t K = k1 - k0;
+        mof_stats st{};
+        if (K > 0) {
+            const int32_t Bmax = o.batch > 0 ? o.batch : 16;
+            const int32_t B = std::min(K, Bmax);
+            mof::ensure_workspace(m, B);
+            mof::Workspace &w = m->ws;
+            const int64_t N = m->N;
+            Events ev;
+            std::vector<double> dts(B);
+            for (int32_t k = k0; k < k1; k += B) {
+                const int32_t nb = std::min(B, k1 - k);
+                for (int32_t b = 0; b < nb; ++b) dts[b] = t_k[k + b + 1] - t_k[k + b];
+                MOF_HIP(hipMemcpyAsync(w.dt.p, dts.data(), sizeof(double) * nb, hipMemcpyHostToDevice, s));
+                const double *I0p, *I1p;
+                if (dev_io) {
+                    I0p = I + (int64_t)k * N;
+                    I1p = I2 + (int64_t)(k + 1) * N;
+                } else {
+                    MOF_HIP(hipMemcpyAsync(w.Ibuf.p, I + (int64_t)k * N, sizeof(double) * N * nb,
+                                           hipMemcpyHostToDevice, s));
+                    MOF_HIP(hipMemcpyAsync(w.Ibuf.p + N * B, I2 + (int64_t)(k + 1) * N,
+                                           sizeof(double) * N * nb, hipMemcpyHostToDevice, s));
+                    I0p = w.Ibuf.p;
+                    I1p = w.Ibuf.p + N * B;
+                }
+                MOF_HIP(hipEventRecord(ev.e[0], s));
+                mof::launch_assemble(m, nb, I0p, I1p, N, lambda, sp.block_jacobi, s);
+                MOF_HIP(hipEventRecord(ev.e[1], s));
+                int32_t outer = 0;
+                st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
+                st.outer_steps = outer;
+                double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : w.Vbuf.p;
+                mof::launch_to_planar(m, nb, Vdst, s);
+                MOF_HIP(hipEventRecord(ev.e[2], s));
+                if (!dev_io)
+                    MOF_HIP(hipMemcpyAsync(V_out + (int64_t)(k - k0) * 2 * N, w.Vbuf.p,
+                                           sizeof(double) * 2 * N * nb, hipMemcpyDeviceToHost, s));
+                MOF_HIP(hipStreamSynchronize(s));
+                st.ms_assembly += ev.ms(0, 1);
+                st.ms_solve += ev.ms(1, 2);
+                for (int32_t b = 0; b < nb; ++b) {
+                    if (m->h_sysi[b * mof::kSysStride + mof::SI_FAILED]) st.failed++;
+                    st.max_rel_residual =
+                        std::max(st.max_rel_residual, m->h_sysd[b * mof::kSysStride + mof::SD_REL]);
+                }
+                st.batches++;
+            }
+            m->have_last_A = false;  // slot 0 no longer holds a mof_assemble result
+        }
+        st.systems = K;
+        st.spmv_launches = timing.launches;
+        st.ms_spmv = timing.ms;
+        st.spmv_bytes = timing.bytes;
+        if (stats) *stats = st;
+        if (st.failed) {
+            nonconv = 1;
+            g_err = std::to_string(st.failed) + " system(s) did not converge; their V is NaN-filled";
+        }
+    });
+    if (rc == MOF_OK && nonconv) return MOF_E_NOCONV;
+    return rc;
+}
+
+int mof_bench_spmv(mof_mesh *m, uint32_t precision, int32_t batch, int32_t reps,
+                   double *ms_per_launch, double *bytes_per_launch) {
+    return guarded([&] {
+        MOF_REQUIRE(m && ms_per_launch && bytes_per_launch, "NULL argument");
+        MOF_REQUIRE(reps > 0, "reps must be positive");
+        DeviceGuard dg(m->device);
+        *ms_per_launch = mof::bench_spmv(m, precision, batch, reps, m->stream, bytes_per_launch);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,339 @@
+// mof_assemble.hip -- geometry and per-timestep FEM assembly kernels (gfx950).
+//
+// Compiled with -ffp-contract=off: every product and sum below is rounded
+// exactly where the reference's numpy code rounds it, and the only fused
+// multiply-adds are the explicit fma() calls that restate np.dot of two
+// float64 3-vectors on the reference's BLAS (fma(x2,y2, fma(x1,y1, x0*y0)),
+// DESIGN.md §Bit-exact assembly). The assembled A and f therefore match the
+// reference's bit for bit (tests/test_gpu_parity.py).
+//
+// All per-timestep accumulation is a gather in triangle order over the
+// pre-built contribution lists (mof_pattern.cpp): deterministic, no atomics.
+#include "mof_internal.h"
+
+namespace mof {
+namespace {
+
+__device__ __forceinline__ double dot64(const double *x, const double *y) {
+    return fma(x[2], y[2], fma(x[1], y[1], x[0] * y[0]));
+}
+
+// np.dot of two float32 3-vectors on scipy-openblas: float products summed
+// in double, rounded to float once.
+__device__ __forceinline__ float dot32(const float *x, const float *y) {
+    double acc = 0.0;
+    acc += (double)(x[0] * y[0]);
+    acc += (double)(x[1] * y[1]);
+    acc += (double)(x[2] * y[2]);
+    return (float)acc;
+}
+
+// compute_orthonormal_basis (compute_optical_flow.py:210-235), one vertex per
+// thread. numpy types the basis float64 even for float32 normals.
+__global__ __launch_bounds__(kWG) void k_basis(const double *__restrict__ nrm, int32_t N,
+                                               double *__restrict__ e) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    if (i >= N) return;
+    const double n[3] = {nrm[3 * (int64_t)i], nrm[3 * (int64_t)i + 1], nrm[3 * (int64_t)i + 2]};
+    double a[3], c[3];
+    if (n[0] != 0.0 || n[1] != 0.0) {
+        a[0] = -n[1]; a[1] = n[0]; a[2] = 0.0;
+    } else {
+        a[0] = 0.0; a[1] = -n[2]; a[2] = n[1];
+    }
+    c[0] = n[1] * a[2] - n[2] * a[1];
+    c[1] = n[2] * a[0] - n[0] * a[2];
+    c[2] = n[0] * a[1] - n[1] * a[0];
+    const double na = sqrt(dot64(a, a)), nc = sqrt(dot64(c, c));
+    double *o = e + 6 * (int64_t)i;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        o[d] = a[d] / na;
+        o[3 + d] = c[d] / nc;
+    }
+}
+
+// compute_gradient_w(p_i, p_j, p_k) (:238-255): the altitude vector from i
+// scaled by 1/|h|^2.
+__device__ void grad_w64(const double *pi, const double *pj, const double *pk, double *g) {
+    double jk[3], ji[3], ih[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        jk[d] = pk[d] - pj[d];
+        ji[d] = pi[d] - pj[d];
+    }
+    const double s = dot64(ji, jk), q = dot64(jk, jk);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) ih[d] = (pj[d] - pi[d]) + (s * jk[d]) / q;
+    const double h = dot64(ih, ih);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) g[d] = ih[d] / h;
+}
+
+__device__ void grad_w32(const double *pid, const double *pjd, const double *pkd, double *g) {
+    float pi[3], pj[3], pk[3], jk[3], ji[3], ih[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        pi[d] = (float)pid[d];
+        pj[d] = (float)pjd[d];
+        pk[d] = (float)pkd[d];
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        jk[d] = pk[d] - pj[d];
+        ji[d] = pi[d] - pj[d];
+    }
+    const float s = dot32(ji, jk), q = dot32(jk, jk);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) ih[d] = (pj[d] - pi[d]) + (s * jk[d]) / q;
+    const float h = dot32(ih, ih);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) g[d] = (double)(ih[d] / h);
+}
+
+// grad_w (M,3,3) and integral_wi_wj (M,2) (:60-75), one triangle per thread.
+template <bool F32>
+__global__ __launch_bounds__(kWG) void k_gradw(const double *__restrict__ xyz,
+                                               const int32_t *__restrict__ tri,
+                                               const double *__restrict__ area, int32_t M,
+                                               double *__restrict__ gw, double *__restrict__ iw) {
+    const int32_t T = blockIdx.x * kWG + threadIdx.x;
+    if (T >= M) return;
+    const int32_t *v = tri + 3 * (int64_t)T;
+    double P[3][3];
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) P[l][d] = xyz[3 * (int64_t)v[l] + d];
+    double *g = gw + 9 * (int64_t)T;
+    if (F32) {
+        grad_w32(P[0], P[1], P[2], g);
+        grad_w32(P[1], P[0], P[2], g + 3);
+        grad_w32(P[2], P[0], P[1], g + 6);
+    } else {
+        grad_w64(P[0], P[1], P[2], g);
+        grad_w64(P[1], P[0], P[2], g + 3);
+        grad_w64(P[2], P[0], P[1], g + 6);
+    }
+    const double A = area[T];
+    iw[2 * (int64_t)T] = A / 6;
+    iw[2 * (int64_t)T + 1] = A / 12;
+}
+
+__device__ __forceinline__ int64_t sell_pos(const int32_t *sell_off, int32_t i, int32_t t) {
+    return (int64_t)sell_off[i >> 6] + (int64_t)t * kSlice + (i & 63);
+}
+
+// a2 (:78-93, compute_a2 :258-270), one vertex row per thread: block (i, j)
+// entry (alpha, beta) = fold over the triangles holding edge (i, j) of
+// (e_i^alpha . e_j^beta)(grad w_a . grad w_b) A_T, in triangle order.
+__global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict__ vptr,
+                                            const int32_t *__restrict__ vcol,
+                                            const int32_t *__restrict__ cptr,
+                                            const int32_t *__restrict__ clist,
+                                            const int32_t *__restrict__ sell_off,
+                                            const double *__restrict__ e,
+                                            const double *__restrict__ gw,
+                                            const double *__restrict__ area,
+                                            double *__restrict__ a2) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    if (i >= N) return;
+    const double *ei = e + 6 * (int64_t)i;
+    for (int32_t p = vptr[i], t = 0; p < vptr[i + 1]; ++p, ++t) {
+        const int32_t j = vcol[p];
+        const double *ej = e + 6 * (int64_t)j;
+        double ee[4];
+#pragma unroll
+        for (int al = 0; al < 2; ++al)
+#pragma unroll
+            for (int be = 0; be < 2; ++be) ee[2 * al + be] = dot64(ei + 3 * al, ej + 3 * be);
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
+            const int32_t code = clist[c];
+            const int32_t T = code / 9, a = (code % 9) / 3, b = code % 3;
+            const double *g = gw + 9 * (int64_t)T;
+            const double gg = dot64(g + 3 * a, g + 3 * b);
+            const double A = area[T];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] += ee[q] * gg * A;
+        }
+        double *o = a2 + 4 * sell_pos(sell_off, i, t);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = acc[q];
+    }
+}
+
+// Per-triangle half of worker (:113-126, compute_f :288-311) for B systems:
+// grad_M I and, for each corner a and alpha, u = grad_M I . e_a^alpha and the
+// f term (u (2 dI_a + sum of the other distinct corners' dI) A_T) / 12.
+__global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__restrict__ tri,
+                                                  const double *__restrict__ gw,
+                                                  const double *__restrict__ e,
+                                                  const double *__restrict__ area,
+                                                  const double *__restrict__ I0,
+                                                  const double *__restrict__ I1, int64_t ldI,
+                                                  const double *__restrict__ dt,
+                                                  double *__restrict__ u,
+                                                  double *__restrict__ fc) {
+    const int32_t T = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (T >= M) return;
+    const int32_t v[3] = {tri[3 * (int64_t)T], tri[3 * (int64_t)T + 1], tri[3 * (int64_t)T + 2]};
+    const double *g = gw + 9 * (int64_t)T;
+    const double *i0 = I0 + b * ldI;
+    const double *i1 = I1 + b * ldI;
+    const double a0 = i0[v[0]], a1 = i0[v[1]], a2 = i0[v[2]];
+    double gI[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) gI[d] = (a0 * g[d] + a1 * g[3 + d]) + a2 * g[6 + d];
+    const double h = dt[b];
+    const double pd[3] = {(i1[v[0]] - a0) / h, (i1[v[1]] - a1) / h, (i1[v[2]] - a2) / h};
+    const double A = area[T];
+    const int64_t base = 6 * ((int64_t)b * M + T);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        // set(T) - {i}: distinct corners other than vertex v[a], in corner order
+        double po = 0.0;
+        int cnt = 0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            bool dup = false;
+#pragma unroll
+            for (int q = 0; q < c; ++q) dup |= (v[q] == v[c]);
+            if (dup || v[c] == v[a]) continue;
+            po = cnt ? po + pd[c] : pd[c];
+            ++cnt;
+        }
+        const double *ea = e + 6 * (int64_t)v[a];
+#pragma unroll
+        for (int al = 0; al < 2; ++al) {
+            const double uu = dot64(gI, ea + 3 * al);
+            u[base + 2 * a + al] = uu;
+            fc[base + 2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
+        }
+    }
+}
+
+// Per-vertex half of worker (:127-146) for B systems: block (i, j) of
+// a1 = fold over its terms of (u_a^alpha u_b^beta) integral, then
+// A = a1 + lambda*a2 (fp64 and a rounded fp32 copy, SELL layout); the
+// diagonal block's terms also fold f_i and give the 2x2 block-Jacobi inverse.
+__global__ __launch_bounds__(kWG) void k_assemble_rows(
+    int32_t N, int32_t M, int64_t sell_nb, const int32_t *__restrict__ vptr,
+    const int32_t *__restrict__ vcol, const int32_t *__restrict__ cptr,
+    const int32_t *__restrict__ clist, const int32_t *__restrict__ sell_off,
+    const double *__restrict__ iw, const double *__restrict__ a2, const double *__restrict__ u,
+    const double *__restrict__ fc, double lambda, int block_jacobi, double *__restrict__ A64,
+    float *__restrict__ A32, double *__restrict__ dinv64, float *__restrict__ dinv32,
+    double *__restrict__ rhs) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= N) return;
+    const double *ub = u + 6 * (int64_t)b * M;
+    const double *fb = fc + 6 * (int64_t)b * M;
+    double f0 = 0.0, f1 = 0.0;
+    double D[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int32_t p = vptr[i], t = 0; p < vptr[i + 1]; ++p, ++t) {
+        const int32_t j = vcol[p];
+        const bool diag = (j == i);
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
+            const int32_t code = clist[c];
+            const int32_t T = code / 9, a = (code % 9) / 3, bb = code % 3;
+            const double ua0 = ub[6 * (int64_t)T + 2 * a], ua1 = ub[6 * (int64_t)T + 2 * a + 1];
+            const double ub0 = ub[6 * (int64_t)T + 2 * bb], ub1 = ub[6 * (int64_t)T + 2 * bb + 1];
+            const double integ = iw[2 * (int64_t)T + (diag ? 0 : 1)];
+            acc[0] += ua0 * ub0 * integ;
+            acc[1] += ua0 * ub1 * integ;
+            acc[2] += ua1 * ub0 * integ;
+            acc[3] += ua1 * ub1 * integ;
+            if (diag && a == bb) {
+                f0 += fb[6 * (int64_t)T + 2 * a];
+                f1 += fb[6 * (int64_t)T + 2 * a + 1];
+            }
+        }
+        const int64_t pos = sell_pos(sell_off, i, t);
+        const double *s2 = a2 + 4 * pos;
+        double Av[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Av[q] = acc[q] + lambda * s2[q];
+        double *o64 = A64 + 4 * ((int64_t)b * sell_nb + pos);
+        *reinterpret_cast<double2 *>(o64) = make_double2(Av[0], Av[1]);
+        *reinterpret_cast<double2 *>(o64 + 2) = make_double2(Av[2], Av[3]);
+        *reinterpret_cast<float4 *>(A32 + 4 * ((int64_t)b * sell_nb + pos)) =
+            make_float4((float)Av[0], (float)Av[1], (float)Av[2], (float)Av[3]);
+        if (diag) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) D[q] = Av[q];
+        }
+    }
+    double inv[4];
+    if (block_jacobi) {
+        const double det = D[0] * D[3] - D[1] * D[2];
+        inv[0] = D[3] / det; inv[1] = -D[1] / det; inv[2] = -D[2] / det; inv[3] = D[0] / det;
+    } else {
+        inv[0] = 1.0 / D[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / D[3];
+    }
+    const int64_t vi = (int64_t)b * N + i;
+    *reinterpret_cast<double2 *>(dinv64 + 4 * vi) = make_double2(inv[0], inv[1]);
+    *reinterpret_cast<double2 *>(dinv64 + 4 * vi + 2) = make_double2(inv[2], inv[3]);
+    *reinterpret_cast<float4 *>(dinv32 + 4 * vi) =
+        make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+    *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
+}
+
+// x64 (interleaved) -> V (B, 2N) planar; failed systems are NaN-filled.
+__global__ __launch_bounds__(kWG) void k_to_planar(int32_t N, const double *__restrict__ x,
+                                                   const int32_t *__restrict__ sysi,
+                                                   double *__restrict__ V) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= N) return;
+    const bool failed = sysi[b * kSysStride + SI_FAILED] != 0;
+    const double2 v = *reinterpret_cast<const double2 *>(x + 2 * ((int64_t)b * N + i));
+    const double nan = __builtin_nan("");
+    V[(int64_t)b * 2 * N + i] = failed ? nan : v.x;
+    V[(int64_t)b * 2 * N + N + i] = failed ? nan : v.y;
+}
+
+inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
+
+}  // namespace
+
+void launch_geometry(mof_mesh *m, const double *d_xyz, const double *d_nrm, bool f32_points) {
+    hipStream_t s = m->stream;
+    k_basis<<<grid1(m->N), kWG, 0, s>>>(d_nrm, m->N, m->e.p);
+    if (f32_points)
+        k_gradw<true><<<grid1(m->M), kWG, 0, s>>>(d_xyz, m->tri.p, m->area.p, m->M, m->gw.p, m->iw.p);
+    else
+        k_gradw<false><<<grid1(m->M), kWG, 0, s>>>(d_xyz, m->tri.p, m->area.p, m->M, m->gw.p, m->iw.p);
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_a2(mof_mesh *m) {
+    k_a2<<<grid1(m->N), kWG, 0, m->stream>>>(m->N, m->vptr.p, m->vcol.p, m->cptr.p, m->clist.p,
+                                             m->sell_off.p, m->e.p, m->gw.p, m->area.p, m->a2.p);
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
+                     double lambda, bool block_jacobi, hipStream_t s) {
+    Workspace &w = m->ws;
+    dim3 gt((unsigned)((m->M + kWG - 1) / kWG), (unsigned)B);
+    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
+                                  w.u.p, w.fc.p);
+    dim3 gr((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
+    k_assemble_rows<<<gr, kWG, 0, s>>>(m->N, m->M, m->pat.sell_nb(), m->vptr.p, m->vcol.p,
+                                       m->cptr.p, m->clist.p, m->sell_off.p, m->iw.p, m->a2.p,
+                                       w.u.p, w.fc.p, lambda, block_jacobi ? 1 : 0, w.A64.p,
+                                       w.A32.p, w.dinv64.p, w.dinv32.p, w.rhs.p);
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s) {
+    dim3 g((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
+    k_to_planar<<<g, kWG, 0, s>>>(m->N, m->ws.x64.p, m->ws.sysi.p, V);
+    MOF_HIP(hipGetLastError());
+}
+
+}  // namespace mof

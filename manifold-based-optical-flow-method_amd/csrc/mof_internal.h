@@ -1,0 +1,168 @@
+// mof_internal.h -- shared declarations of libmofhip (MI355X / gfx950).
+//
+// Device data layout:
+//  * vertex 2x2 blocks: block p = (i, j) of vertex row i holds
+//      {A(i,j), A(i,j+N), A(i+N,j), A(i+N,j+N)}  (planar unknowns of the
+//      reference, compute_optical_flow.py:83-84)
+//  * matrices are stored SELL-64: row i = slice i/64, lane i%64; its t-th
+//    block lives at sell_off[i/64] + 64*t + i%64, so one wave-instruction
+//    reads 64 consecutive blocks (16 B each in fp32, 32 B in fp64);
+//  * solver vectors are interleaved per vertex: v[2*i + alpha].
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/mof.h"
+
+namespace mof {
+
+constexpr int kWG = 256;     // threads per workgroup (4 waves)
+constexpr int kSlice = 64;   // SELL slice height = wavefront size
+
+struct Error {
+    int code;
+    std::string msg;
+};
+
+#define MOF_HIP(call)                                                              \
+    do {                                                                           \
+        hipError_t e_ = (call);                                                    \
+        if (e_ != hipSuccess)                                                      \
+            throw ::mof::Error{MOF_E_HIP, std::string(#call) + " failed: " +       \
+                                              hipGetErrorString(e_)};              \
+    } while (0)
+
+#define MOF_REQUIRE(cond, msg)                                                     \
+    do {                                                                           \
+        if (!(cond)) throw ::mof::Error{MOF_E_ARG, (msg)};                         \
+    } while (0)
+
+template <typename T>
+struct DevArray {
+    T *p = nullptr;
+    size_t n = 0;
+    DevArray() = default;
+    DevArray(const DevArray &) = delete;
+    DevArray &operator=(const DevArray &) = delete;
+    ~DevArray() { release(); }
+    void alloc(size_t count) {
+        release();
+        if (count == 0) count = 1;
+        MOF_HIP(hipMalloc(&p, count * sizeof(T)));
+        n = count;
+    }
+    void zero(hipStream_t s) { MOF_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s)); }
+    void upload(const T *h, size_t count, hipStream_t s) {
+        MOF_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+// Host-side sparsity structures, built once per mesh (mof_pattern.cpp).
+struct Pattern {
+    int32_t N = 0, M = 0;
+    std::vector<int32_t> vptr, vcol;   // vertex adjacency, self included, sorted
+    std::vector<int32_t> cptr, clist;  // per block: contributions T*9 + a*3 + b, T ascending
+    int32_t nslices = 0;
+    std::vector<int32_t> sell_off;     // (nslices+1), in blocks (multiples of 64)
+    std::vector<int32_t> sell_col;     // (sell_off[nslices]) column vertex, padding -> row itself
+    int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
+    int32_t nblocks() const { return (int32_t)vcol.size(); }
+};
+
+void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat);
+
+// Per-batch device workspace (capacity B systems).
+struct Workspace {
+    int32_t cap = 0;        // systems
+    int32_t nblk = 0;       // workgroups per system for row kernels
+    DevArray<double> u, fc;            // [B][M][6] per-triangle g.e and f terms
+    DevArray<double> A64;              // [B][sell_nb][4]
+    DevArray<float> A32;               // [B][sell_nb][4]
+    DevArray<double> dinv64;           // [B][N][4] 2x2 block-Jacobi inverses
+    DevArray<float> dinv32;
+    DevArray<double> rhs;              // [B][N][2] f (interleaved)
+    DevArray<double> x64, r64;         // [B][N][2] outer solution / residual
+    DevArray<double> vx, vr, vz, vp, vq;  // [B][N][2] inner PCG vectors (fp64 sized)
+    DevArray<double> part_pq;          // [B][nblk]
+    DevArray<double> part_rzrr;        // [2][B][nblk][2]
+    DevArray<double> part_rr0;         // [B][nblk][2]
+    DevArray<double> sysd;             // [B][8] per-system scalars
+    DevArray<int32_t> sysi;            // [B][8] per-system flags
+    DevArray<double> dt;               // [B]
+    DevArray<double> Ibuf;             // [B][N] I0 rows + [B][N] I1 rows (host-staged)
+    DevArray<double> Vbuf;             // [B][2N] planar output staging
+};
+
+// per-system scalar slots (Workspace::sysd / sysi)
+enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3 };
+enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_ITERS = 3 };
+constexpr int kSysStride = 8;
+
+}  // namespace mof
+
+// The opaque handle of the C ABI.
+struct mof_mesh {
+    int32_t N = 0, M = 0, device = 0;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    mof::Pattern pat;
+    // device mesh data
+    mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col;
+    mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4]
+    mof::Workspace ws;
+    bool have_last_A = false;
+    double ms_geometry = 0.0, ms_pattern = 0.0;
+    // pinned host mirror of per-system flags
+    int32_t *h_sysi = nullptr;
+    double *h_sysd = nullptr;
+    int32_t h_cap = 0;
+    // HIP event pairs bracketing timed SpMV launches (MOF_TIME_SPMV)
+    std::vector<hipEvent_t> spmv_events;
+};
+
+namespace mof {
+
+// kernels launched from the host side (mof_assemble.hip / mof_pcg.hip)
+void launch_geometry(mof_mesh *m, const double *d_xyz, const double *d_nrm, bool f32_points);
+void launch_a2(mof_mesh *m);
+// assemble B systems: I0 rows / I1 rows are device pointers (row b at +b*ldI)
+void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
+                     double lambda, bool block_jacobi, hipStream_t s);
+void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);
+
+struct SpmvTiming {
+    int64_t launches = 0;
+    double ms = 0.0, bytes = 0.0;
+};
+
+// Algorithmic bytes of one k_pcg_spmv launch over `active` systems:
+// per system the block values, the z gather and q, p read + write; the
+// column indices are shared by all systems.
+double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active);
+
+struct SolveParams {
+    uint32_t precision;
+    bool block_jacobi;
+    bool time_spmv;
+    int32_t max_iter, max_outer;
+    double rtol, inner_rtol;
+};
+// Solve the B assembled systems in the workspace; fills sysd/sysi.
+// Returns total inner iterations; sets *outer to the refinement steps used.
+int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
+                    int32_t *max_iters, SpmvTiming *timing);
+void ensure_workspace(mof_mesh *m, int32_t B);
+double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,
+                  double *bytes);
+
+}  // namespace mof

@@ -1,0 +1,110 @@
+// mof_pattern.cpp -- one-time host build of the block sparsity pattern.
+//
+// The reference discovers the pattern implicitly: it scatters every
+// per-triangle term into a scipy lil_matrix (compute_optical_flow.py:78-93,
+// 127-141). Here the pattern is built once per mesh so that every
+// per-timestep assembly is a deterministic gather (no atomics):
+//  * vptr/vcol   vertex adjacency (self included, sorted): the 2x2 blocks;
+//  * cptr/clist  for each block (i, j) the (triangle, local i, local j)
+//                terms that land on it, in triangle order -- the order in
+//                which the reference's lil "+=" folds them;
+//  * sell_off/sell_col  SELL-64 layout of the blocks for the SpMV.
+#include <algorithm>
+#include <chrono>
+
+#include "mof_internal.h"
+
+namespace mof {
+
+void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
+    MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
+    MOF_REQUIRE((int64_t)M * 9 < (int64_t)INT32_MAX, "too many triangles for int32 term codes");
+    for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+        MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
+    pat.N = N;
+    pat.M = M;
+
+    // incidence counts -> candidate neighbour lists (3 per incident corner)
+    std::vector<int64_t> inc(N + 1, 0);
+    for (int64_t q = 0; q < 3 * (int64_t)M; ++q) inc[tri[q] + 1]++;
+    for (int32_t i = 0; i < N; ++i) inc[i + 1] += inc[i];
+    std::vector<int32_t> cand(3 * inc[N] + N);
+    std::vector<int64_t> cfill(N);
+    std::vector<int64_t> cbase(N + 1);
+    for (int32_t i = 0; i <= N; ++i) cbase[i] = 3 * inc[i] + i;
+    for (int32_t i = 0; i < N; ++i) {
+        cfill[i] = cbase[i];
+        cand[cfill[i]++] = i;  // every vertex keeps its diagonal block
+    }
+    for (int32_t T = 0; T < M; ++T) {
+        const int32_t *v = tri + 3 * (int64_t)T;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                if (a == b) continue;
+                cand[cfill[v[a]]++] = v[b];
+            }
+    }
+    pat.vptr.assign(N + 1, 0);
+    pat.vcol.clear();
+    pat.vcol.reserve(7 * (size_t)N);
+    for (int32_t i = 0; i < N; ++i) {
+        auto b = cand.begin() + cbase[i], e = cand.begin() + cfill[i];
+        std::sort(b, e);
+        e = std::unique(b, e);
+        pat.vcol.insert(pat.vcol.end(), b, e);
+        pat.vptr[i + 1] = (int32_t)pat.vcol.size();
+    }
+    const int32_t nb = (int32_t)pat.vcol.size();
+
+    // contribution lists: term (T, a, b) -> block (v_a, v_b); T ascending
+    auto block_of = [&](int32_t i, int32_t j) -> int32_t {
+        auto b = pat.vcol.begin() + pat.vptr[i], e = pat.vcol.begin() + pat.vptr[i + 1];
+        return (int32_t)(std::lower_bound(b, e, j) - pat.vcol.begin());
+    };
+    pat.cptr.assign(nb + 1, 0);
+    std::vector<int32_t> term_block(9 * (size_t)M);
+    for (int32_t T = 0; T < M; ++T) {
+        const int32_t *v = tri + 3 * (int64_t)T;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                int32_t p = block_of(v[a], v[b]);
+                term_block[9 * (size_t)T + 3 * a + b] = p;
+                pat.cptr[p + 1]++;
+            }
+    }
+    for (int32_t p = 0; p < nb; ++p) pat.cptr[p + 1] += pat.cptr[p];
+    pat.clist.assign(pat.cptr[nb], 0);
+    std::vector<int32_t> fill(pat.cptr.begin(), pat.cptr.end() - 1);
+    for (int32_t T = 0; T < M; ++T)
+        for (int q = 0; q < 9; ++q) {
+            int32_t p = term_block[9 * (size_t)T + q];
+            pat.clist[fill[p]++] = 9 * T + q;
+        }
+
+    // SELL-64
+    pat.nslices = (N + kSlice - 1) / kSlice;
+    pat.sell_off.assign(pat.nslices + 1, 0);
+    for (int32_t s = 0; s < pat.nslices; ++s) {
+        int32_t w = 0;
+        for (int32_t i = s * kSlice; i < std::min(N, (s + 1) * kSlice); ++i)
+            w = std::max(w, pat.vptr[i + 1] - pat.vptr[i]);
+        pat.sell_off[s + 1] = pat.sell_off[s] + w * kSlice;
+    }
+    pat.sell_col.assign(pat.sell_off[pat.nslices], 0);
+    for (int32_t s = 0; s < pat.nslices; ++s) {
+        int32_t w = (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice;
+        for (int32_t l = 0; l < kSlice; ++l) {
+            int32_t i = s * kSlice + l;
+            for (int32_t t = 0; t < w; ++t) {
+                int32_t c = 0;
+                if (i < N) {
+                    int32_t deg = pat.vptr[i + 1] - pat.vptr[i];
+                    c = t < deg ? pat.vcol[pat.vptr[i] + t] : i;
+                }
+                pat.sell_col[pat.sell_off[s] + t * kSlice + l] = c;
+            }
+        }
+    }
+}
+
+}  // namespace mof

@@ -1,0 +1,597 @@
+// mof_pcg.hip -- batched block-Jacobi preconditioned CG on gfx950.
+//
+// Replaces scipy.sparse.linalg.spsolve (compute_optical_flow.py:147) for B
+// timesteps at once: every launch covers all B systems (grid.y = system), so
+// the per-iteration launch cost is shared and the SELL column indices are
+// read once per workgroup for all systems that share the mesh.
+//
+// One CG iteration = two launches:
+//   k_pcg_spmv    w = A z ; q = w + beta q ; p = z + beta p ; partial p.q
+//                 (q = A p without a separate p update: A(z + beta p) =
+//                  A z + beta A p)
+//   k_pcg_update  x += alpha p ; r -= alpha q ; z = D^-1 r ; partial r.z, r.r
+// Scalars (alpha, beta, |r|) are never sent to the host: every workgroup
+// re-reduces the per-workgroup partials of the previous launch in one fixed
+// order, so all workgroups (and every run, on any GPU count) agree bit for
+// bit. Convergence is checked on the device; the host polls a flag word every
+// few iterations.
+//
+// MOF_PREC_MIXED: the inner CG runs on fp32 A and fp32 vectors (dot products
+// in fp64) for the correction d of A d = r64, and an fp64 SpMV refreshes
+// r64 = f - A64 x64 between inner solves (iterative refinement).
+#include <chrono>
+#include <cmath>
+
+#include "mof_internal.h"
+
+namespace mof {
+namespace {
+
+template <typename V>
+struct VT;
+template <>
+struct VT<float> {
+    using V2 = float2;
+};
+template <>
+struct VT<double> {
+    using V2 = double2;
+};
+
+__device__ __forceinline__ void ld_blk(const float *A, int64_t pos, float (&a)[4]) {
+    const float4 v = reinterpret_cast<const float4 *>(A)[pos];
+    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+}
+__device__ __forceinline__ void ld_blk(const double *A, int64_t pos, double (&a)[4]) {
+    const double2 v0 = reinterpret_cast<const double2 *>(A)[2 * pos];
+    const double2 v1 = reinterpret_cast<const double2 *>(A)[2 * pos + 1];
+    a[0] = v0.x; a[1] = v0.y; a[2] = v1.x; a[3] = v1.y;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;  // valid in lane 0
+}
+
+// Deterministic workgroup sum of NV values; every thread gets the result.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = ((lds[k] + lds[NV + k]) + lds[2 * NV + k]) + lds[3 * NV + k];
+    __syncthreads();
+}
+
+// Sum n partials of NV values each (record stride NV) in a fixed order.
+template <int NV>
+__device__ __forceinline__ void reduce_partials(const double *part, int n, double (&out)[NV],
+                                                double *lds) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = 0.0;
+    for (int q = threadIdx.x; q < n; q += kWG) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) out[k] += part[(int64_t)q * NV + k];
+    }
+    block_sum<NV>(out, lds);
+}
+
+template <typename V>
+struct PcgArgs {
+    int32_t N, nblk, B;
+    int64_t sell_nb;
+    const int32_t *sell_off, *sell_col;
+    const V *A;      // [B][sell_nb][4]
+    const V *dinv;   // [B][N][4]
+    V *x, *r, *z, *p, *q;  // [B][N][2]
+    double *part_pq;       // [B][nblk]
+    double *part_rzrr;     // [2][B][nblk][2]
+    double *sysd;          // [B][8]
+    int32_t *sysi;         // [B][8]
+};
+
+// y_i = sum_t A_blk(i,t) x_col(i,t) over the SELL-64 row of vertex i.
+template <typename V, typename X>
+__device__ __forceinline__ void spmv_row(const V *__restrict__ A, const int32_t *__restrict__ col,
+                                         const int32_t *__restrict__ sell_off, int32_t i,
+                                         const X *__restrict__ x, double &y0, double &y1) {
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = sell_off[s];
+    const int32_t w = (sell_off[s + 1] - o) >> 6;
+    X a0 = 0, a1 = 0;
+    for (int32_t t = 0; t < w; ++t) {
+        const int64_t pos = (int64_t)o + t * kSlice + l;
+        const int32_t j = col[pos];
+        V a[4];
+        ld_blk(A, pos, a);
+        const typename VT<X>::V2 xj = *reinterpret_cast<const typename VT<X>::V2 *>(x + 2 * (int64_t)j);
+        a0 += (X)a[0] * xj.x + (X)a[1] * xj.y;
+        a1 += (X)a[2] * xj.x + (X)a[3] * xj.y;
+    }
+    y0 = a0;
+    y1 = a1;
+}
+
+constexpr int kForce = 1;  // bench: ignore convergence / activity flags
+
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__restrict__ rhs) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.y;
+    if (!a.sysi[b * kSysStride + SI_ACTIVE]) return;
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    double rz = 0.0, rr = 0.0;
+    if (i < a.N) {
+        using V2 = typename VT<V>::V2;
+        const int64_t vi = (int64_t)b * a.N + i;
+        const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
+        const V r0 = (V)f.x, r1 = (V)f.y;
+        const V *d = a.dinv + 4 * vi;
+        const V z0 = d[0] * r0 + d[1] * r1, z1 = d[2] * r0 + d[3] * r1;
+        *reinterpret_cast<V2 *>(a.r + 2 * vi) = V2{r0, r1};
+        *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
+        *reinterpret_cast<V2 *>(a.x + 2 * vi) = V2{(V)0, (V)0};
+        rz = (double)r0 * z0 + (double)r1 * z1;
+        rr = (double)r0 * r0 + (double)r1 * r1;
+    }
+    double v[2] = {rz, rr};
+    block_sum<2>(v, lds);
+    if (threadIdx.x == 0) {
+        double *o = a.part_rzrr + 2 * ((int64_t)b * a.nblk + blockIdx.x);  // slot 0
+        o[0] = v[0];
+        o[1] = v[1];
+    }
+}
+
+// One workgroup per system: tolerance from |rhs|^2, reset the convergence word.
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.x;
+    int32_t *si = a.sysi + b * kSysStride;
+    if (!si[SI_ACTIVE]) {
+        if (threadIdx.x == 0) si[SI_CONV] = 0;
+        return;
+    }
+    double v[2];
+    reduce_partials<2>(a.part_rzrr + 2 * (int64_t)b * a.nblk, a.nblk, v, lds);
+    if (threadIdx.x == 0) {
+        a.sysd[b * kSysStride + SD_TOL2] = rtol * rtol * v[1];
+        si[SI_CONV] = -1;
+    }
+}
+
+template <typename V, bool FIRST>
+__global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int32_t flags) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.y;
+    const bool force = flags & kForce;
+    if (!force && !a.sysi[b * kSysStride + SI_ACTIVE]) return;
+    const int64_t ps = (int64_t)a.B * a.nblk * 2;  // slot stride
+    double cur[2];
+    reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
+    if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
+            a.sysi[b * kSysStride + SI_CONV] = it;
+        return;
+    }
+    V beta = 0;
+    if (!FIRST) {
+        double old[2];
+        reduce_partials<2>(a.part_rzrr + ((it + 1) & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, old,
+                           lds);
+        beta = (V)(cur[0] / old[0]);
+    }
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    double pq = 0.0;
+    if (i < a.N) {
+        using V2 = typename VT<V>::V2;
+        const int64_t vb = (int64_t)b * a.N;
+        double y0, y1;
+        spmv_row<V, V>(a.A + 4 * (int64_t)b * a.sell_nb, a.sell_col, a.sell_off, i, a.z + 2 * vb,
+                       y0, y1);
+        const int64_t vi = vb + i;
+        const V2 zi = *reinterpret_cast<const V2 *>(a.z + 2 * vi);
+        V2 qi, pi;
+        if (FIRST) {
+            qi = V2{(V)y0, (V)y1};
+            pi = zi;
+        } else {
+            const V2 q0 = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
+            const V2 p0 = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
+            qi = V2{(V)y0 + beta * q0.x, (V)y1 + beta * q0.y};
+            pi = V2{zi.x + beta * p0.x, zi.y + beta * p0.y};
+        }
+        *reinterpret_cast<V2 *>(a.q + 2 * vi) = qi;
+        *reinterpret_cast<V2 *>(a.p + 2 * vi) = pi;
+        pq = (double)pi.x * qi.x + (double)pi.y * qi.y;
+    }
+    double v[1] = {pq};
+    block_sum<1>(v, lds);
+    if (threadIdx.x == 0) a.part_pq[(int64_t)b * a.nblk + blockIdx.x] = v[0];
+}
+
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.y;
+    int32_t *si = a.sysi + b * kSysStride;
+    if (!si[SI_ACTIVE]) return;
+    const int64_t ps = (int64_t)a.B * a.nblk * 2;
+    double cur[2];
+    reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
+    if (cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) return;
+    double pqv[1];
+    reduce_partials<1>(a.part_pq + (int64_t)b * a.nblk, a.nblk, pqv, lds);
+    if (!(pqv[0] > 0.0) || !isfinite(pqv[0]) || !isfinite(cur[0])) {
+        // breakdown: A (or the preconditioner) is not SPD / singular
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            si[SI_FAILED] = 1;
+            si[SI_ACTIVE] = 0;
+        }
+        return;
+    }
+    const V alpha = (V)(cur[0] / pqv[0]);
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    double rz = 0.0, rr = 0.0;
+    if (i < a.N) {
+        using V2 = typename VT<V>::V2;
+        const int64_t vi = (int64_t)b * a.N + i;
+        const V2 pi = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
+        const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
+        V2 xi = *reinterpret_cast<const V2 *>(a.x + 2 * vi);
+        V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
+        xi.x += alpha * pi.x;
+        xi.y += alpha * pi.y;
+        ri.x -= alpha * qi.x;
+        ri.y -= alpha * qi.y;
+        const V *d = a.dinv + 4 * vi;
+        const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
+        *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
+        *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
+        *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
+        rz = (double)ri.x * z0 + (double)ri.y * z1;
+        rr = (double)ri.x * ri.x + (double)ri.y * ri.y;
+    }
+    double v[2] = {rz, rr};
+    block_sum<2>(v, lds);
+    if (threadIdx.x == 0) {
+        double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * ((int64_t)b * a.nblk + blockIdx.x);
+        o[0] = v[0];
+        o[1] = v[1];
+    }
+}
+
+// x64 (+)= x_inner for systems active in the inner solve.
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
+                                                      const V *__restrict__ xin,
+                                                      const int32_t *__restrict__ sysi,
+                                                      double *__restrict__ x64) {
+    const int32_t b = blockIdx.y;
+    if (!sysi[b * kSysStride + SI_ACTIVE]) return;
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    if (i >= N) return;
+    const int64_t vi = (int64_t)b * N + i;
+    using V2 = typename VT<V>::V2;
+    const V2 d = *reinterpret_cast<const V2 *>(xin + 2 * vi);
+    double2 x = first ? make_double2(0.0, 0.0) : *reinterpret_cast<const double2 *>(x64 + 2 * vi);
+    x.x += (double)d.x;
+    x.y += (double)d.y;
+    *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
+}
+
+// r64 = f - A64 x64 with partial |r|^2 and |f|^2.
+__global__ __launch_bounds__(kWG) void k_residual(int32_t N, int32_t nblk, int64_t sell_nb,
+                                                  const int32_t *__restrict__ sell_off,
+                                                  const int32_t *__restrict__ sell_col,
+                                                  const double *__restrict__ A64,
+                                                  const double *__restrict__ rhs,
+                                                  const double *__restrict__ x64,
+                                                  const int32_t *__restrict__ sysi,
+                                                  double *__restrict__ r64,
+                                                  double *__restrict__ part) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.y;
+    if (!sysi[b * kSysStride + SI_ACTIVE]) return;
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    double rr = 0.0, ff = 0.0;
+    if (i < N) {
+        const int64_t vb = (int64_t)b * N;
+        double y0, y1;
+        spmv_row<double, double>(A64 + 4 * (int64_t)b * sell_nb, sell_col, sell_off, i,
+                                 x64 + 2 * vb, y0, y1);
+        const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
+        const double r0 = f.x - y0, r1 = f.y - y1;
+        *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
+        rr = r0 * r0 + r1 * r1;
+        ff = f.x * f.x + f.y * f.y;
+    }
+    double v[2] = {rr, ff};
+    block_sum<2>(v, lds);
+    if (threadIdx.x == 0) {
+        double *o = part + 2 * ((int64_t)b * nblk + blockIdx.x);
+        o[0] = v[0];
+        o[1] = v[1];
+    }
+}
+
+// One workgroup per system: relative true residual; retire converged systems.
+__global__ __launch_bounds__(kWG) void k_outer_check(int32_t nblk, const double *__restrict__ part,
+                                                     double rtol, double *__restrict__ sysd,
+                                                     int32_t *__restrict__ sysi) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.x;
+    int32_t *si = sysi + b * kSysStride;
+    if (!si[SI_ACTIVE]) return;
+    double v[2];
+    reduce_partials<2>(part + 2 * (int64_t)b * nblk, nblk, v, lds);
+    if (threadIdx.x == 0) {
+        const double rel = v[1] > 0.0 ? sqrt(v[0] / v[1]) : (v[0] > 0.0 ? INFINITY : 0.0);
+        sysd[b * kSysStride + SD_REL] = rel;
+        sysd[b * kSysStride + SD_RR] = v[0];
+        sysd[b * kSysStride + SD_FF] = v[1];
+        if (!isfinite(rel)) {
+            si[SI_FAILED] = 1;
+            si[SI_ACTIVE] = 0;
+        } else if (rel <= rtol) {
+            si[SI_ACTIVE] = 0;
+        }
+    }
+}
+
+__global__ void k_sys_reset(int32_t B, int32_t *__restrict__ sysi, double *__restrict__ sysd) {
+    const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    for (int k = 0; k < kSysStride; ++k) {
+        sysi[b * kSysStride + k] = 0;
+        sysd[b * kSysStride + k] = 0.0;
+    }
+    sysi[b * kSysStride + SI_ACTIVE] = 1;
+    sysi[b * kSysStride + SI_CONV] = -1;
+}
+
+__global__ void k_mark_unconverged(int32_t B, int32_t *__restrict__ sysi) {
+    const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    if (sysi[b * kSysStride + SI_ACTIVE]) {
+        sysi[b * kSysStride + SI_FAILED] = 1;
+        sysi[b * kSysStride + SI_ACTIVE] = 0;
+    }
+}
+
+template <typename V>
+PcgArgs<V> make_args(mof_mesh *m, int32_t B, const V *A, const V *dinv) {
+    Workspace &w = m->ws;
+    PcgArgs<V> a;
+    a.N = m->N;
+    a.nblk = w.nblk;
+    a.B = B;
+    a.sell_nb = m->pat.sell_nb();
+    a.sell_off = m->sell_off.p;
+    a.sell_col = m->sell_col.p;
+    a.A = A;
+    a.dinv = dinv;
+    a.x = reinterpret_cast<V *>(w.vx.p);
+    a.r = reinterpret_cast<V *>(w.vr.p);
+    a.z = reinterpret_cast<V *>(w.vz.p);
+    a.p = reinterpret_cast<V *>(w.vp.p);
+    a.q = reinterpret_cast<V *>(w.vq.p);
+    a.part_pq = w.part_pq.p;
+    a.part_rzrr = w.part_rzrr.p;
+    a.sysd = w.sysd.p;
+    a.sysi = w.sysi.p;
+    return a;
+}
+
+void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
+    MOF_HIP(hipMemcpyAsync(m->h_sysi, m->ws.sysi.p, sizeof(int32_t) * kSysStride * B,
+                           hipMemcpyDeviceToHost, s));
+    MOF_HIP(hipMemcpyAsync(m->h_sysd, m->ws.sysd.p, sizeof(double) * kSysStride * B,
+                           hipMemcpyDeviceToHost, s));
+    MOF_HIP(hipStreamSynchronize(s));
+}
+
+// Inner PCG on all active systems; returns iterations summed over systems.
+template <typename V>
+int64_t pcg(mof_mesh *m, int32_t B, const V *A, const V *dinv, const double *rhs, double rtol,
+            int32_t max_iter, hipStream_t s, int32_t *max_iters, uint32_t precision,
+            SpmvTiming *timing) {
+    PcgArgs<V> a = make_args<V>(m, B, A, dinv);
+    dim3 g((unsigned)m->ws.nblk, (unsigned)B);
+    k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
+    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol);
+    MOF_HIP(hipGetLastError());
+    // systems active at the start of this solve
+    fetch_flags(m, B, s);
+    std::vector<int32_t> was_active(B);
+    for (int32_t b = 0; b < B; ++b) was_active[b] = m->h_sysi[b * kSysStride + SI_ACTIVE];
+    int32_t it = 0;
+    int32_t chunk = 8;
+    bool done = false;
+    int32_t running = 0;
+    for (int32_t b = 0; b < B; ++b) running += was_active[b];
+    std::vector<hipEvent_t> &ev = m->spmv_events;
+    if (timing && ev.empty()) {
+        ev.resize(2 * 64);
+        for (auto &e : ev) MOF_HIP(hipEventCreate(&e));
+    }
+    while (!done && it < max_iter) {
+        const int32_t n = std::min(chunk, max_iter - it);
+        for (int32_t c = 0; c < n; ++c, ++it) {
+            if (timing) MOF_HIP(hipEventRecord(ev[2 * c], s));
+            if (it == 0)
+                k_pcg_spmv<V, true><<<g, kWG, 0, s>>>(a, it, 0);
+            else
+                k_pcg_spmv<V, false><<<g, kWG, 0, s>>>(a, it, 0);
+            if (timing) MOF_HIP(hipEventRecord(ev[2 * c + 1], s));
+            k_pcg_update<V><<<g, kWG, 0, s>>>(a, it);
+        }
+        MOF_HIP(hipGetLastError());
+        fetch_flags(m, B, s);
+        if (timing) {
+            for (int32_t c = 0; c < n; ++c) {
+                float ms = 0.f;
+                MOF_HIP(hipEventElapsedTime(&ms, ev[2 * c], ev[2 * c + 1]));
+                timing->ms += ms;
+            }
+            timing->launches += n;
+            timing->bytes += n * spmv_launch_bytes(m, precision, running);
+        }
+        done = true;
+        running = 0;
+        for (int32_t b = 0; b < B; ++b) {
+            const int32_t *si = m->h_sysi + b * kSysStride;
+            if (si[SI_ACTIVE] && !si[SI_FAILED] && si[SI_CONV] < 0) {
+                done = false;
+                ++running;
+            }
+        }
+        chunk = std::min(chunk * 2, 64);
+    }
+    if (!done) {
+        // one more check launch so SI_CONV records systems converged at max_iter
+        k_pcg_spmv<V, false><<<g, kWG, 0, s>>>(a, it, 0);
+        fetch_flags(m, B, s);
+    }
+    int64_t total = 0;
+    for (int32_t b = 0; b < B; ++b) {
+        if (!was_active[b]) continue;
+        const int32_t c = m->h_sysi[b * kSysStride + SI_CONV];
+        const int32_t its = c >= 0 ? c : it;
+        total += its;
+        *max_iters = std::max(*max_iters, its);
+    }
+    return total;
+}
+
+}  // namespace
+
+double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
+    const double N = m->N, nb = m->pat.nblocks();
+    const double sv = precision == MOF_PREC_MIXED ? 4.0 : 8.0;
+    return active * (nb * 4 * sv + N * 2 * sv * 5) + nb * 4.0;
+}
+
+void ensure_workspace(mof_mesh *m, int32_t B) {
+    Workspace &w = m->ws;
+    if (w.cap >= B) return;
+    const int64_t N = m->N, M = m->M, snb = m->pat.sell_nb();
+    w.cap = B;
+    w.nblk = (int32_t)((N + kWG - 1) / kWG);
+    w.u.alloc(6 * M * B);
+    w.fc.alloc(6 * M * B);
+    w.A64.alloc(4 * snb * B);
+    w.A32.alloc(4 * snb * B);
+    // SELL padding stays zero forever: assembly writes real blocks only
+    w.A64.zero(m->stream);
+    w.A32.zero(m->stream);
+    w.dinv64.alloc(4 * N * B);
+    w.dinv32.alloc(4 * N * B);
+    w.rhs.alloc(2 * N * B);
+    w.x64.alloc(2 * N * B);
+    w.r64.alloc(2 * N * B);
+    w.vx.alloc(2 * N * B);
+    w.vr.alloc(2 * N * B);
+    w.vz.alloc(2 * N * B);
+    w.vp.alloc(2 * N * B);
+    w.vq.alloc(2 * N * B);
+    w.part_pq.alloc((size_t)w.nblk * B);
+    w.part_rzrr.alloc((size_t)4 * w.nblk * B);
+    w.part_rr0.alloc((size_t)2 * w.nblk * B);
+    w.sysd.alloc((size_t)kSysStride * B);
+    w.sysi.alloc((size_t)kSysStride * B);
+    w.dt.alloc(B);
+    w.Ibuf.alloc(2 * N * B);
+    w.Vbuf.alloc(2 * N * B);
+    if (m->h_cap < B) {
+        if (m->h_sysi) (void)hipHostFree(m->h_sysi);
+        if (m->h_sysd) (void)hipHostFree(m->h_sysd);
+        m->h_sysi = nullptr;
+        m->h_sysd = nullptr;
+        MOF_HIP(hipHostMalloc((void **)&m->h_sysi, sizeof(int32_t) * kSysStride * B, 0));
+        MOF_HIP(hipHostMalloc((void **)&m->h_sysd, sizeof(double) * kSysStride * B, 0));
+        m->h_cap = B;
+    }
+    MOF_HIP(hipStreamSynchronize(m->stream));
+}
+
+int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
+                    int32_t *max_iters, SpmvTiming *timing) {
+    SpmvTiming *tm = sp.time_spmv ? timing : nullptr;
+    Workspace &w = m->ws;
+    k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
+    MOF_HIP(hipGetLastError());
+    dim3 g((unsigned)w.nblk, (unsigned)B);
+    int64_t iters = 0;
+    int32_t o = 0;
+    for (; o < sp.max_outer; ++o) {
+        const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
+        if (sp.precision == MOF_PREC_MIXED) {
+            iters += pcg<float>(m, B, w.A32.p, w.dinv32.p, rhs, sp.inner_rtol, sp.max_iter, s,
+                                max_iters, sp.precision, tm);
+            k_outer_update<float><<<g, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
+                                                    w.sysi.p, w.x64.p);
+        } else {
+            iters += pcg<double>(m, B, w.A64.p, w.dinv64.p, rhs, o == 0 ? 0.5 * sp.rtol : sp.inner_rtol,
+                                 sp.max_iter, s, max_iters, sp.precision, tm);
+            k_outer_update<double><<<g, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+        }
+        k_residual<<<g, kWG, 0, s>>>(m->N, w.nblk, m->pat.sell_nb(), m->sell_off.p, m->sell_col.p,
+                                     w.A64.p, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
+        k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(w.nblk, w.part_rr0.p, sp.rtol, w.sysd.p,
+                                                        w.sysi.p);
+        MOF_HIP(hipGetLastError());
+        fetch_flags(m, B, s);
+        bool any = false;
+        for (int32_t b = 0; b < B; ++b) any |= m->h_sysi[b * kSysStride + SI_ACTIVE] != 0;
+        if (!any) {
+            ++o;
+            break;
+        }
+    }
+    k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p);
+    MOF_HIP(hipGetLastError());
+    fetch_flags(m, B, s);
+    *outer = o;
+    return iters;
+}
+
+double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,
+                  double *bytes) {
+    Workspace &w = m->ws;
+    MOF_REQUIRE(B >= 1 && B <= w.cap, "bench batch exceeds the workspace of the last solve");
+    dim3 g((unsigned)w.nblk, (unsigned)B);
+    hipEvent_t e0, e1;
+    MOF_HIP(hipEventCreate(&e0));
+    MOF_HIP(hipEventCreate(&e1));
+    *bytes = spmv_launch_bytes(m, precision, B);
+    auto launch = [&]() {
+        if (precision == MOF_PREC_MIXED) {
+            PcgArgs<float> a = make_args<float>(m, B, w.A32.p, w.dinv32.p);
+            k_pcg_spmv<float, false><<<g, kWG, 0, s>>>(a, 1, kForce);
+        } else {
+            PcgArgs<double> a = make_args<double>(m, B, w.A64.p, w.dinv64.p);
+            k_pcg_spmv<double, false><<<g, kWG, 0, s>>>(a, 1, kForce);
+        }
+    };
+    for (int r = 0; r < 3; ++r) launch();
+    MOF_HIP(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch();
+    MOF_HIP(hipEventRecord(e1, s));
+    MOF_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    MOF_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ms / reps;
+}
+
+}  // namespace mof

@@ -1,0 +1,44 @@
+"""Test configuration: paths, markers, golden fixtures.
+
+`-m "not gpu"`: oracle vs golden vectors, host logic, C-ABI load/exports.
+`-m gpu`: parity of the HIP path (through the C ABI) against the oracle and
+the golden vectors captured from the reference.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "manifold-based-optical-flow-method_amd")
+for p in (PKG, os.path.join(REPO, "oracle"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN_DIR = os.path.join(REPO, "tests", "golden")
+GOLDEN_CASES = ["G1_ico642", "G2_cap641", "G3_ico642_f32", "G4_pool2", "G5_dt512"]
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: larger meshes (seconds to a minute)")
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(params=GOLDEN_CASES)
+def golden(request):
+    g = load_golden(request.param)
+    g["name"] = request.param
+    return g
+
+
+def golden_csr(g, prefix):
+    import scipy.sparse as sp
+    n = len(g[prefix + "_indptr"]) - 1
+    return sp.csr_matrix((g[prefix + "_data"], g[prefix + "_indices"], g[prefix + "_indptr"]),
+                         shape=(n, n))
