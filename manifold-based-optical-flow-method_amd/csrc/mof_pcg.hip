@@ -173,7 +173,10 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
     __shared__ double lds[8];
     const int32_t b = blockIdx.y;
     const bool force = flags & kForce;
-    if (!force && !a.sysi[b * kSysStride + SI_ACTIVE]) return;
+    // retired systems: inactive, or converged in an earlier iteration (the
+    // word is sticky, so no later launch re-reads a stale partial slot)
+    if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || a.sysi[b * kSysStride + SI_CONV] >= 0))
+        return;
     const int64_t ps = (int64_t)a.B * a.nblk * 2;  // slot stride
     double cur[2];
     reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     __shared__ double lds[8];
     const int32_t b = blockIdx.y;
     int32_t *si = a.sysi + b * kSysStride;
-    if (!si[SI_ACTIVE]) return;
+    if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
     const int64_t ps = (int64_t)a.B * a.nblk * 2;
     double cur[2];
     reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
