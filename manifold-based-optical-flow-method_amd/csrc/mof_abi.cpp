@@ -141,6 +141,10 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
             m->sell_off.upload(P.sell_off.data(), P.sell_off.size(), s);
             m->sell_col.alloc(P.sell_col.size());
             m->sell_col.upload(P.sell_col.data(), P.sell_col.size(), s);
+            m->sell_blk.alloc(P.sell_blk.size());
+            m->sell_blk.upload(P.sell_blk.data(), P.sell_blk.size(), s);
+            m->blk_row.alloc(P.blk_row.size());
+            m->blk_row.upload(P.blk_row.data(), P.blk_row.size(), s);
             mof::DevArray<double> dxyz, dnrm;
             dxyz.alloc(3 * (size_t)N);
             dxyz.upload(xyz, 3 * (size_t)N, s);

@@ -214,65 +214,65 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
     }
 }
 
-// Per-vertex half of worker (:127-146) for B systems: block (i, j) of
-// a1 = fold over its terms of (u_a^alpha u_b^beta) integral, then
-// A = a1 + lambda*a2 (fp64 and a rounded fp32 copy, SELL layout); the
-// diagonal block's terms also fold f_i and give the 2x2 block-Jacobi inverse.
-__global__ __launch_bounds__(kWG) void k_assemble_rows(
-    int32_t N, int32_t M, int64_t sell_nb, const int32_t *__restrict__ vptr,
-    const int32_t *__restrict__ vcol, const int32_t *__restrict__ cptr,
-    const int32_t *__restrict__ clist, const int32_t *__restrict__ sell_off,
+// Per-block half of worker (:127-146) for B systems, one SELL position per
+// thread (coalesced stores): block (i, j) of a1 = fold over its terms of
+// (u_a^alpha u_b^beta) integral, in triangle order, then A = a1 + lambda*a2
+// (fp64 and a rounded fp32 copy). The thread holding a diagonal block also
+// folds f_i and writes the 2x2 block-Jacobi inverse of vertex i.
+__global__ __launch_bounds__(kWG) void k_assemble_sell(
+    int64_t sell_nb, int32_t N, int32_t M, const int32_t *__restrict__ sell_blk,
+    const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
+    const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
     const double *__restrict__ iw, const double *__restrict__ a2, const double *__restrict__ u,
     const double *__restrict__ fc, double lambda, int block_jacobi, double *__restrict__ A64,
     float *__restrict__ A32, double *__restrict__ dinv64, float *__restrict__ dinv32,
     double *__restrict__ rhs) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
     const int32_t b = blockIdx.y;
-    if (i >= N) return;
+    if (pos >= sell_nb) return;
+    const int32_t p = sell_blk[pos];
+    if (p < 0) return;  // SELL padding stays zero
+    const int32_t i = blk_row[p], j = vcol[p];
+    const bool diag = (j == i);
     const double *ub = u + 6 * (int64_t)b * M;
     const double *fb = fc + 6 * (int64_t)b * M;
     double f0 = 0.0, f1 = 0.0;
-    double D[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int32_t p = vptr[i], t = 0; p < vptr[i + 1]; ++p, ++t) {
-        const int32_t j = vcol[p];
-        const bool diag = (j == i);
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
-            const int32_t code = clist[c];
-            const int32_t T = code / 9, a = (code % 9) / 3, bb = code % 3;
-            const double ua0 = ub[6 * (int64_t)T + 2 * a], ua1 = ub[6 * (int64_t)T + 2 * a + 1];
-            const double ub0 = ub[6 * (int64_t)T + 2 * bb], ub1 = ub[6 * (int64_t)T + 2 * bb + 1];
-            const double integ = iw[2 * (int64_t)T + (diag ? 0 : 1)];
-            acc[0] += ua0 * ub0 * integ;
-            acc[1] += ua0 * ub1 * integ;
-            acc[2] += ua1 * ub0 * integ;
-            acc[3] += ua1 * ub1 * integ;
-            if (diag && a == bb) {
-                f0 += fb[6 * (int64_t)T + 2 * a];
-                f1 += fb[6 * (int64_t)T + 2 * a + 1];
-            }
-        }
-        const int64_t pos = sell_pos(sell_off, i, t);
-        const double *s2 = a2 + 4 * pos;
-        double Av[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Av[q] = acc[q] + lambda * s2[q];
-        double *o64 = A64 + 4 * ((int64_t)b * sell_nb + pos);
-        *reinterpret_cast<double2 *>(o64) = make_double2(Av[0], Av[1]);
-        *reinterpret_cast<double2 *>(o64 + 2) = make_double2(Av[2], Av[3]);
-        *reinterpret_cast<float4 *>(A32 + 4 * ((int64_t)b * sell_nb + pos)) =
-            make_float4((float)Av[0], (float)Av[1], (float)Av[2], (float)Av[3]);
-        if (diag) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) D[q] = Av[q];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
+        const int32_t code = clist[c];
+        const int32_t T = code / 9, a = (code % 9) / 3, bb = code % 3;
+        const double2 ua = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)T + 2 * a);
+        const double2 uv = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)T + 2 * bb);
+        const double integ = iw[2 * (int64_t)T + (diag ? 0 : 1)];
+        acc[0] += ua.x * uv.x * integ;
+        acc[1] += ua.x * uv.y * integ;
+        acc[2] += ua.y * uv.x * integ;
+        acc[3] += ua.y * uv.y * integ;
+        if (diag && a == bb) {
+            const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)T + 2 * a);
+            f0 += fv.x;
+            f1 += fv.y;
         }
     }
+    const double2 s01 = *reinterpret_cast<const double2 *>(a2 + 4 * pos);
+    const double2 s23 = *reinterpret_cast<const double2 *>(a2 + 4 * pos + 2);
+    double Av[4];
+    Av[0] = acc[0] + lambda * s01.x;
+    Av[1] = acc[1] + lambda * s01.y;
+    Av[2] = acc[2] + lambda * s23.x;
+    Av[3] = acc[3] + lambda * s23.y;
+    double *o64 = A64 + 4 * ((int64_t)b * sell_nb + pos);
+    *reinterpret_cast<double2 *>(o64) = make_double2(Av[0], Av[1]);
+    *reinterpret_cast<double2 *>(o64 + 2) = make_double2(Av[2], Av[3]);
+    *reinterpret_cast<float4 *>(A32 + 4 * ((int64_t)b * sell_nb + pos)) =
+        make_float4((float)Av[0], (float)Av[1], (float)Av[2], (float)Av[3]);
+    if (!diag) return;
     double inv[4];
     if (block_jacobi) {
-        const double det = D[0] * D[3] - D[1] * D[2];
-        inv[0] = D[3] / det; inv[1] = -D[1] / det; inv[2] = -D[2] / det; inv[3] = D[0] / det;
+        const double det = Av[0] * Av[3] - Av[1] * Av[2];
+        inv[0] = Av[3] / det; inv[1] = -Av[1] / det; inv[2] = -Av[2] / det; inv[3] = Av[0] / det;
     } else {
-        inv[0] = 1.0 / D[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / D[3];
+        inv[0] = 1.0 / Av[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / Av[3];
     }
     const int64_t vi = (int64_t)b * N + i;
     *reinterpret_cast<double2 *>(dinv64 + 4 * vi) = make_double2(inv[0], inv[1]);
@@ -322,11 +322,12 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), (unsigned)B);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
                                   w.u.p, w.fc.p);
-    dim3 gr((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
-    k_assemble_rows<<<gr, kWG, 0, s>>>(m->N, m->M, m->pat.sell_nb(), m->vptr.p, m->vcol.p,
-                                       m->cptr.p, m->clist.p, m->sell_off.p, m->iw.p, m->a2.p,
-                                       w.u.p, w.fc.p, lambda, block_jacobi ? 1 : 0, w.A64.p,
-                                       w.A32.p, w.dinv64.p, w.dinv32.p, w.rhs.p);
+    const int64_t snb = m->pat.sell_nb();
+    dim3 gr((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
+    k_assemble_sell<<<gr, kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p, m->vcol.p,
+                                       m->cptr.p, m->clist.p, m->iw.p, m->a2.p, w.u.p, w.fc.p,
+                                       lambda, block_jacobi ? 1 : 0, w.A64.p, w.A32.p, w.dinv64.p,
+                                       w.dinv32.p, w.rhs.p);
     MOF_HIP(hipGetLastError());
 }
 

@@ -75,6 +75,8 @@ struct Pattern {
     int32_t nslices = 0;
     std::vector<int32_t> sell_off;     // (nslices+1), in blocks (multiples of 64)
     std::vector<int32_t> sell_col;     // (sell_off[nslices]) column vertex, padding -> row itself
+    std::vector<int32_t> sell_blk;     // (sell_nb) block index at a SELL position, -1 = padding
+    std::vector<int32_t> blk_row;      // (nblocks) row vertex of each block
     int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
     int32_t nblocks() const { return (int32_t)vcol.size(); }
 };
@@ -117,7 +119,7 @@ struct mof_mesh {
     hipStream_t stream = nullptr;
     mof::Pattern pat;
     // device mesh data
-    mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col;
+    mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row;
     mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4]
     mof::Workspace ws;
     bool have_last_A = false;

@@ -91,17 +91,23 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
         pat.sell_off[s + 1] = pat.sell_off[s] + w * kSlice;
     }
     pat.sell_col.assign(pat.sell_off[pat.nslices], 0);
+    pat.sell_blk.assign(pat.sell_off[pat.nslices], -1);
+    pat.blk_row.assign(nb, 0);
+    for (int32_t i = 0; i < N; ++i)
+        for (int32_t q = pat.vptr[i]; q < pat.vptr[i + 1]; ++q) pat.blk_row[q] = i;
     for (int32_t s = 0; s < pat.nslices; ++s) {
         int32_t w = (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice;
         for (int32_t l = 0; l < kSlice; ++l) {
             int32_t i = s * kSlice + l;
             for (int32_t t = 0; t < w; ++t) {
                 int32_t c = 0;
+                const int64_t pos = pat.sell_off[s] + (int64_t)t * kSlice + l;
                 if (i < N) {
                     int32_t deg = pat.vptr[i + 1] - pat.vptr[i];
                     c = t < deg ? pat.vcol[pat.vptr[i] + t] : i;
+                    if (t < deg) pat.sell_blk[pos] = pat.vptr[i] + t;
                 }
-                pat.sell_col[pat.sell_off[s] + t * kSlice + l] = c;
+                pat.sell_col[pos] = c;
             }
         }
     }
