@@ -88,9 +88,8 @@ def cpu_baseline(p, t, n, a, lam, frac):
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from mofhip.dist import max_over_ranks, rank_env, rank_k_range, sum_over_ranks
+    rank, world, local = rank_env()
     precision = args.precision or ("f64" if args.config == "C2" else "mixed")
 
     import torch
@@ -114,7 +113,7 @@ def main():
     B = args.batch
     steps_total = args.warmup + args.steps
     K_rank = steps_total * B
-    k_off = rank * K_rank
+    k_off, _ = rank_k_range(rank, world, 0, world * K_rank)  # this rank's timesteps
     I_host = np.sin(3.0 * np.arctan2(p[:, 1], p[:, 0])[None, :]
                     - 0.3 * (k_off + np.arange(K_rank + 1, dtype=np.float64))[:, None])
     dev = torch.device("cuda", local)
@@ -147,13 +146,8 @@ def main():
         agg["max_rel_residual"] = max(agg["max_rel_residual"], st["max_rel_residual"])
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        ff = torch.tensor([agg["failed"]], dtype=torch.float64, device=dev)
-        dist.all_reduce(ff)
-        agg["failed"] = int(ff.item())
+    elapsed = max_over_ranks(elapsed, dist, dev)
+    agg["failed"] = int(sum_over_ranks(agg["failed"], dist, dev))
     n_ts = world * args.steps * B
     value = n_ts / elapsed
 

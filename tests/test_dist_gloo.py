@@ -1,0 +1,82 @@
+"""N > 1 path on CPU: world_size-2 gloo process group.
+
+Each rank solves its contiguous k-shard (the partition bench.py and
+compute_velocity_field use) with the oracle; the gathered result equals the
+serial solve bit for bit, and the timing reduction returns the max."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path.insert(0, os.path.join(repo, "manifold-based-optical-flow-method_amd"))
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    sys.path.insert(0, here)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle
+    from conftest import load_golden
+    from mofhip.dist import max_over_ranks, rank_env, rank_k_range
+    r, w, lr = rank_env()
+    assert (r, w, lr) == (rank, world, rank)
+    g = load_golden("G1_ico642")
+    a2, gw, e, iw = oracle.geometry(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+    K = len(g["I"]) - 1
+    a, b = rank_k_range(rank, world, 0, K)
+    V = np.stack([oracle.worker(k, a2, gw, e, iw, g["triangles"], list(g["t_k"]), g["areas"],
+                                float(g["lambda_"]), g["I"][k], g["I"][k + 1]) for k in range(a, b)])
+    parts = [None] * world
+    dist.all_gather_object(parts, (a, b, V))
+    m = max_over_ranks(float(rank + 1), dist)
+    if rank == 0:
+        out.put((parts, m))
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_match_serial():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts, m = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from conftest import load_golden
+    g = load_golden("G1_ico642")
+    ranges = [(a, b) for a, b, _ in parts]
+    assert ranges[0][0] == 0 and ranges[-1][1] == len(g["I"]) - 1
+    assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+    V = np.concatenate([v for _, _, v in parts])
+    assert np.array_equal(V, g["V_k"])  # oracle == reference bit for bit
+    assert m == 2.0
+
+
+def test_shard_ranges_cover():
+    from mofhip.solve import shard_ranges
+    for n, p in [(0, 3), (1, 4), (15, 2), (15, 8), (1000, 8), (7, 7)]:
+        r = shard_ranges(0, n, p)
+        assert len(r) == p and r[0][0] == 0 and r[-1][1] == n
+        assert all(r[i][1] == r[i + 1][0] for i in range(p - 1))
+        sizes = [b - a for a, b in r]
+        assert max(sizes) - min(sizes) <= 1
