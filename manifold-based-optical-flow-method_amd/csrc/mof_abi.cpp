@@ -145,6 +145,12 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
             m->sell_blk.upload(P.sell_blk.data(), P.sell_blk.size(), s);
             m->blk_row.alloc(P.blk_row.size());
             m->blk_row.upload(P.blk_row.data(), P.blk_row.size(), s);
+            m->diag_pos.alloc(P.diag_pos.size());
+            m->diag_pos.upload(P.diag_pos.data(), P.diag_pos.size(), s);
+            m->tsell_off.alloc(P.tsell_off.size());
+            m->tsell_off.upload(P.tsell_off.data(), P.tsell_off.size(), s);
+            m->tinc.alloc(P.tinc.size());
+            m->tinc.upload(P.tinc.data(), P.tinc.size(), s);
             mof::DevArray<double> dxyz, dnrm;
             dxyz.alloc(3 * (size_t)N);
             dxyz.upload(xyz, 3 * (size_t)N, s);
@@ -155,6 +161,13 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
             m->iw.alloc(2 * (size_t)M);
             m->a2.alloc(4 * (size_t)P.sell_nb());
             m->a2.zero(s);
+            m->a2s64.alloc(4 * (size_t)P.sell_nb());
+            m->a2s32.alloc(4 * (size_t)P.sell_nb());
+            m->w12_64.alloc((size_t)M + 1);
+            m->w12_32.alloc((size_t)M + 1);
+            m->Aexp.alloc(4 * (size_t)P.sell_nb());
+            m->Aexp.zero(s);
+            m->fexp.alloc(2 * (size_t)N);
             Events ev;
             MOF_HIP(hipEventRecord(ev.e[0], s));
             mof::launch_geometry(m, dxyz.p, dnrm.p, (flags & MOF_GEOM_F32_POINTS) != 0);
@@ -223,7 +236,7 @@ int mof_csr_export(mof_mesh *m, int32_t which, int32_t drop_zeros, int32_t *indp
         const double *src = m->a2.p;
         if (which == MOF_CSR_A_LAST) {
             if (!m->have_last_A) throw mof::Error{MOF_E_STATE, "no assembled system: call mof_assemble first"};
-            src = m->ws.A64.p;
+            src = m->Aexp.p;
         }
         MOF_HIP(hipMemcpyAsync(blk.data(), src, sizeof(double) * blk.size(), hipMemcpyDeviceToHost,
                                m->stream));
@@ -238,23 +251,16 @@ int mof_assemble(mof_mesh *m, const double *I0, const double *I1, double dt, dou
         MOF_REQUIRE(m && I0 && I1, "NULL argument");
         DeviceGuard dg(m->device);
         hipStream_t s = m->stream;
-        mof::ensure_workspace(m, 1);
+        mof::ensure_workspace(m, 1, MOF_PREC_MIXED);
         mof::Workspace &w = m->ws;
         const int64_t N = m->N;
         MOF_HIP(hipMemcpyAsync(w.Ibuf.p, I0, sizeof(double) * N, hipMemcpyHostToDevice, s));
         MOF_HIP(hipMemcpyAsync(w.Ibuf.p + N, I1, sizeof(double) * N, hipMemcpyHostToDevice, s));
         MOF_HIP(hipMemcpyAsync(w.dt.p, &dt, sizeof(double), hipMemcpyHostToDevice, s));
-        mof::launch_assemble(m, 1, w.Ibuf.p, w.Ibuf.p + N, N, lambda, true, s);
+        mof::launch_assemble_export(m, w.Ibuf.p, w.Ibuf.p + N, lambda, s);
         m->have_last_A = true;
-        if (f) {
-            std::vector<double> fi(2 * N);
-            MOF_HIP(hipMemcpyAsync(fi.data(), w.rhs.p, sizeof(double) * 2 * N, hipMemcpyDeviceToHost, s));
-            MOF_HIP(hipStreamSynchronize(s));
-            for (int64_t i = 0; i < N; ++i) {
-                f[i] = fi[2 * i];
-                f[N + i] = fi[2 * i + 1];
-            }
-        }
+        if (f)
+            MOF_HIP(hipMemcpyAsync(f, m->fexp.p, sizeof(double) * 2 * N, hipMemcpyDeviceToHost, s));
         MOF_HIP(hipStreamSynchronize(s));
     });
 }
@@ -291,10 +297,11 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         if (K > 0) {
             const int32_t Bmax = o.batch > 0 ? o.batch : 16;
             const int32_t B = std::min(K, Bmax);
-            mof::ensure_workspace(m, B);
+            mof::ensure_workspace(m, B, sp.precision);
             mof::Workspace &w = m->ws;
             const int64_t N = m->N;
             Events ev;
+            mof::prepare_operator(m, lambda, s);
             std::vector<double> dts(B);
             for (int32_t k = k0; k < k1; k += B) {
                 const int32_t nb = std::min(B, k1 - k);
@@ -313,7 +320,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                     I1p = w.Ibuf.p + N * B;
                 }
                 MOF_HIP(hipEventRecord(ev.e[0], s));
-                mof::launch_assemble(m, nb, I0p, I1p, N, lambda, sp.block_jacobi, s);
+                mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s);
                 MOF_HIP(hipEventRecord(ev.e[1], s));
                 int32_t outer = 0;
                 st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
@@ -334,7 +341,6 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 }
                 st.batches++;
             }
-            m->have_last_A = false;  // slot 0 no longer holds a mof_assemble result
         }
         st.systems = K;
         st.spmv_launches = timing.launches;

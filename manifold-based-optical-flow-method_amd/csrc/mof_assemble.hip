@@ -166,6 +166,7 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
 // Per-triangle half of worker (:113-126, compute_f :288-311) for B systems:
 // grad_M I and, for each corner a and alpha, u = grad_M I . e_a^alpha and the
 // f term (u (2 dI_a + sum of the other distinct corners' dI) A_T) / 12.
+// Triangle slot M of u / fc stays zero (padding of the incidence lists).
 __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__restrict__ tri,
                                                   const double *__restrict__ gw,
                                                   const double *__restrict__ e,
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
                                                   const double *__restrict__ I0,
                                                   const double *__restrict__ I1, int64_t ldI,
                                                   const double *__restrict__ dt,
-                                                  double *__restrict__ u,
+                                                  double *__restrict__ u, float *__restrict__ u32,
                                                   double *__restrict__ fc) {
     const int32_t T = blockIdx.x * kWG + threadIdx.x;
     const int32_t b = blockIdx.y;
@@ -189,7 +190,8 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
     const double h = dt[b];
     const double pd[3] = {(i1[v[0]] - a0) / h, (i1[v[1]] - a1) / h, (i1[v[2]] - a2) / h};
     const double A = area[T];
-    const int64_t base = 6 * ((int64_t)b * M + T);
+    const int64_t base = 6 * ((int64_t)b * (M + 1) + T);
+    double uo[6], fo[6];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         // set(T) - {i}: distinct corners other than vertex v[a], in corner order
@@ -208,35 +210,85 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
 #pragma unroll
         for (int al = 0; al < 2; ++al) {
             const double uu = dot64(gI, ea + 3 * al);
-            u[base + 2 * a + al] = uu;
-            fc[base + 2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
+            uo[2 * a + al] = uu;
+            fo[2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
         }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q += 2) {
+        *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
+        *reinterpret_cast<double2 *>(fc + base + q) = make_double2(fo[q], fo[q + 1]);
+        *reinterpret_cast<float2 *>(u32 + base + q) = make_float2((float)uo[q], (float)uo[q + 1]);
     }
 }
 
-// Per-block half of worker (:127-146) for B systems, one SELL position per
-// thread (coalesced stores): block (i, j) of a1 = fold over its terms of
-// (u_a^alpha u_b^beta) integral, in triangle order, then A = a1 + lambda*a2
-// (fp64 and a rounded fp32 copy). The thread holding a diagonal block also
-// folds f_i and writes the 2x2 block-Jacobi inverse of vertex i.
-__global__ __launch_bounds__(kWG) void k_assemble_sell(
-    int64_t sell_nb, int32_t N, int32_t M, const int32_t *__restrict__ sell_blk,
+// Per-vertex terms of B systems on the solve path: f_i folded over the
+// incident triangles in triangle order (bit-identical to the reference's
+// f), the diagonal block D_i = lambda a2_ii + sum_T u_a u_a^T A_T/6 and its
+// 2x2 block-Jacobi inverse.
+__global__ __launch_bounds__(kWG) void k_vertex_step(
+    int32_t N, int32_t M, const int32_t *__restrict__ tsell_off, const int4 *__restrict__ tinc,
+    const int32_t *__restrict__ diag_pos, const double *__restrict__ a2s,
+    const double *__restrict__ iw, const double *__restrict__ u, const double *__restrict__ fc,
+    int block_jacobi, double *__restrict__ dinv64, float *__restrict__ dinv32,
+    double *__restrict__ rhs) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= N) return;
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = tsell_off[s], w = (tsell_off[s + 1] - o) >> 6;
+    const double *ub = u + 6 * (int64_t)b * (M + 1);
+    const double *fb = fc + 6 * (int64_t)b * (M + 1);
+    double f0 = 0.0, f1 = 0.0, d00 = 0.0, d01 = 0.0, d10 = 0.0, d11 = 0.0;
+    for (int32_t t = 0; t < w; ++t) {
+        const int4 q = tinc[(int64_t)o + t * kSlice + l];
+        if (q.x >= M) break;  // padding comes last in every row
+        const double2 ua = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)q.x + 2 * q.y);
+        const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)q.x + 2 * q.y);
+        const double c = iw[2 * (int64_t)q.x];
+        f0 += fv.x;
+        f1 += fv.y;
+        d00 += ua.x * ua.x * c;
+        d01 += ua.x * ua.y * c;
+        d10 += ua.y * ua.x * c;
+        d11 += ua.y * ua.y * c;
+    }
+    const double *sd = a2s + 4 * (int64_t)diag_pos[i];
+    const double D[4] = {d00 + sd[0], d01 + sd[1], d10 + sd[2], d11 + sd[3]};
+    double inv[4];
+    if (block_jacobi) {
+        const double det = D[0] * D[3] - D[1] * D[2];
+        inv[0] = D[3] / det; inv[1] = -D[1] / det; inv[2] = -D[2] / det; inv[3] = D[0] / det;
+    } else {
+        inv[0] = 1.0 / D[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / D[3];
+    }
+    const int64_t vi = (int64_t)b * N + i;
+    *reinterpret_cast<double2 *>(dinv64 + 4 * vi) = make_double2(inv[0], inv[1]);
+    *reinterpret_cast<double2 *>(dinv64 + 4 * vi + 2) = make_double2(inv[2], inv[3]);
+    *reinterpret_cast<float4 *>(dinv32 + 4 * vi) =
+        make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+    *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
+}
+
+// Solve-path A_b = a1_b + lambda a2 of B systems, one SELL position per
+// thread (coalesced stores): the a1 block is folded in fp64 over its terms in
+// triangle order exactly as the export path does, then stored in the inner
+// solver's precision (fp32 for MOF_PREC_MIXED, fp64 otherwise). SELL padding
+// is never written and stays zero.
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_assemble_blocks(
+    int64_t sell_nb, int32_t M, const int32_t *__restrict__ sell_blk,
     const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
     const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
-    const double *__restrict__ iw, const double *__restrict__ a2, const double *__restrict__ u,
-    const double *__restrict__ fc, double lambda, int block_jacobi, double *__restrict__ A64,
-    float *__restrict__ A32, double *__restrict__ dinv64, float *__restrict__ dinv32,
-    double *__restrict__ rhs) {
+    const double *__restrict__ iw, const double *__restrict__ a2s, const double *__restrict__ u,
+    V *__restrict__ A) {
     const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
     const int32_t b = blockIdx.y;
     if (pos >= sell_nb) return;
     const int32_t p = sell_blk[pos];
-    if (p < 0) return;  // SELL padding stays zero
-    const int32_t i = blk_row[p], j = vcol[p];
-    const bool diag = (j == i);
-    const double *ub = u + 6 * (int64_t)b * M;
-    const double *fb = fc + 6 * (int64_t)b * M;
-    double f0 = 0.0, f1 = 0.0;
+    if (p < 0) return;
+    const bool diag = (vcol[p] == blk_row[p]);
+    const double *ub = u + 6 * (int64_t)b * (M + 1);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
         const int32_t code = clist[c];
@@ -248,38 +300,86 @@ __global__ __launch_bounds__(kWG) void k_assemble_sell(
         acc[1] += ua.x * uv.y * integ;
         acc[2] += ua.y * uv.x * integ;
         acc[3] += ua.y * uv.y * integ;
+    }
+    const double2 s01 = *reinterpret_cast<const double2 *>(a2s + 4 * pos);
+    const double2 s23 = *reinterpret_cast<const double2 *>(a2s + 4 * pos + 2);
+    const double v0 = acc[0] + s01.x, v1 = acc[1] + s01.y, v2 = acc[2] + s23.x, v3 = acc[3] + s23.y;
+    V *o = A + 4 * ((int64_t)b * sell_nb + pos);
+    if constexpr (sizeof(V) == 4) {
+        *reinterpret_cast<float4 *>(o) = make_float4((float)v0, (float)v1, (float)v2, (float)v3);
+    } else {
+        *reinterpret_cast<double2 *>(o) = make_double2(v0, v1);
+        *reinterpret_cast<double2 *>(o + 2) = make_double2(v2, v3);
+    }
+}
+
+// lambda * a2 for the solve operator (fp64 copy bit-identical to the
+// reference's lambda_ * a2, :144) and its fp32 rounding.
+__global__ __launch_bounds__(kWG) void k_scale_a2(int64_t n, double lambda,
+                                                  const double *__restrict__ a2,
+                                                  double *__restrict__ s64,
+                                                  float *__restrict__ s32) {
+    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (q >= n) return;
+    const double v = lambda * a2[q];
+    s64[q] = v;
+    s32[q] = (float)v;
+}
+
+// A_T / 12 per triangle (= integral_wi_wj[T][1]), slot M = 0.
+__global__ __launch_bounds__(kWG) void k_w12(int32_t M, const double *__restrict__ iw,
+                                             double *__restrict__ w64, float *__restrict__ w32) {
+    const int32_t T = blockIdx.x * kWG + threadIdx.x;
+    if (T > M) return;
+    const double v = T < M ? iw[2 * (int64_t)T + 1] : 0.0;
+    w64[T] = v;
+    w32[T] = (float)v;
+}
+
+// Export path (mof_assemble): the reference's A = a1 + lambda*a2 of one
+// timestep, one SELL position per thread, bit for bit (:127-146): block
+// (i, j) of a1 = fold over its terms of (u_a^alpha u_b^beta) integral in
+// triangle order; the diagonal-block thread also folds f_i.
+__global__ __launch_bounds__(kWG) void k_assemble_export(
+    int64_t sell_nb, int32_t N, int32_t M, const int32_t *__restrict__ sell_blk,
+    const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
+    const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
+    const double *__restrict__ iw, const double *__restrict__ a2, const double *__restrict__ u,
+    const double *__restrict__ fc, double lambda, double *__restrict__ A64,
+    double *__restrict__ f) {
+    const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (pos >= sell_nb) return;
+    const int32_t p = sell_blk[pos];
+    if (p < 0) return;  // SELL padding stays zero
+    const int32_t i = blk_row[p], j = vcol[p];
+    const bool diag = (j == i);
+    double f0 = 0.0, f1 = 0.0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
+        const int32_t code = clist[c];
+        const int32_t T = code / 9, a = (code % 9) / 3, bb = code % 3;
+        const double2 ua = *reinterpret_cast<const double2 *>(u + 6 * (int64_t)T + 2 * a);
+        const double2 uv = *reinterpret_cast<const double2 *>(u + 6 * (int64_t)T + 2 * bb);
+        const double integ = iw[2 * (int64_t)T + (diag ? 0 : 1)];
+        acc[0] += ua.x * uv.x * integ;
+        acc[1] += ua.x * uv.y * integ;
+        acc[2] += ua.y * uv.x * integ;
+        acc[3] += ua.y * uv.y * integ;
         if (diag && a == bb) {
-            const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)T + 2 * a);
+            const double2 fv = *reinterpret_cast<const double2 *>(fc + 6 * (int64_t)T + 2 * a);
             f0 += fv.x;
             f1 += fv.y;
         }
     }
     const double2 s01 = *reinterpret_cast<const double2 *>(a2 + 4 * pos);
     const double2 s23 = *reinterpret_cast<const double2 *>(a2 + 4 * pos + 2);
-    double Av[4];
-    Av[0] = acc[0] + lambda * s01.x;
-    Av[1] = acc[1] + lambda * s01.y;
-    Av[2] = acc[2] + lambda * s23.x;
-    Av[3] = acc[3] + lambda * s23.y;
-    double *o64 = A64 + 4 * ((int64_t)b * sell_nb + pos);
-    *reinterpret_cast<double2 *>(o64) = make_double2(Av[0], Av[1]);
-    *reinterpret_cast<double2 *>(o64 + 2) = make_double2(Av[2], Av[3]);
-    *reinterpret_cast<float4 *>(A32 + 4 * ((int64_t)b * sell_nb + pos)) =
-        make_float4((float)Av[0], (float)Av[1], (float)Av[2], (float)Av[3]);
-    if (!diag) return;
-    double inv[4];
-    if (block_jacobi) {
-        const double det = Av[0] * Av[3] - Av[1] * Av[2];
-        inv[0] = Av[3] / det; inv[1] = -Av[1] / det; inv[2] = -Av[2] / det; inv[3] = Av[0] / det;
-    } else {
-        inv[0] = 1.0 / Av[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / Av[3];
+    double *o64 = A64 + 4 * pos;
+    *reinterpret_cast<double2 *>(o64) = make_double2(acc[0] + lambda * s01.x, acc[1] + lambda * s01.y);
+    *reinterpret_cast<double2 *>(o64 + 2) = make_double2(acc[2] + lambda * s23.x, acc[3] + lambda * s23.y);
+    if (diag) {
+        f[i] = f0;
+        f[N + i] = f1;
     }
-    const int64_t vi = (int64_t)b * N + i;
-    *reinterpret_cast<double2 *>(dinv64 + 4 * vi) = make_double2(inv[0], inv[1]);
-    *reinterpret_cast<double2 *>(dinv64 + 4 * vi + 2) = make_double2(inv[2], inv[3]);
-    *reinterpret_cast<float4 *>(dinv32 + 4 * vi) =
-        make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
-    *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
 }
 
 // x64 (interleaved) -> V (B, 2N) planar; failed systems are NaN-filled.
@@ -307,6 +407,7 @@ void launch_geometry(mof_mesh *m, const double *d_xyz, const double *d_nrm, bool
         k_gradw<true><<<grid1(m->M), kWG, 0, s>>>(d_xyz, m->tri.p, m->area.p, m->M, m->gw.p, m->iw.p);
     else
         k_gradw<false><<<grid1(m->M), kWG, 0, s>>>(d_xyz, m->tri.p, m->area.p, m->M, m->gw.p, m->iw.p);
+    k_w12<<<grid1(m->M + 1), kWG, 0, s>>>(m->M, m->iw.p, m->w12_64.p, m->w12_32.p);
     MOF_HIP(hipGetLastError());
 }
 
@@ -316,18 +417,49 @@ void launch_a2(mof_mesh *m) {
     MOF_HIP(hipGetLastError());
 }
 
+void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
+    if (m->a2s_valid && m->a2s_lambda == lambda) return;
+    const int64_t n = 4 * m->pat.sell_nb();
+    k_scale_a2<<<grid1(n), kWG, 0, s>>>(n, lambda, m->a2.p, m->a2s64.p, m->a2s32.p);
+    MOF_HIP(hipGetLastError());
+    m->a2s_lambda = lambda;
+    m->a2s_valid = true;
+}
+
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
-                     double lambda, bool block_jacobi, hipStream_t s) {
+                     bool block_jacobi, uint32_t precision, hipStream_t s) {
     Workspace &w = m->ws;
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), (unsigned)B);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
-                                  w.u.p, w.fc.p);
+                                  w.u64.p, w.u32.p, w.fc.p);
+    dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
+    k_vertex_step<<<gv, kWG, 0, s>>>(m->N, m->M, m->tsell_off.p,
+                                     reinterpret_cast<const int4 *>(m->tinc.p), m->diag_pos.p,
+                                     m->a2s64.p, m->iw.p, w.u64.p, w.fc.p, block_jacobi ? 1 : 0,
+                                     w.dinv64.p, w.dinv32.p, w.rhs.p);
     const int64_t snb = m->pat.sell_nb();
-    dim3 gr((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
-    k_assemble_sell<<<gr, kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p, m->vcol.p,
-                                       m->cptr.p, m->clist.p, m->iw.p, m->a2.p, w.u.p, w.fc.p,
-                                       lambda, block_jacobi ? 1 : 0, w.A64.p, w.A32.p, w.dinv64.p,
-                                       w.dinv32.p, w.rhs.p);
+    dim3 gb((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
+    if (precision == MOF_PREC_MIXED)
+        k_assemble_blocks<float><<<gb, kWG, 0, s>>>(snb, m->M, m->sell_blk.p, m->blk_row.p, m->vcol.p,
+                                                    m->cptr.p, m->clist.p, m->iw.p, m->a2s64.p,
+                                                    w.u64.p, w.A32.p);
+    else
+        k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->M, m->sell_blk.p, m->blk_row.p,
+                                                     m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
+                                                     m->a2s64.p, w.u64.p, w.A64.p);
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
+                            hipStream_t s) {
+    Workspace &w = m->ws;
+    dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
+    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
+                                  w.u64.p, w.u32.p, w.fc.p);
+    const int64_t snb = m->pat.sell_nb();
+    k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
+                                                 m->vcol.p, m->cptr.p, m->clist.p, m->iw.p, m->a2.p,
+                                                 w.u64.p, w.fc.p, lambda, m->Aexp.p, m->fexp.p);
     MOF_HIP(hipGetLastError());
 }
 

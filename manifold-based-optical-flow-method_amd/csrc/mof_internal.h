@@ -1,12 +1,16 @@
 // mof_internal.h -- shared declarations of libmofhip (MI355X / gfx950).
 //
-// Device data layout (DESIGN.md §Layout):
+// Device data layout (DESIGN.md §3):
 //  * vertex 2x2 blocks: block p = (i, j) of vertex row i holds
 //      {A(i,j), A(i,j+N), A(i+N,j), A(i+N,j+N)}  (planar unknowns of the
-//      reference, compute_optical_flow.py:83-84)
-//  * matrices are stored SELL-64: row i = slice i/64, lane i%64; its t-th
-//    block lives at sell_off[i/64] + 64*t + i%64, so one wave-instruction
-//    reads 64 consecutive blocks (16 B each in fp32, 32 B in fp64);
+//      reference, compute_optical_flow.py:83-84);
+//  * the smoothness matrix a2 is stored SELL-64: row i = slice i/64, lane
+//    i%64; its t-th block lives at sell_off[i/64] + 64*t + i%64, so one
+//    wave-instruction reads 64 consecutive blocks;
+//  * A_b = a1_b + lambda a2 of every system is materialised in the same SELL
+//    layout in the inner solver's precision; the fp64 residual applies a1
+//    per triangle from u_T = (grad_M I . e_a^alpha), 6 values per triangle,
+//    through a SELL-64 vertex -> incident-triangle list (tinc);
 //  * solver vectors are interleaved per vertex: v[2*i + alpha].
 #pragma once
 
@@ -74,10 +78,17 @@ struct Pattern {
     std::vector<int32_t> cptr, clist;  // per block: contributions T*9 + a*3 + b, T ascending
     int32_t nslices = 0;
     std::vector<int32_t> sell_off;     // (nslices+1), in blocks (multiples of 64)
-    std::vector<int32_t> sell_col;     // (sell_off[nslices]) column vertex, padding -> row itself
+    std::vector<int32_t> sell_col;     // (sell_nb) column vertex, padding -> row itself
     std::vector<int32_t> sell_blk;     // (sell_nb) block index at a SELL position, -1 = padding
     std::vector<int32_t> blk_row;      // (nblocks) row vertex of each block
+    std::vector<int32_t> diag_pos;     // (N) SELL position of the diagonal block of row i
+    // vertex -> incident triangles, SELL-64, triangle order; 4 ints per entry:
+    // {T, corner of i in T, vertex of corner a+1, vertex of corner a+2};
+    // padding entries point at the all-zero triangle slot T = M.
+    std::vector<int32_t> tsell_off;    // (nslices+1), in entries
+    std::vector<int32_t> tinc;         // (4 * tsell_nb)
     int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
+    int64_t tsell_nb() const { return tsell_off.empty() ? 0 : tsell_off.back(); }
     int32_t nblocks() const { return (int32_t)vcol.size(); }
 };
 
@@ -87,9 +98,10 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat);
 struct Workspace {
     int32_t cap = 0;        // systems
     int32_t nblk = 0;       // workgroups per system for row kernels
-    DevArray<double> u, fc;            // [B][M][6] per-triangle g.e and f terms
-    DevArray<double> A64;              // [B][sell_nb][4]
-    DevArray<float> A32;               // [B][sell_nb][4]
+    DevArray<double> u64, fc;          // [B][M+1][6] per-triangle u = grad_M I . e, f terms
+    DevArray<float> u32;               // [B][M+1][6] fp32 copy of u
+    DevArray<float> A32;               // [B][sell_nb][4] A_b in fp32 (MOF_PREC_MIXED)
+    DevArray<double> A64;              // [B][sell_nb][4] A_b in fp64 (MOF_PREC_F64), lazily
     DevArray<double> dinv64;           // [B][N][4] 2x2 block-Jacobi inverses
     DevArray<float> dinv32;
     DevArray<double> rhs;              // [B][N][2] f (interleaved)
@@ -119,8 +131,16 @@ struct mof_mesh {
     hipStream_t stream = nullptr;
     mof::Pattern pat;
     // device mesh data
-    mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row;
-    mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4]
+    mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row,
+        diag_pos, tsell_off, tinc;
+    mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4] (unscaled, bit-exact)
+    // operator copies: lambda*a2 (cached per lambda) and A_T/12 with a zero slot M
+    mof::DevArray<double> a2s64, w12_64;
+    mof::DevArray<float> a2s32, w12_32;
+    double a2s_lambda = 0.0;
+    bool a2s_valid = false;
+    // mof_assemble / mof_csr_export(MOF_CSR_A_LAST): one assembled A (SELL) and f
+    mof::DevArray<double> Aexp, fexp;
     mof::Workspace ws;
     bool have_last_A = false;
     double ms_geometry = 0.0, ms_pattern = 0.0;
@@ -137,9 +157,15 @@ namespace mof {
 // kernels launched from the host side (mof_assemble.hip / mof_pcg.hip)
 void launch_geometry(mof_mesh *m, const double *d_xyz, const double *d_nrm, bool f32_points);
 void launch_a2(mof_mesh *m);
-// assemble B systems: I0 rows / I1 rows are device pointers (row b at +b*ldI)
+// lambda * a2 operator copies (cached per lambda)
+void prepare_operator(mof_mesh *m, double lambda, hipStream_t s);
+// per-timestep terms of B systems: u, f, D^-1. I0 / I1 rows are device
+// pointers (row b at +b*ldI).
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
-                     double lambda, bool block_jacobi, hipStream_t s);
+                     bool block_jacobi, uint32_t precision, hipStream_t s);
+// bit-exact A (SELL, fp64) and f of one timestep into m->Aexp / m->fexp
+void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
+                            hipStream_t s);
 void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);
 
 struct SpmvTiming {
@@ -147,9 +173,8 @@ struct SpmvTiming {
     double ms = 0.0, bytes = 0.0;
 };
 
-// Algorithmic bytes of one k_pcg_spmv launch over `active` systems:
-// per system the block values, the z gather and q, p read + write; the
-// column indices are shared by all systems.
+// Algorithmic bytes of one k_pcg_spmv launch over `active` systems
+// (Roofline).
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active);
 
 struct SolveParams {
@@ -163,7 +188,7 @@ struct SolveParams {
 // Returns total inner iterations; sets *outer to the refinement steps used.
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
                     int32_t *max_iters, SpmvTiming *timing);
-void ensure_workspace(mof_mesh *m, int32_t B);
+void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision);
 double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,
                   double *bytes);
 

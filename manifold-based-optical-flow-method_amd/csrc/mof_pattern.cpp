@@ -8,7 +8,9 @@
 //  * cptr/clist  for each block (i, j) the (triangle, local i, local j)
 //                terms that land on it, in triangle order -- the order in
 //                which the reference's lil "+=" folds them;
-//  * sell_off/sell_col  SELL-64 layout of the blocks for the SpMV.
+//  * sell_off/sell_col  SELL-64 layout of the blocks for the SpMV;
+//  * tsell_off/tinc      SELL-64 vertex -> incident-triangle lists, for the
+//                        per-triangle (matrix-free) application of a1.
 #include <algorithm>
 #include <chrono>
 
@@ -109,6 +111,45 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
                 }
                 pat.sell_col[pos] = c;
             }
+        }
+    }
+    pat.diag_pos.assign(N, 0);
+    for (int32_t i = 0; i < N; ++i) {
+        int32_t t = (int32_t)(std::lower_bound(pat.vcol.begin() + pat.vptr[i],
+                                               pat.vcol.begin() + pat.vptr[i + 1], i) -
+                              (pat.vcol.begin() + pat.vptr[i]));
+        pat.diag_pos[i] = pat.sell_off[i / kSlice] + t * kSlice + (i % kSlice);
+    }
+
+    // vertex -> incident (triangle, corner) in triangle order, SELL-64
+    std::vector<int32_t> tdeg(N, 0);
+    for (int64_t q = 0; q < 3 * (int64_t)M; ++q) tdeg[tri[q]]++;
+    pat.tsell_off.assign(pat.nslices + 1, 0);
+    for (int32_t s = 0; s < pat.nslices; ++s) {
+        int32_t w = 0;
+        for (int32_t i = s * kSlice; i < std::min(N, (s + 1) * kSlice); ++i) w = std::max(w, tdeg[i]);
+        pat.tsell_off[s + 1] = pat.tsell_off[s] + w * kSlice;
+    }
+    const int64_t tnb = pat.tsell_off[pat.nslices];
+    pat.tinc.assign(4 * (size_t)tnb, 0);
+    for (int32_t s = 0; s < pat.nslices; ++s) {
+        const int32_t w = (pat.tsell_off[s + 1] - pat.tsell_off[s]) / kSlice;
+        for (int32_t l = 0; l < kSlice; ++l) {
+            const int32_t i = std::min(s * kSlice + l, N - 1);
+            for (int32_t t = 0; t < w; ++t) {  // padding: zero triangle slot M
+                int32_t *q = &pat.tinc[4 * ((int64_t)pat.tsell_off[s] + (int64_t)t * kSlice + l)];
+                q[0] = M; q[1] = 0; q[2] = i; q[3] = i;
+            }
+        }
+    }
+    std::vector<int32_t> tfill(N, 0);
+    for (int32_t T = 0; T < M; ++T) {
+        const int32_t *v = tri + 3 * (int64_t)T;
+        for (int a = 0; a < 3; ++a) {
+            const int32_t i = v[a];
+            const int32_t t = tfill[i]++;
+            int32_t *q = &pat.tinc[4 * ((int64_t)pat.tsell_off[i / kSlice] + (int64_t)t * kSlice + (i % kSlice))];
+            q[0] = T; q[1] = a; q[2] = v[(a + 1) % 3]; q[3] = v[(a + 2) % 3];
         }
     }
 }

@@ -1,9 +1,19 @@
 // mof_pcg.hip -- batched block-Jacobi preconditioned CG on gfx950.
 //
 // Replaces scipy.sparse.linalg.spsolve (compute_optical_flow.py:147) for B
-// timesteps at once: every launch covers all B systems (grid.y = system), so
-// the per-iteration launch cost is shared and the SELL column indices are
-// read once per workgroup for all systems that share the mesh.
+// timesteps at once: every launch covers all B systems, so the per-iteration
+// launch cost is shared. A_b is materialised per system in SELL-64 2x2 blocks
+// (16 B per block in fp32, read with one dwordx4 per lane, 1 KiB per
+// wave-instruction). The SpMV grid is XCD-aware: each XCD owns one
+// contiguous eighth of the vertex rows of every system, so the z gathers of
+// a row block hit rows that the same XCD's L2 already holds.
+//
+// The fp64 residual of the refinement (k_residual) applies A without the
+// materialised blocks: lambda a2 (shared SELL blocks) plus a1 per incident
+// triangle from the 6 values u_T of each triangle (a1 restricted to a
+// triangle is u u^T (x) [A/6 on the diagonal, A/12 off it],
+// compute_optical_flow.py:127-141):
+//   (a1 x)_i = sum_{T ni i} u_{T,i} (A_T/12) (2 s_i + s_j + s_k),  s_v = u_{T,v} . x_v
 //
 // One CG iteration = two launches:
 //   k_pcg_spmv    w = A z ; q = w + beta q ; p = z + beta p ; partial p.q
@@ -19,6 +29,7 @@
 // MOF_PREC_MIXED: the inner CG runs on fp32 A and fp32 vectors (dot products
 // in fp64) for the correction d of A d = r64, and an fp64 SpMV refreshes
 // r64 = f - A64 x64 between inner solves (iterative refinement).
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 
@@ -37,6 +48,14 @@ template <>
 struct VT<double> {
     using V2 = double2;
 };
+
+// Row kernels: a workgroup covers kRows groups of 256 consecutive vertex rows
+// (thread t takes rows base + 256 r + t, so every group stays 4 whole SELL
+// slices and every access stays coalesced). Fewer, larger workgroups keep the
+// per-workgroup partial sums short: each workgroup of the next launch re-reads
+// all nblk partials of its system, nblk = ceil(N / (256 kRows)).
+constexpr int kRows = 4;
+constexpr int kRowsPerWG = kWG * kRows;
 
 __device__ __forceinline__ void ld_blk(const float *A, int64_t pos, float (&a)[4]) {
     const float4 v = reinterpret_cast<const float4 *>(A)[pos];
@@ -76,19 +95,49 @@ __device__ __forceinline__ void reduce_partials(const double *part, int n, doubl
                                                 double *lds) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = 0.0;
-    for (int q = threadIdx.x; q < n; q += kWG) {
+    int q = threadIdx.x;
+    for (; q + 3 * kWG < n; q += 4 * kWG) {  // four independent loads in flight
+        double v[4][NV];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) v[u][k] = part[(int64_t)(q + u * kWG) * NV + k];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) out[k] += v[u][k];
+    }
+    for (; q < n; q += kWG) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) out[k] += part[(int64_t)q * NV + k];
     }
     block_sum<NV>(out, lds);
 }
 
+// The operator of B systems sharing a mesh.
+template <typename V>
+struct OpArgs {
+    int32_t N, M;
+    const int32_t *sell_off, *sell_col;  // a2 blocks, SELL-64
+    const V *a2s;                        // [sell_nb][4] lambda * a2
+    const int32_t *tsell_off;            // vertex -> incident triangles, SELL-64
+    const int4 *tinc;                    // {T, corner, vertex of corner+1, vertex of corner+2}
+    const V *w12;                        // [M+1] A_T / 12 (slot M = 0)
+    const V *u;                          // [B][M+1][6] u_T per system (slot M = 0)
+};
+
+// Materialised A of B systems (inner PCG operator).
+template <typename V>
+struct MatArgs {
+    int64_t sell_nb;
+    const int32_t *sell_off, *sell_col;
+    const V *A;  // [B][sell_nb][4]
+};
+
 template <typename V>
 struct PcgArgs {
     int32_t N, nblk, B;
-    int64_t sell_nb;
-    const int32_t *sell_off, *sell_col;
-    const V *A;      // [B][sell_nb][4]
+    MatArgs<V> mat;
     const V *dinv;   // [B][N][4]
     V *x, *r, *z, *p, *q;  // [B][N][2]
     double *part_pq;       // [B][nblk]
@@ -97,26 +146,117 @@ struct PcgArgs {
     int32_t *sysi;         // [B][8]
 };
 
+template <typename V>
+__device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
+    return *reinterpret_cast<const typename VT<V>::V2 *>(p);
+}
+
 // y_i = sum_t A_blk(i,t) x_col(i,t) over the SELL-64 row of vertex i.
-template <typename V, typename X>
-__device__ __forceinline__ void spmv_row(const V *__restrict__ A, const int32_t *__restrict__ col,
-                                         const int32_t *__restrict__ sell_off, int32_t i,
-                                         const X *__restrict__ x, double &y0, double &y1) {
+// Slots are processed U at a time with every load of a chunk issued before
+// the first use (column indices, then block values, then the x gathers), so
+// a row costs two memory round trips instead of two per slot. Slots past
+// the slice width re-load the last valid slot and are masked out, keeping
+// every load unconditional.
+template <typename V>
+__device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
+                                         const V *__restrict__ x, V &y0, V &y1) {
+    using V2 = typename VT<V>::V2;
+    constexpr int U = sizeof(V) == 4 ? 8 : 4;
+    const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
     const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = sell_off[s];
-    const int32_t w = (sell_off[s + 1] - o) >> 6;
-    X a0 = 0, a1 = 0;
-    for (int32_t t = 0; t < w; ++t) {
-        const int64_t pos = (int64_t)o + t * kSlice + l;
-        const int32_t j = col[pos];
-        V a[4];
-        ld_blk(A, pos, a);
-        const typename VT<X>::V2 xj = *reinterpret_cast<const typename VT<X>::V2 *>(x + 2 * (int64_t)j);
-        a0 += (X)a[0] * xj.x + (X)a[1] * xj.y;
-        a1 += (X)a[2] * xj.x + (X)a[3] * xj.y;
+    const int32_t o = mt.sell_off[s];
+    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    V a0 = 0, a1 = 0;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U];
+        V blk[U][4];
+        V2 xj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = min(t0 + u, w - 1);
+            j[u] = mt.sell_col[(int64_t)o + t * kSlice + l];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = min(t0 + u, w - 1);
+            ld_blk(A, (int64_t)o + t * kSlice + l, blk[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xj[u] = ld2(x + 2 * (int64_t)j[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool on = t0 + u < w;
+            a0 += on ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : (V)0;
+            a1 += on ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : (V)0;
+        }
     }
     y0 = a0;
     y1 = a1;
+}
+
+// y_i = (A_b x)_i for vertex row i of system b without materialised blocks
+// (lambda a2 + per-triangle a1; x = that system's vector).
+template <typename V>
+__device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int32_t i,
+                                          const V *__restrict__ x, double &y0, double &y1) {
+    using V2 = typename VT<V>::V2;
+    const int32_t s = i >> 6, l = i & 63;
+    V a0 = 0, a1 = 0;
+    // lambda a2 x
+    {
+        const int32_t o = op.sell_off[s];
+        const int32_t w = (op.sell_off[s + 1] - o) >> 6;
+        for (int32_t t = 0; t < w; ++t) {
+            const int64_t pos = (int64_t)o + t * kSlice + l;
+            const int32_t j = op.sell_col[pos];
+            V a[4];
+            ld_blk(op.a2s, pos, a);
+            const V2 xj = ld2(x + 2 * (int64_t)j);
+            a0 += a[0] * xj.x + a[1] * xj.y;
+            a1 += a[2] * xj.x + a[3] * xj.y;
+        }
+    }
+    // a1_b x, per incident triangle
+    {
+        const V *ub = op.u + 6 * (int64_t)b * (op.M + 1);
+        const V2 xi = ld2(x + 2 * (int64_t)i);
+        const int32_t o = op.tsell_off[s];
+        const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
+        for (int32_t t = 0; t < w; ++t) {
+            const int4 q = op.tinc[(int64_t)o + t * kSlice + l];
+            const V *uT = ub + 6 * (int64_t)q.x;
+            const V2 P0 = ld2(uT), P1 = ld2(uT + 2), P2 = ld2(uT + 4);
+            const V2 ui = q.y == 0 ? P0 : (q.y == 1 ? P1 : P2);
+            const V2 uj = q.y == 0 ? P1 : (q.y == 1 ? P2 : P0);
+            const V2 uk = q.y == 0 ? P2 : (q.y == 1 ? P0 : P1);
+            const V2 xj = ld2(x + 2 * (int64_t)q.z);
+            const V2 xk = ld2(x + 2 * (int64_t)q.w);
+            const V si = ui.x * xi.x + ui.y * xi.y;
+            const V sj = uj.x * xj.x + uj.y * xj.y;
+            const V sk = uk.x * xk.x + uk.y * xk.y;
+            const V c = op.w12[q.x] * ((si + si) + sj + sk);
+            a0 += ui.x * c;
+            a1 += ui.y * c;
+        }
+    }
+    y0 = a0;
+    y1 = a1;
+}
+
+// XCD-aware workgroup -> (row block, system): workgroups w and w+8 share an
+// XCD (round-robin dispatch; speed only, never correctness). XCD x takes row
+// blocks [x*chunk, (x+1)*chunk) of every system, system by system.
+__device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, int32_t &sys) {
+    const int32_t w = blockIdx.x;
+    const int32_t q = w >> 3;
+    const int32_t chunk = (nblk + 7) >> 3;
+    sys = q / chunk;
+    rb = (w & 7) * chunk + q % chunk;
+    return rb < nblk && sys < B;
+}
+
+inline unsigned xcd_grid(int32_t nblk, int32_t B) {
+    return (unsigned)(8 * B * ((nblk + 7) / 8));
 }
 
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
@@ -126,10 +266,12 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
     __shared__ double lds[8];
     const int32_t b = blockIdx.y;
     if (!a.sysi[b * kSysStride + SI_ACTIVE]) return;
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    using V2 = typename VT<V>::V2;
     double rz = 0.0, rr = 0.0;
-    if (i < a.N) {
-        using V2 = typename VT<V>::V2;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= a.N) break;
         const int64_t vi = (int64_t)b * a.N + i;
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
         const V r0 = (V)f.x, r1 = (V)f.y;
@@ -138,8 +280,8 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = V2{r0, r1};
         *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = V2{(V)0, (V)0};
-        rz = (double)r0 * z0 + (double)r1 * z1;
-        rr = (double)r0 * r0 + (double)r1 * r1;
+        rz += (double)r0 * z0 + (double)r1 * z1;
+        rr += (double)r0 * r0 + (double)r1 * r1;
     }
     double v[2] = {rz, rr};
     block_sum<2>(v, lds);
@@ -171,7 +313,8 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol) {
 template <typename V, bool FIRST>
 __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int32_t flags) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.y;
+    int32_t rb, b;
+    if (!xcd_map(a.nblk, a.B, rb, b)) return;
     const bool force = flags & kForce;
     // retired systems: inactive, or converged in an earlier iteration (the
     // word is sticky, so no later launch re-reads a stale partial slot)
@@ -181,7 +324,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
     double cur[2];
     reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
     if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
-        if (blockIdx.x == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
+        if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
             a.sysi[b * kSysStride + SI_CONV] = it;
         return;
     }
@@ -192,33 +335,34 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
                            lds);
         beta = (V)(cur[0] / old[0]);
     }
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    using V2 = typename VT<V>::V2;
+    const int64_t vb = (int64_t)b * a.N;
     double pq = 0.0;
-    if (i < a.N) {
-        using V2 = typename VT<V>::V2;
-        const int64_t vb = (int64_t)b * a.N;
-        double y0, y1;
-        spmv_row<V, V>(a.A + 4 * (int64_t)b * a.sell_nb, a.sell_col, a.sell_off, i, a.z + 2 * vb,
-                       y0, y1);
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= a.N) break;
+        V y0, y1;
+        spmv_row<V>(a.mat, b, i, a.z + 2 * vb, y0, y1);
         const int64_t vi = vb + i;
         const V2 zi = *reinterpret_cast<const V2 *>(a.z + 2 * vi);
         V2 qi, pi;
         if (FIRST) {
-            qi = V2{(V)y0, (V)y1};
+            qi = V2{y0, y1};
             pi = zi;
         } else {
             const V2 q0 = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
             const V2 p0 = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
-            qi = V2{(V)y0 + beta * q0.x, (V)y1 + beta * q0.y};
+            qi = V2{y0 + beta * q0.x, y1 + beta * q0.y};
             pi = V2{zi.x + beta * p0.x, zi.y + beta * p0.y};
         }
         *reinterpret_cast<V2 *>(a.q + 2 * vi) = qi;
         *reinterpret_cast<V2 *>(a.p + 2 * vi) = pi;
-        pq = (double)pi.x * qi.x + (double)pi.y * qi.y;
+        pq += (double)pi.x * qi.x + (double)pi.y * qi.y;
     }
     double v[1] = {pq};
     block_sum<1>(v, lds);
-    if (threadIdx.x == 0) a.part_pq[(int64_t)b * a.nblk + blockIdx.x] = v[0];
+    if (threadIdx.x == 0) a.part_pq[(int64_t)b * a.nblk + rb] = v[0];
 }
 
 template <typename V>
@@ -242,26 +386,29 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
         return;
     }
     const V alpha = (V)(cur[0] / pqv[0]);
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    using V2 = typename VT<V>::V2;
     double rz = 0.0, rr = 0.0;
-    if (i < a.N) {
-        using V2 = typename VT<V>::V2;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= a.N) break;
         const int64_t vi = (int64_t)b * a.N + i;
         const V2 pi = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
         const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
         V2 xi = *reinterpret_cast<const V2 *>(a.x + 2 * vi);
         V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
+        V d[4];
+        ld_blk(a.dinv, vi, d);
         xi.x += alpha * pi.x;
         xi.y += alpha * pi.y;
         ri.x -= alpha * qi.x;
         ri.y -= alpha * qi.y;
-        const V *d = a.dinv + 4 * vi;
         const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
         *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
-        rz = (double)ri.x * z0 + (double)ri.y * z1;
-        rr = (double)ri.x * ri.x + (double)ri.y * ri.y;
+        rz += (double)ri.x * z0 + (double)ri.y * z1;
+        rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
     }
     double v[2] = {rz, rr};
     block_sum<2>(v, lds);
@@ -291,11 +438,9 @@ __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
     *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
 }
 
-// r64 = f - A64 x64 with partial |r|^2 and |f|^2.
-__global__ __launch_bounds__(kWG) void k_residual(int32_t N, int32_t nblk, int64_t sell_nb,
-                                                  const int32_t *__restrict__ sell_off,
-                                                  const int32_t *__restrict__ sell_col,
-                                                  const double *__restrict__ A64,
+// r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
+// partial |r|^2 and |f|^2.
+__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk,
                                                   const double *__restrict__ rhs,
                                                   const double *__restrict__ x64,
                                                   const int32_t *__restrict__ sysi,
@@ -304,18 +449,20 @@ __global__ __launch_bounds__(kWG) void k_residual(int32_t N, int32_t nblk, int64
     __shared__ double lds[8];
     const int32_t b = blockIdx.y;
     if (!sysi[b * kSysStride + SI_ACTIVE]) return;
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t N = op.N;
+    const int64_t vb = (int64_t)b * N;
     double rr = 0.0, ff = 0.0;
-    if (i < N) {
-        const int64_t vb = (int64_t)b * N;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= N) break;
         double y0, y1;
-        spmv_row<double, double>(A64 + 4 * (int64_t)b * sell_nb, sell_col, sell_off, i,
-                                 x64 + 2 * vb, y0, y1);
+        apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
         const double r0 = f.x - y0, r1 = f.y - y1;
         *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
-        rr = r0 * r0 + r1 * r1;
-        ff = f.x * f.x + f.y * f.y;
+        rr += r0 * r0 + r1 * r1;
+        ff += f.x * f.x + f.y * f.y;
     }
     double v[2] = {rr, ff};
     block_sum<2>(v, lds);
@@ -371,16 +518,40 @@ __global__ void k_mark_unconverged(int32_t B, int32_t *__restrict__ sysi) {
 }
 
 template <typename V>
-PcgArgs<V> make_args(mof_mesh *m, int32_t B, const V *A, const V *dinv) {
+OpArgs<V> make_op(mof_mesh *m, const V *a2s, const V *w12, const V *u) {
+    OpArgs<V> op;
+    op.N = m->N;
+    op.M = m->M;
+    op.sell_off = m->sell_off.p;
+    op.sell_col = m->sell_col.p;
+    op.a2s = a2s;
+    op.tsell_off = m->tsell_off.p;
+    op.tinc = reinterpret_cast<const int4 *>(m->tinc.p);
+    op.w12 = w12;
+    op.u = u;
+    return op;
+}
+
+OpArgs<double> op64(mof_mesh *m) { return make_op<double>(m, m->a2s64.p, m->w12_64.p, m->ws.u64.p); }
+
+template <typename V>
+MatArgs<V> make_mat(mof_mesh *m, const V *A) {
+    MatArgs<V> mt;
+    mt.sell_nb = m->pat.sell_nb();
+    mt.sell_off = m->sell_off.p;
+    mt.sell_col = m->sell_col.p;
+    mt.A = A;
+    return mt;
+}
+
+template <typename V>
+PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv) {
     Workspace &w = m->ws;
     PcgArgs<V> a;
     a.N = m->N;
     a.nblk = w.nblk;
     a.B = B;
-    a.sell_nb = m->pat.sell_nb();
-    a.sell_off = m->sell_off.p;
-    a.sell_col = m->sell_col.p;
-    a.A = A;
+    a.mat = mat;
     a.dinv = dinv;
     a.x = reinterpret_cast<V *>(w.vx.p);
     a.r = reinterpret_cast<V *>(w.vr.p);
@@ -404,11 +575,12 @@ void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
 
 // Inner PCG on all active systems; returns iterations summed over systems.
 template <typename V>
-int64_t pcg(mof_mesh *m, int32_t B, const V *A, const V *dinv, const double *rhs, double rtol,
-            int32_t max_iter, hipStream_t s, int32_t *max_iters, uint32_t precision,
+int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
+            double rtol, int32_t max_iter, hipStream_t s, int32_t *max_iters, uint32_t precision,
             SpmvTiming *timing) {
-    PcgArgs<V> a = make_args<V>(m, B, A, dinv);
+    PcgArgs<V> a = make_args<V>(m, B, mat, dinv);
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
+    const dim3 gx(xcd_grid(m->ws.nblk, B));
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol);
     MOF_HIP(hipGetLastError());
@@ -431,9 +603,9 @@ int64_t pcg(mof_mesh *m, int32_t B, const V *A, const V *dinv, const double *rhs
         for (int32_t c = 0; c < n; ++c, ++it) {
             if (timing) MOF_HIP(hipEventRecord(ev[2 * c], s));
             if (it == 0)
-                k_pcg_spmv<V, true><<<g, kWG, 0, s>>>(a, it, 0);
+                k_pcg_spmv<V, true><<<gx, kWG, 0, s>>>(a, it, 0);
             else
-                k_pcg_spmv<V, false><<<g, kWG, 0, s>>>(a, it, 0);
+                k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(a, it, 0);
             if (timing) MOF_HIP(hipEventRecord(ev[2 * c + 1], s));
             k_pcg_update<V><<<g, kWG, 0, s>>>(a, it);
         }
@@ -461,7 +633,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const V *A, const V *dinv, const double *rhs
     }
     if (!done) {
         // one more check launch so SI_CONV records systems converged at max_iter
-        k_pcg_spmv<V, false><<<g, kWG, 0, s>>>(a, it, 0);
+        k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(a, it, 0);
         fetch_flags(m, B, s);
     }
     int64_t total = 0;
@@ -478,24 +650,41 @@ int64_t pcg(mof_mesh *m, int32_t B, const V *A, const V *dinv, const double *rhs
 }  // namespace
 
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
+    // per system: the 2x2 block values, z gathered once, q and p read and
+    // written; shared by all systems of the launch: the column indices.
     const double N = m->N, nb = m->pat.nblocks();
     const double sv = precision == MOF_PREC_MIXED ? 4.0 : 8.0;
     return active * (nb * 4 * sv + N * 2 * sv * 5) + nb * 4.0;
 }
 
-void ensure_workspace(mof_mesh *m, int32_t B) {
+void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     Workspace &w = m->ws;
-    if (w.cap >= B) return;
     const int64_t N = m->N, M = m->M, snb = m->pat.sell_nb();
+    const int32_t cap = std::max(B, w.cap);
+    // the materialised A of the requested precision (SELL padding stays zero);
+    // an A of the other precision is kept only if it already exists
+    auto need_A = [&](auto &arr, bool wanted) {
+        const size_t n = (size_t)(4 * snb * cap);
+        if ((wanted || arr.n > 1) && arr.n < n) {
+            arr.alloc(n);
+            arr.zero(m->stream);
+        }
+    };
+    need_A(w.A32, precision == MOF_PREC_MIXED);
+    need_A(w.A64, precision == MOF_PREC_F64);
+    if (w.cap >= B) {
+        MOF_HIP(hipStreamSynchronize(m->stream));
+        return;
+    }
     w.cap = B;
-    w.nblk = (int32_t)((N + kWG - 1) / kWG);
-    w.u.alloc(6 * M * B);
-    w.fc.alloc(6 * M * B);
-    w.A64.alloc(4 * snb * B);
-    w.A32.alloc(4 * snb * B);
-    // SELL padding stays zero forever: assembly writes real blocks only
-    w.A64.zero(m->stream);
-    w.A32.zero(m->stream);
+    w.nblk = (int32_t)((N + kRowsPerWG - 1) / kRowsPerWG);
+    // triangle slot M of u / fc stays zero: the padding of the incidence lists
+    w.u64.alloc(6 * (M + 1) * B);
+    w.u32.alloc(6 * (M + 1) * B);
+    w.fc.alloc(6 * (M + 1) * B);
+    w.u64.zero(m->stream);
+    w.u32.zero(m->stream);
+    w.fc.zero(m->stream);
     w.dinv64.alloc(4 * N * B);
     w.dinv32.alloc(4 * N * B);
     w.rhs.alloc(2 * N * B);
@@ -533,22 +722,24 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
     MOF_HIP(hipGetLastError());
     dim3 g((unsigned)w.nblk, (unsigned)B);
+    dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
     int64_t iters = 0;
     int32_t o = 0;
+    const OpArgs<double> o64 = op64(m);
     for (; o < sp.max_outer; ++o) {
         const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
         if (sp.precision == MOF_PREC_MIXED) {
-            iters += pcg<float>(m, B, w.A32.p, w.dinv32.p, rhs, sp.inner_rtol, sp.max_iter, s,
-                                max_iters, sp.precision, tm);
-            k_outer_update<float><<<g, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
+            iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol,
+                                sp.max_iter, s, max_iters, sp.precision, tm);
+            k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
                                                     w.sysi.p, w.x64.p);
         } else {
-            iters += pcg<double>(m, B, w.A64.p, w.dinv64.p, rhs, o == 0 ? 0.5 * sp.rtol : sp.inner_rtol,
-                                 sp.max_iter, s, max_iters, sp.precision, tm);
-            k_outer_update<double><<<g, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+            iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
+                                 o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s, max_iters,
+                                 sp.precision, tm);
+            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
-        k_residual<<<g, kWG, 0, s>>>(m->N, w.nblk, m->pat.sell_nb(), m->sell_off.p, m->sell_col.p,
-                                     w.A64.p, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
+        k_residual<<<g, kWG, 0, s>>>(o64, w.nblk, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(w.nblk, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
         MOF_HIP(hipGetLastError());
@@ -571,18 +762,18 @@ double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipS
                   double *bytes) {
     Workspace &w = m->ws;
     MOF_REQUIRE(B >= 1 && B <= w.cap, "bench batch exceeds the workspace of the last solve");
-    dim3 g((unsigned)w.nblk, (unsigned)B);
     hipEvent_t e0, e1;
     MOF_HIP(hipEventCreate(&e0));
     MOF_HIP(hipEventCreate(&e1));
     *bytes = spmv_launch_bytes(m, precision, B);
+    const dim3 gx(xcd_grid(w.nblk, B));
     auto launch = [&]() {
         if (precision == MOF_PREC_MIXED) {
-            PcgArgs<float> a = make_args<float>(m, B, w.A32.p, w.dinv32.p);
-            k_pcg_spmv<float, false><<<g, kWG, 0, s>>>(a, 1, kForce);
+            PcgArgs<float> a = make_args<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p);
+            k_pcg_spmv<float, false><<<gx, kWG, 0, s>>>(a, 1, kForce);
         } else {
-            PcgArgs<double> a = make_args<double>(m, B, w.A64.p, w.dinv64.p);
-            k_pcg_spmv<double, false><<<g, kWG, 0, s>>>(a, 1, kForce);
+            PcgArgs<double> a = make_args<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p);
+            k_pcg_spmv<double, false><<<gx, kWG, 0, s>>>(a, 1, kForce);
         }
     };
     for (int r = 0; r < 3; ++r) launch();
