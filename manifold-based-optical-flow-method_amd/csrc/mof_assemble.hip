@@ -222,45 +222,84 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
     }
 }
 
-// Per-vertex terms of B systems on the solve path: f_i folded over the
-// incident triangles in triangle order (bit-identical to the reference's
-// f), the diagonal block D_i = lambda a2_ii + sum_T u_a u_a^T A_T/6 and its
-// 2x2 block-Jacobi inverse.
-__global__ __launch_bounds__(kWG) void k_vertex_step(
-    int32_t N, int32_t M, const int32_t *__restrict__ tsell_off, const int4 *__restrict__ tinc,
-    const int32_t *__restrict__ diag_pos, const double *__restrict__ a2s,
-    const double *__restrict__ iw, const double *__restrict__ u, const double *__restrict__ fc,
-    int block_jacobi, double *__restrict__ dinv64, float *__restrict__ dinv32,
-    double *__restrict__ rhs) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+// Solve-path A_b = a1_b + lambda a2 of B systems, one SELL position per
+// thread (coalesced stores): the a1 block is folded in fp64 over its terms in
+// triangle order exactly as the export path does, then stored in the inner
+// solver's precision (fp32 for MOF_PREC_MIXED, fp64 otherwise). The thread
+// holding a diagonal block also folds f_i (bit-identical to the reference's
+// f) and writes the 2x2 block-Jacobi inverse of vertex i. Terms are fetched
+// four at a time (indices, then u pairs) so the fold is not one memory round
+// trip per term. SELL padding is never written and stays zero.
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_assemble_blocks(
+    int64_t sell_nb, int32_t N, int32_t M, const int32_t *__restrict__ sell_blk,
+    const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
+    const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
+    const double *__restrict__ iw, const double *__restrict__ a2s, const double *__restrict__ u,
+    const double *__restrict__ fc, int block_jacobi, V *__restrict__ A,
+    double *__restrict__ dinv64, float *__restrict__ dinv32, double *__restrict__ rhs) {
+    const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
     const int32_t b = blockIdx.y;
-    if (i >= N) return;
-    const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = tsell_off[s], w = (tsell_off[s + 1] - o) >> 6;
+    if (pos >= sell_nb) return;
+    const int32_t p = sell_blk[pos];
+    if (p < 0) return;
+    const int32_t i = blk_row[p];
+    const bool diag = (vcol[p] == i);
     const double *ub = u + 6 * (int64_t)b * (M + 1);
     const double *fb = fc + 6 * (int64_t)b * (M + 1);
-    double f0 = 0.0, f1 = 0.0, d00 = 0.0, d01 = 0.0, d10 = 0.0, d11 = 0.0;
-    for (int32_t t = 0; t < w; ++t) {
-        const int4 q = tinc[(int64_t)o + t * kSlice + l];
-        if (q.x >= M) break;  // padding comes last in every row
-        const double2 ua = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)q.x + 2 * q.y);
-        const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)q.x + 2 * q.y);
-        const double c = iw[2 * (int64_t)q.x];
-        f0 += fv.x;
-        f1 += fv.y;
-        d00 += ua.x * ua.x * c;
-        d01 += ua.x * ua.y * c;
-        d10 += ua.y * ua.x * c;
-        d11 += ua.y * ua.y * c;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double f0 = 0.0, f1 = 0.0;
+    const int32_t c0 = cptr[p], c1 = cptr[p + 1];
+    constexpr int U = 4;
+    for (int32_t c = c0; c < c1; c += U) {
+        int32_t T[U], a[U], bb[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int32_t code = clist[min(c + q, c1 - 1)];
+            T[q] = code / 9;
+            a[q] = (code % 9) / 3;
+            bb[q] = code % 3;
+        }
+        double2 ua[U], uv[U];
+        double integ[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            ua[q] = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)T[q] + 2 * a[q]);
+            uv[q] = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)T[q] + 2 * bb[q]);
+            integ[q] = iw[2 * (int64_t)T[q] + (diag ? 0 : 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            if (c + q >= c1) break;
+            acc[0] += ua[q].x * uv[q].x * integ[q];
+            acc[1] += ua[q].x * uv[q].y * integ[q];
+            acc[2] += ua[q].y * uv[q].x * integ[q];
+            acc[3] += ua[q].y * uv[q].y * integ[q];
+            if (diag && a[q] == bb[q]) {
+                const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)T[q] + 2 * a[q]);
+                f0 += fv.x;
+                f1 += fv.y;
+            }
+        }
     }
-    const double *sd = a2s + 4 * (int64_t)diag_pos[i];
-    const double D[4] = {d00 + sd[0], d01 + sd[1], d10 + sd[2], d11 + sd[3]};
+    const double2 s01 = *reinterpret_cast<const double2 *>(a2s + 4 * pos);
+    const double2 s23 = *reinterpret_cast<const double2 *>(a2s + 4 * pos + 2);
+    const double Av[4] = {acc[0] + s01.x, acc[1] + s01.y, acc[2] + s23.x, acc[3] + s23.y};
+    V *o = A + 4 * ((int64_t)b * sell_nb + pos);
+    if constexpr (sizeof(V) == 4) {
+        *reinterpret_cast<float4 *>(o) =
+            make_float4((float)Av[0], (float)Av[1], (float)Av[2], (float)Av[3]);
+    } else {
+        *reinterpret_cast<double2 *>(o) = make_double2(Av[0], Av[1]);
+        *reinterpret_cast<double2 *>(o + 2) = make_double2(Av[2], Av[3]);
+    }
+    if (!diag) return;
     double inv[4];
     if (block_jacobi) {
-        const double det = D[0] * D[3] - D[1] * D[2];
-        inv[0] = D[3] / det; inv[1] = -D[1] / det; inv[2] = -D[2] / det; inv[3] = D[0] / det;
+        const double det = Av[0] * Av[3] - Av[1] * Av[2];
+        inv[0] = Av[3] / det; inv[1] = -Av[1] / det; inv[2] = -Av[2] / det; inv[3] = Av[0] / det;
     } else {
-        inv[0] = 1.0 / D[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / D[3];
+        inv[0] = 1.0 / Av[0]; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / Av[3];
     }
     const int64_t vi = (int64_t)b * N + i;
     *reinterpret_cast<double2 *>(dinv64 + 4 * vi) = make_double2(inv[0], inv[1]);
@@ -268,49 +307,6 @@ __global__ __launch_bounds__(kWG) void k_vertex_step(
     *reinterpret_cast<float4 *>(dinv32 + 4 * vi) =
         make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
     *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
-}
-
-// Solve-path A_b = a1_b + lambda a2 of B systems, one SELL position per
-// thread (coalesced stores): the a1 block is folded in fp64 over its terms in
-// triangle order exactly as the export path does, then stored in the inner
-// solver's precision (fp32 for MOF_PREC_MIXED, fp64 otherwise). SELL padding
-// is never written and stays zero.
-template <typename V>
-__global__ __launch_bounds__(kWG) void k_assemble_blocks(
-    int64_t sell_nb, int32_t M, const int32_t *__restrict__ sell_blk,
-    const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
-    const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
-    const double *__restrict__ iw, const double *__restrict__ a2s, const double *__restrict__ u,
-    V *__restrict__ A) {
-    const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
-    if (pos >= sell_nb) return;
-    const int32_t p = sell_blk[pos];
-    if (p < 0) return;
-    const bool diag = (vcol[p] == blk_row[p]);
-    const double *ub = u + 6 * (int64_t)b * (M + 1);
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
-        const int32_t code = clist[c];
-        const int32_t T = code / 9, a = (code % 9) / 3, bb = code % 3;
-        const double2 ua = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)T + 2 * a);
-        const double2 uv = *reinterpret_cast<const double2 *>(ub + 6 * (int64_t)T + 2 * bb);
-        const double integ = iw[2 * (int64_t)T + (diag ? 0 : 1)];
-        acc[0] += ua.x * uv.x * integ;
-        acc[1] += ua.x * uv.y * integ;
-        acc[2] += ua.y * uv.x * integ;
-        acc[3] += ua.y * uv.y * integ;
-    }
-    const double2 s01 = *reinterpret_cast<const double2 *>(a2s + 4 * pos);
-    const double2 s23 = *reinterpret_cast<const double2 *>(a2s + 4 * pos + 2);
-    const double v0 = acc[0] + s01.x, v1 = acc[1] + s01.y, v2 = acc[2] + s23.x, v3 = acc[3] + s23.y;
-    V *o = A + 4 * ((int64_t)b * sell_nb + pos);
-    if constexpr (sizeof(V) == 4) {
-        *reinterpret_cast<float4 *>(o) = make_float4((float)v0, (float)v1, (float)v2, (float)v3);
-    } else {
-        *reinterpret_cast<double2 *>(o) = make_double2(v0, v1);
-        *reinterpret_cast<double2 *>(o + 2) = make_double2(v2, v3);
-    }
 }
 
 // lambda * a2 for the solve operator (fp64 copy bit-identical to the
@@ -432,21 +428,19 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), (unsigned)B);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
                                   w.u64.p, w.u32.p, w.fc.p);
-    dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
-    k_vertex_step<<<gv, kWG, 0, s>>>(m->N, m->M, m->tsell_off.p,
-                                     reinterpret_cast<const int4 *>(m->tinc.p), m->diag_pos.p,
-                                     m->a2s64.p, m->iw.p, w.u64.p, w.fc.p, block_jacobi ? 1 : 0,
-                                     w.dinv64.p, w.dinv32.p, w.rhs.p);
     const int64_t snb = m->pat.sell_nb();
     dim3 gb((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
+    const int bj = block_jacobi ? 1 : 0;
     if (precision == MOF_PREC_MIXED)
-        k_assemble_blocks<float><<<gb, kWG, 0, s>>>(snb, m->M, m->sell_blk.p, m->blk_row.p, m->vcol.p,
-                                                    m->cptr.p, m->clist.p, m->iw.p, m->a2s64.p,
-                                                    w.u64.p, w.A32.p);
+        k_assemble_blocks<float><<<gb, kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
+                                                    m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
+                                                    m->a2s64.p, w.u64.p, w.fc.p, bj, w.A32.p,
+                                                    w.dinv64.p, w.dinv32.p, w.rhs.p);
     else
-        k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->M, m->sell_blk.p, m->blk_row.p,
+        k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
-                                                     m->a2s64.p, w.u64.p, w.A64.p);
+                                                     m->a2s64.p, w.u64.p, w.fc.p, bj, w.A64.p,
+                                                     w.dinv64.p, w.dinv32.p, w.rhs.p);
     MOF_HIP(hipGetLastError());
 }
 

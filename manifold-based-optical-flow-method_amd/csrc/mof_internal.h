@@ -150,6 +150,8 @@ struct mof_mesh {
     int32_t h_cap = 0;
     // HIP event pairs bracketing timed SpMV launches (MOF_TIME_SPMV)
     std::vector<hipEvent_t> spmv_events;
+    // PCG iterations the previous batch needed, per (precision, outer step)
+    std::vector<int32_t> iter_hint;
 };
 
 namespace mof {

@@ -195,48 +195,70 @@ __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_
 }
 
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
-// (lambda a2 + per-triangle a1; x = that system's vector).
+// (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
+// U slots / incident triangles at a time as in spmv_row.
 template <typename V>
 __device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int32_t i,
-                                          const V *__restrict__ x, double &y0, double &y1) {
+                                             const V *__restrict__ x, double &y0, double &y1) {
     using V2 = typename VT<V>::V2;
+    constexpr int U = 4;
     const int32_t s = i >> 6, l = i & 63;
     V a0 = 0, a1 = 0;
     // lambda a2 x
     {
         const int32_t o = op.sell_off[s];
         const int32_t w = (op.sell_off[s + 1] - o) >> 6;
-        for (int32_t t = 0; t < w; ++t) {
-            const int64_t pos = (int64_t)o + t * kSlice + l;
-            const int32_t j = op.sell_col[pos];
-            V a[4];
-            ld_blk(op.a2s, pos, a);
-            const V2 xj = ld2(x + 2 * (int64_t)j);
-            a0 += a[0] * xj.x + a[1] * xj.y;
-            a1 += a[2] * xj.x + a[3] * xj.y;
+        for (int32_t t0 = 0; t0 < w; t0 += U) {
+            int32_t j[U];
+            V blk[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+            for (int u = 0; u < U; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const V2 xj = ld2(x + 2 * (int64_t)j[u]);
+                const bool on = t0 + u < w;
+                a0 += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : (V)0;
+                a1 += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : (V)0;
+            }
         }
     }
-    // a1_b x, per incident triangle
+    // a1_b x, per incident triangle (padding entries point at the zero slot M)
     {
         const V *ub = op.u + 6 * (int64_t)b * (op.M + 1);
         const V2 xi = ld2(x + 2 * (int64_t)i);
         const int32_t o = op.tsell_off[s];
         const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
-        for (int32_t t = 0; t < w; ++t) {
-            const int4 q = op.tinc[(int64_t)o + t * kSlice + l];
-            const V *uT = ub + 6 * (int64_t)q.x;
-            const V2 P0 = ld2(uT), P1 = ld2(uT + 2), P2 = ld2(uT + 4);
-            const V2 ui = q.y == 0 ? P0 : (q.y == 1 ? P1 : P2);
-            const V2 uj = q.y == 0 ? P1 : (q.y == 1 ? P2 : P0);
-            const V2 uk = q.y == 0 ? P2 : (q.y == 1 ? P0 : P1);
-            const V2 xj = ld2(x + 2 * (int64_t)q.z);
-            const V2 xk = ld2(x + 2 * (int64_t)q.w);
-            const V si = ui.x * xi.x + ui.y * xi.y;
-            const V sj = uj.x * xj.x + uj.y * xj.y;
-            const V sk = uk.x * xk.x + uk.y * xk.y;
-            const V c = op.w12[q.x] * ((si + si) + sj + sk);
-            a0 += ui.x * c;
-            a1 += ui.y * c;
+        for (int32_t t0 = 0; t0 < w; t0 += U) {
+            int4 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) q[u] = op.tinc[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+            V2 P0[U], P1[U], P2[U], xj[U], xk[U];
+            V w12[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const V *uT = ub + 6 * (int64_t)q[u].x;
+                P0[u] = ld2(uT);
+                P1[u] = ld2(uT + 2);
+                P2[u] = ld2(uT + 4);
+                xj[u] = ld2(x + 2 * (int64_t)q[u].z);
+                xk[u] = ld2(x + 2 * (int64_t)q[u].w);
+                w12[u] = op.w12[q[u].x];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = q[u].y;
+                const V2 ui = c == 0 ? P0[u] : (c == 1 ? P1[u] : P2[u]);
+                const V2 uj = c == 0 ? P1[u] : (c == 1 ? P2[u] : P0[u]);
+                const V2 uk = c == 0 ? P2[u] : (c == 1 ? P0[u] : P1[u]);
+                const V si = ui.x * xi.x + ui.y * xi.y;
+                const V sj = uj.x * xj[u].x + uj.y * xj[u].y;
+                const V sk = uk.x * xk[u].x + uk.y * xk[u].y;
+                const V cc = (t0 + u < w) ? w12[u] * ((si + si) + sj + sk) : (V)0;
+                a0 += ui.x * cc;
+                a1 += ui.y * cc;
+            }
         }
     }
     y0 = a0;
@@ -577,29 +599,41 @@ void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
 template <typename V>
 int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
             double rtol, int32_t max_iter, hipStream_t s, int32_t *max_iters, uint32_t precision,
-            SpmvTiming *timing) {
+            SpmvTiming *timing, int32_t *hint) {
     PcgArgs<V> a = make_args<V>(m, B, mat, dinv);
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B));
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol);
     MOF_HIP(hipGetLastError());
-    // systems active at the start of this solve
-    fetch_flags(m, B, s);
+    // systems active at the start of this solve: the host mirror is current
+    // (reset by solve_batch, refreshed by every outer check)
     std::vector<int32_t> was_active(B);
-    for (int32_t b = 0; b < B; ++b) was_active[b] = m->h_sysi[b * kSysStride + SI_ACTIVE];
-    int32_t it = 0;
-    int32_t chunk = 8;
-    bool done = false;
     int32_t running = 0;
-    for (int32_t b = 0; b < B; ++b) running += was_active[b];
+    for (int32_t b = 0; b < B; ++b) {
+        was_active[b] = m->h_sysi[b * kSysStride + SI_ACTIVE];
+        running += was_active[b];
+    }
+    // The first chunk runs as many iterations as the same solve of the
+    // previous batch needed (timesteps of one run converge alike), so the
+    // host usually synchronises once per inner solve; converged systems
+    // retire on the device, so overshooting costs only early-exit launches.
+    int32_t it = 0;
+    int32_t chunk = *hint > 0 ? *hint : 8;
+    bool done = false;
     std::vector<hipEvent_t> &ev = m->spmv_events;
-    if (timing && ev.empty()) {
-        ev.resize(2 * 64);
-        for (auto &e : ev) MOF_HIP(hipEventCreate(&e));
+    if (timing && (int32_t)ev.size() < 2 * chunk) {
+        const size_t old = ev.size();
+        ev.resize(2 * (size_t)std::max(chunk, 64));
+        for (size_t q = old; q < ev.size(); ++q) MOF_HIP(hipEventCreate(&ev[q]));
     }
     while (!done && it < max_iter) {
         const int32_t n = std::min(chunk, max_iter - it);
+        if (timing && (int32_t)ev.size() < 2 * n) {
+            const size_t old = ev.size();
+            ev.resize(2 * (size_t)n);
+            for (size_t q = old; q < ev.size(); ++q) MOF_HIP(hipEventCreate(&ev[q]));
+        }
         for (int32_t c = 0; c < n; ++c, ++it) {
             if (timing) MOF_HIP(hipEventRecord(ev[2 * c], s));
             if (it == 0)
@@ -629,7 +663,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 ++running;
             }
         }
-        chunk = std::min(chunk * 2, 64);
+        chunk = 8;
     }
     if (!done) {
         // one more check launch so SI_CONV records systems converged at max_iter
@@ -637,13 +671,16 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         fetch_flags(m, B, s);
     }
     int64_t total = 0;
+    int32_t slowest = 0;
     for (int32_t b = 0; b < B; ++b) {
         if (!was_active[b]) continue;
         const int32_t c = m->h_sysi[b * kSysStride + SI_CONV];
         const int32_t its = c >= 0 ? c : it;
         total += its;
-        *max_iters = std::max(*max_iters, its);
+        slowest = std::max(slowest, its);
     }
+    *max_iters = std::max(*max_iters, slowest);
+    if (slowest > 0) *hint = slowest + 1;  // +1: convergence is seen by the launch after
     return total;
 }
 
@@ -721,6 +758,13 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     Workspace &w = m->ws;
     k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
     MOF_HIP(hipGetLastError());
+    for (int32_t b = 0; b < B; ++b) {  // host mirror of the reset state
+        int32_t *si = m->h_sysi + b * kSysStride;
+        for (int k = 0; k < kSysStride; ++k) si[k] = 0;
+        si[SI_ACTIVE] = 1;
+        si[SI_CONV] = -1;
+    }
+    if (m->iter_hint.size() < 2 * 16) m->iter_hint.assign(2 * 16, 0);
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
     int64_t iters = 0;
@@ -730,13 +774,14 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
         if (sp.precision == MOF_PREC_MIXED) {
             iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol,
-                                sp.max_iter, s, max_iters, sp.precision, tm);
+                                sp.max_iter, s, max_iters, sp.precision, tm,
+                                &m->iter_hint[16 + std::min(o, 15)]);
             k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
                                                     w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s, max_iters,
-                                 sp.precision, tm);
+                                 sp.precision, tm, &m->iter_hint[std::min(o, 15)]);
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         k_residual<<<g, kWG, 0, s>>>(o64, w.nblk, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
