@@ -34,6 +34,8 @@ CONFIG_NAMES = {
     "C2": "32k-vertex jittered icosphere (n=57, 32,492 vertices), fp64 Jacobi-PCG",
     "C3": "160k-vertex jittered icosphere (n=128, 163,842 vertices), fp32 PCG + fp64 refinement",
     "C5": "640k-vertex jittered icosphere (n=253, 640,092 vertices)",
+    "R3": "163,842-vertex irregular random-hull sphere (valence 3-14, random vertex order)",
+    "P3": "C3 mesh with randomly relabelled vertices (no index locality)",
 }
 
 

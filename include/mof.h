@@ -41,6 +41,10 @@ extern "C" {
 #define MOF_GEOM_F32_POINTS 1u /* xyz holds float32 values: grad_w in float32
                                   arithmetic, as numpy does for pyvista's
                                   float32 points (S3…py:79, :238-255) */
+#define MOF_NO_REORDER 2u      /* keep the caller's vertex order on the device
+                                  (default: reverse Cuthill-McKee; results and
+                                  every export are in the caller's order either
+                                  way, bit for bit) */
 
 /* mof_opts.precision */
 #define MOF_PREC_F64 0         /* fp64 values + vectors, Jacobi-PCG */

@@ -62,21 +62,28 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// SELL block layout -> canonical scalar CSR (2N x 2N).
+// SELL block layout (internal order) -> canonical scalar CSR (2N x 2N) in
+// the caller's vertex order.
 void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop_zeros,
                  int32_t *indptr, int32_t *indices, double *data, int64_t *nnz_out) {
     const mof::Pattern &P = m->pat;
     const int32_t N = m->N;
     int64_t nnz = 0;
     indptr[0] = 0;
+    std::vector<std::pair<int32_t, int64_t>> row;  // (caller column vertex, SELL pos)
     for (int32_t r = 0; r < 2 * N; ++r) {
-        const int32_t i = r % N, al = r / N;
+        const int32_t io = r % N, al = r / N;
+        const int32_t i = m->perm[io];
+        row.clear();
+        for (int32_t p = P.vptr[i], t = 0; p < P.vptr[i + 1]; ++p, ++t)
+            row.emplace_back(m->inv[P.vcol[p]],
+                             (int64_t)P.sell_off[i >> 6] + (int64_t)t * mof::kSlice + (i & 63));
+        std::sort(row.begin(), row.end());
         for (int half = 0; half < 2; ++half) {  // columns j, then j + N
-            for (int32_t p = P.vptr[i], t = 0; p < P.vptr[i + 1]; ++p, ++t) {
-                const int64_t pos = (int64_t)P.sell_off[i >> 6] + (int64_t)t * mof::kSlice + (i & 63);
-                const double v = blk[4 * pos + 2 * al + half];
+            for (const auto &cp : row) {
+                const double v = blk[4 * cp.second + 2 * al + half];
                 if (drop_zeros && v == 0.0) continue;
-                indices[nnz] = P.vcol[p] + half * N;
+                indices[nnz] = cp.first + half * N;
                 data[nnz] = v;
                 ++nnz;
             }
@@ -120,42 +127,79 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
             m->device = device;
             m->flags = flags;
             double t0 = now_ms();
-            mof::build_pattern(tri, N, M, m->pat);
+            MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
+            for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+                MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
+            // internal vertex order (RCM) and triangle order (by smallest
+            // internal vertex id), and the relabelled inputs
+            m->perm.resize(N);
+            m->tperm.resize(M);
+            for (int32_t i = 0; i < N; ++i) m->perm[i] = i;
+            for (int32_t T = 0; T < M; ++T) m->tperm[T] = T;
+            if (!(flags & MOF_NO_REORDER)) {
+                mof::Pattern adj;
+                mof::build_pattern(tri, N, M, adj);
+                m->perm = mof::rcm_order(adj);
+                std::vector<int32_t> key(M);
+                for (int32_t T = 0; T < M; ++T)
+                    key[T] = std::min({m->perm[tri[3 * (size_t)T]], m->perm[tri[3 * (size_t)T + 1]],
+                                       m->perm[tri[3 * (size_t)T + 2]]});
+                std::stable_sort(m->tperm.begin(), m->tperm.end(),
+                                 [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+            }
+            m->inv.resize(N);
+            for (int32_t i = 0; i < N; ++i) m->inv[m->perm[i]] = i;
+            m->tinv.resize(M);
+            for (int32_t T = 0; T < M; ++T) m->tinv[m->tperm[T]] = T;
+            std::vector<int32_t> tri_new(3 * (size_t)M), tri_old(3 * (size_t)M);
+            std::vector<double> area_new(M);
+            for (int32_t T = 0; T < M; ++T) {
+                const int32_t To = m->tperm[T];
+                for (int c = 0; c < 3; ++c) {
+                    tri_old[3 * (size_t)T + c] = tri[3 * (size_t)To + c];
+                    tri_new[3 * (size_t)T + c] = m->perm[tri[3 * (size_t)To + c]];
+                }
+                area_new[T] = area[To];
+            }
+            std::vector<double> xyz_new(3 * (size_t)N), nrm_new(3 * (size_t)N);
+            for (int32_t i = 0; i < N; ++i)
+                for (int d = 0; d < 3; ++d) {
+                    xyz_new[3 * (size_t)m->perm[i] + d] = xyz[3 * (size_t)i + d];
+                    nrm_new[3 * (size_t)m->perm[i] + d] = nrm[3 * (size_t)i + d];
+                }
+            mof::build_pattern(tri_new.data(), N, M, m->pat, m->tinv.data());
             m->ms_pattern = now_ms() - t0;
             MOF_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
             hipStream_t s = m->stream;
             const mof::Pattern &P = m->pat;
             m->tri.alloc(3 * (size_t)M);
-            m->tri.upload(tri, 3 * (size_t)M, s);
+            m->tri.upload(tri_new.data(), 3 * (size_t)M, s);
+            m->tri_orig.alloc(3 * (size_t)M);
+            m->tri_orig.upload(tri_old.data(), 3 * (size_t)M, s);
+            m->inv_d.alloc(N);
+            m->inv_d.upload(m->inv.data(), N, s);
             m->area.alloc(M);
-            m->area.upload(area, M, s);
-            m->vptr.alloc(N + 1);
-            m->vptr.upload(P.vptr.data(), N + 1, s);
-            m->vcol.alloc(P.vcol.size());
-            m->vcol.upload(P.vcol.data(), P.vcol.size(), s);
-            m->cptr.alloc(P.cptr.size());
-            m->cptr.upload(P.cptr.data(), P.cptr.size(), s);
-            m->clist.alloc(P.clist.size());
-            m->clist.upload(P.clist.data(), P.clist.size(), s);
-            m->sell_off.alloc(P.sell_off.size());
-            m->sell_off.upload(P.sell_off.data(), P.sell_off.size(), s);
-            m->sell_col.alloc(P.sell_col.size());
-            m->sell_col.upload(P.sell_col.data(), P.sell_col.size(), s);
-            m->sell_blk.alloc(P.sell_blk.size());
-            m->sell_blk.upload(P.sell_blk.data(), P.sell_blk.size(), s);
-            m->blk_row.alloc(P.blk_row.size());
-            m->blk_row.upload(P.blk_row.data(), P.blk_row.size(), s);
-            m->diag_pos.alloc(P.diag_pos.size());
-            m->diag_pos.upload(P.diag_pos.data(), P.diag_pos.size(), s);
-            m->tsell_off.alloc(P.tsell_off.size());
-            m->tsell_off.upload(P.tsell_off.data(), P.tsell_off.size(), s);
-            m->tinc.alloc(P.tinc.size());
-            m->tinc.upload(P.tinc.data(), P.tinc.size(), s);
+            m->area.upload(area_new.data(), M, s);
+            auto put = [&](mof::DevArray<int32_t> &d, const std::vector<int32_t> &h) {
+                d.alloc(h.size());
+                d.upload(h.data(), h.size(), s);
+            };
+            put(m->vptr, P.vptr);
+            put(m->vcol, P.vcol);
+            put(m->cptr, P.cptr);
+            put(m->clist, P.clist);
+            put(m->sell_off, P.sell_off);
+            put(m->sell_col, P.sell_col);
+            put(m->sell_blk, P.sell_blk);
+            put(m->blk_row, P.blk_row);
+            put(m->diag_pos, P.diag_pos);
+            put(m->tsell_off, P.tsell_off);
+            put(m->tinc, P.tinc);
             mof::DevArray<double> dxyz, dnrm;
             dxyz.alloc(3 * (size_t)N);
-            dxyz.upload(xyz, 3 * (size_t)N, s);
+            dxyz.upload(xyz_new.data(), 3 * (size_t)N, s);
             dnrm.alloc(3 * (size_t)N);
-            dnrm.upload(nrm, 3 * (size_t)N, s);
+            dnrm.upload(nrm_new.data(), 3 * (size_t)N, s);
             m->e.alloc(6 * (size_t)N);
             m->gw.alloc(9 * (size_t)M);
             m->iw.alloc(2 * (size_t)M);
@@ -218,10 +262,30 @@ int mof_geometry_export(mof_mesh *m, double *e, double *grad_w, double *iw) {
         MOF_REQUIRE(m, "mesh is NULL");
         DeviceGuard dg(m->device);
         hipStream_t s = m->stream;
-        if (e) MOF_HIP(hipMemcpyAsync(e, m->e.p, m->e.bytes(), hipMemcpyDeviceToHost, s));
-        if (grad_w) MOF_HIP(hipMemcpyAsync(grad_w, m->gw.p, m->gw.bytes(), hipMemcpyDeviceToHost, s));
-        if (iw) MOF_HIP(hipMemcpyAsync(iw, m->iw.p, m->iw.bytes(), hipMemcpyDeviceToHost, s));
+        std::vector<double> e_int, gw_int, iw_int;
+        if (e) {
+            e_int.resize(m->e.n);
+            MOF_HIP(hipMemcpyAsync(e_int.data(), m->e.p, m->e.bytes(), hipMemcpyDeviceToHost, s));
+        }
+        if (grad_w) {
+            gw_int.resize(m->gw.n);
+            MOF_HIP(hipMemcpyAsync(gw_int.data(), m->gw.p, m->gw.bytes(), hipMemcpyDeviceToHost, s));
+        }
+        if (iw) {
+            iw_int.resize(m->iw.n);
+            MOF_HIP(hipMemcpyAsync(iw_int.data(), m->iw.p, m->iw.bytes(), hipMemcpyDeviceToHost, s));
+        }
         MOF_HIP(hipStreamSynchronize(s));
+        // back to the caller's vertex and triangle order
+        if (e)
+            for (int32_t i = 0; i < m->N; ++i)
+                std::memcpy(e + 6 * (size_t)i, e_int.data() + 6 * (size_t)m->perm[i], 6 * sizeof(double));
+        if (grad_w)
+            for (int32_t T = 0; T < m->M; ++T)
+                std::memcpy(grad_w + 9 * (size_t)T, gw_int.data() + 9 * (size_t)m->tinv[T], 9 * sizeof(double));
+        if (iw)
+            for (int32_t T = 0; T < m->M; ++T)
+                std::memcpy(iw + 2 * (size_t)T, iw_int.data() + 2 * (size_t)m->tinv[T], 2 * sizeof(double));
     });
 }
 
@@ -259,9 +323,15 @@ int mof_assemble(mof_mesh *m, const double *I0, const double *I1, double dt, dou
         MOF_HIP(hipMemcpyAsync(w.dt.p, &dt, sizeof(double), hipMemcpyHostToDevice, s));
         mof::launch_assemble_export(m, w.Ibuf.p, w.Ibuf.p + N, lambda, s);
         m->have_last_A = true;
+        std::vector<double> fi(2 * N);
         if (f)
-            MOF_HIP(hipMemcpyAsync(f, m->fexp.p, sizeof(double) * 2 * N, hipMemcpyDeviceToHost, s));
+            MOF_HIP(hipMemcpyAsync(fi.data(), m->fexp.p, sizeof(double) * 2 * N, hipMemcpyDeviceToHost, s));
         MOF_HIP(hipStreamSynchronize(s));
+        if (f)
+            for (int64_t i = 0; i < N; ++i) {
+                f[i] = fi[m->perm[i]];
+                f[N + i] = fi[N + m->perm[i]];
+            }
     });
 }
 

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
 // f term (u (2 dI_a + sum of the other distinct corners' dI) A_T) / 12.
 // Triangle slot M of u / fc stays zero (padding of the incidence lists).
 __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__restrict__ tri,
+                                                  const int32_t *__restrict__ tri_orig,
                                                   const double *__restrict__ gw,
                                                   const double *__restrict__ e,
                                                   const double *__restrict__ area,
@@ -183,12 +184,15 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
     const double *g = gw + 9 * (int64_t)T;
     const double *i0 = I0 + b * ldI;
     const double *i1 = I1 + b * ldI;
-    const double a0 = i0[v[0]], a1 = i0[v[1]], a2 = i0[v[2]];
+    // I rows are indexed by the caller's vertex ids
+    const int32_t vo[3] = {tri_orig[3 * (int64_t)T], tri_orig[3 * (int64_t)T + 1],
+                           tri_orig[3 * (int64_t)T + 2]};
+    const double a0 = i0[vo[0]], a1 = i0[vo[1]], a2 = i0[vo[2]];
     double gI[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) gI[d] = (a0 * g[d] + a1 * g[3 + d]) + a2 * g[6 + d];
     const double h = dt[b];
-    const double pd[3] = {(i1[v[0]] - a0) / h, (i1[v[1]] - a1) / h, (i1[v[2]] - a2) / h};
+    const double pd[3] = {(i1[vo[0]] - a0) / h, (i1[vo[1]] - a1) / h, (i1[vo[2]] - a2) / h};
     const double A = area[T];
     const int64_t base = 6 * ((int64_t)b * (M + 1) + T);
     double uo[6], fo[6];
@@ -378,8 +382,10 @@ __global__ __launch_bounds__(kWG) void k_assemble_export(
     }
 }
 
-// x64 (interleaved) -> V (B, 2N) planar; failed systems are NaN-filled.
+// x64 (interleaved, internal order) -> V (B, 2N) planar in the caller's
+// vertex order; failed systems are NaN-filled.
 __global__ __launch_bounds__(kWG) void k_to_planar(int32_t N, const double *__restrict__ x,
+                                                   const int32_t *__restrict__ inv,
                                                    const int32_t *__restrict__ sysi,
                                                    double *__restrict__ V) {
     const int32_t i = blockIdx.x * kWG + threadIdx.x;
@@ -388,15 +394,38 @@ __global__ __launch_bounds__(kWG) void k_to_planar(int32_t N, const double *__re
     const bool failed = sysi[b * kSysStride + SI_FAILED] != 0;
     const double2 v = *reinterpret_cast<const double2 *>(x + 2 * ((int64_t)b * N + i));
     const double nan = __builtin_nan("");
-    V[(int64_t)b * 2 * N + i] = failed ? nan : v.x;
-    V[(int64_t)b * 2 * N + N + i] = failed ? nan : v.y;
+    const int32_t o = inv[i];
+    V[(int64_t)b * 2 * N + o] = failed ? nan : v.x;
+    V[(int64_t)b * 2 * N + N + o] = failed ? nan : v.y;
 }
 
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
 
+// Host-side guard before any launch: every device array a kernel indexes is
+// allocated with the size the pattern implies (a missing upload would
+// otherwise surface as a GPU memory fault).
+void check_mesh_arrays(const mof_mesh *m) {
+    const Pattern &P = m->pat;
+    const size_t N = m->N, M = m->M;
+    auto ok = [](const auto &d, size_t n) { return d.p != nullptr && d.n >= n; };
+    MOF_REQUIRE(ok(m->tri, 3 * M) && ok(m->tri_orig, 3 * M) && ok(m->inv_d, N) && ok(m->area, M),
+                "mesh arrays not uploaded");
+    MOF_REQUIRE(ok(m->vptr, N + 1) && ok(m->vcol, P.vcol.size()) && ok(m->cptr, P.cptr.size()) &&
+                    ok(m->clist, P.clist.size()) && ok(m->sell_off, P.sell_off.size()) &&
+                    ok(m->sell_col, (size_t)P.sell_nb()) && ok(m->sell_blk, (size_t)P.sell_nb()) &&
+                    ok(m->blk_row, P.blk_row.size()) && ok(m->diag_pos, N) &&
+                    ok(m->tsell_off, P.tsell_off.size()) && ok(m->tinc, 4 * (size_t)P.tsell_nb()),
+                "pattern arrays not uploaded");
+    MOF_REQUIRE(ok(m->e, 6 * N) && ok(m->gw, 9 * M) && ok(m->iw, 2 * M) &&
+                    ok(m->a2, 4 * (size_t)P.sell_nb()) && ok(m->w12_64, M + 1) && ok(m->w12_32, M + 1),
+                "geometry arrays not allocated");
+}
+
 }  // namespace
 
 void launch_geometry(mof_mesh *m, const double *d_xyz, const double *d_nrm, bool f32_points) {
+    check_mesh_arrays(m);
+    MOF_REQUIRE(d_xyz && d_nrm, "NULL coordinates");
     hipStream_t s = m->stream;
     k_basis<<<grid1(m->N), kWG, 0, s>>>(d_nrm, m->N, m->e.p);
     if (f32_points)
@@ -425,8 +454,15 @@ void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
                      bool block_jacobi, uint32_t precision, hipStream_t s) {
     Workspace &w = m->ws;
+    check_mesh_arrays(m);
+    const size_t nbs = (size_t)m->pat.sell_nb(), mu = 6 * ((size_t)m->M + 1) * B;
+    MOF_REQUIRE(B >= 1 && B <= w.cap && I0 && I1 && w.u64.n >= mu && w.u32.n >= mu && w.fc.n >= mu &&
+                    w.dt.n >= (size_t)B && m->a2s_valid,
+                "assembly workspace / operator not prepared");
+    MOF_REQUIRE(precision == MOF_PREC_MIXED ? w.A32.n >= 4 * nbs * B : w.A64.n >= 4 * nbs * B,
+                "assembly target A not allocated");
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), (unsigned)B);
-    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
+    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
                                   w.u64.p, w.u32.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
     dim3 gb((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
@@ -448,7 +484,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
                             hipStream_t s) {
     Workspace &w = m->ws;
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
-    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
+    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
                                   w.u64.p, w.u32.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
@@ -459,7 +495,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
 
 void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s) {
     dim3 g((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
-    k_to_planar<<<g, kWG, 0, s>>>(m->N, m->ws.x64.p, m->ws.sysi.p, V);
+    k_to_planar<<<g, kWG, 0, s>>>(m->N, m->ws.x64.p, m->inv_d.p, m->ws.sysi.p, V);
     MOF_HIP(hipGetLastError());
 }
 

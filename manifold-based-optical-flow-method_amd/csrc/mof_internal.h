@@ -92,7 +92,12 @@ struct Pattern {
     int32_t nblocks() const { return (int32_t)vcol.size(); }
 };
 
-void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat);
+// torder (optional): torder[q] = index in `tri` of the caller's triangle q;
+// contribution lists then follow the caller's triangle order (the order the
+// reference's lil folds), whatever the storage order of `tri`.
+void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat,
+                   const int32_t *torder = nullptr);
+std::vector<int32_t> rcm_order(const Pattern &pat);
 
 // Per-batch device workspace (capacity B systems).
 struct Workspace {
@@ -130,7 +135,14 @@ struct mof_mesh {
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
     mof::Pattern pat;
-    // device mesh data
+    // Internal vertex order: RCM unless MOF_NO_REORDER. perm[old] = new,
+    // inv[new] = old; the API always speaks the caller's (old) order.
+    std::vector<int32_t> perm, inv;
+    // internal triangle order: tperm[internal] = caller's triangle index
+    std::vector<int32_t> tperm, tinv;
+    mof::DevArray<int32_t> inv_d;     // (N) new -> old, for the planar V scatter
+    mof::DevArray<int32_t> tri_orig;  // (M,3) caller's vertex ids, for gathers of I
+    // device mesh data (internal order)
     mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row,
         diag_pos, tsell_off, tinc;
     mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4] (unscaled, bit-exact)
@@ -168,7 +180,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
 // bit-exact A (SELL, fp64) and f of one timestep into m->Aexp / m->fexp
 void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
                             hipStream_t s);
-void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);
+void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);  // V in caller order
 
 struct SpmvTiming {
     int64_t launches = 0;

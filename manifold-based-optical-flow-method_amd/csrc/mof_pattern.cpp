@@ -18,7 +18,7 @@
 
 namespace mof {
 
-void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
+void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat, const int32_t *torder) {
     MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
     MOF_REQUIRE((int64_t)M * 9 < (int64_t)INT32_MAX, "too many triangles for int32 term codes");
     for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
@@ -65,7 +65,8 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
     };
     pat.cptr.assign(nb + 1, 0);
     std::vector<int32_t> term_block(9 * (size_t)M);
-    for (int32_t T = 0; T < M; ++T) {
+    for (int32_t q = 0; q < M; ++q) {
+        const int32_t T = torder ? torder[q] : q;  // caller's triangle order
         const int32_t *v = tri + 3 * (int64_t)T;
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) {
@@ -77,11 +78,13 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
     for (int32_t p = 0; p < nb; ++p) pat.cptr[p + 1] += pat.cptr[p];
     pat.clist.assign(pat.cptr[nb], 0);
     std::vector<int32_t> fill(pat.cptr.begin(), pat.cptr.end() - 1);
-    for (int32_t T = 0; T < M; ++T)
-        for (int q = 0; q < 9; ++q) {
-            int32_t p = term_block[9 * (size_t)T + q];
-            pat.clist[fill[p]++] = 9 * T + q;
+    for (int32_t q = 0; q < M; ++q) {
+        const int32_t T = torder ? torder[q] : q;  // caller's triangle order
+        for (int c = 0; c < 9; ++c) {
+            int32_t p = term_block[9 * (size_t)T + c];
+            pat.clist[fill[p]++] = 9 * T + c;
         }
+    }
 
     // SELL-64
     pat.nslices = (N + kSlice - 1) / kSlice;
@@ -143,15 +146,74 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat) {
         }
     }
     std::vector<int32_t> tfill(N, 0);
-    for (int32_t T = 0; T < M; ++T) {
+    for (int32_t q = 0; q < M; ++q) {
+        const int32_t T = torder ? torder[q] : q;  // caller's triangle order
         const int32_t *v = tri + 3 * (int64_t)T;
         for (int a = 0; a < 3; ++a) {
             const int32_t i = v[a];
             const int32_t t = tfill[i]++;
-            int32_t *q = &pat.tinc[4 * ((int64_t)pat.tsell_off[i / kSlice] + (int64_t)t * kSlice + (i % kSlice))];
-            q[0] = T; q[1] = a; q[2] = v[(a + 1) % 3]; q[3] = v[(a + 2) % 3];
+            int32_t *ent = &pat.tinc[4 * ((int64_t)pat.tsell_off[i / kSlice] + (int64_t)t * kSlice + (i % kSlice))];
+            ent[0] = T; ent[1] = a; ent[2] = v[(a + 1) % 3]; ent[3] = v[(a + 2) % 3];
         }
     }
+}
+
+// Reverse Cuthill-McKee order of the vertex graph in `pat` (adjacency
+// only). Returns perm with perm[old] = new. BFS from a pseudo-peripheral
+// vertex of every connected component, neighbours in increasing degree,
+// then reversed: rows that share columns end up close together, which keeps
+// the SpMV's z gathers inside the L2 of the XCD that owns the row chunk.
+std::vector<int32_t> rcm_order(const Pattern &pat) {
+    const int32_t N = pat.N;
+    std::vector<int32_t> deg(N), order, perm(N, -1);
+    order.reserve(N);
+    for (int32_t i = 0; i < N; ++i) deg[i] = pat.vptr[i + 1] - pat.vptr[i];
+    std::vector<int32_t> level(N, -1), queue;
+    queue.reserve(N);
+    // farthest vertex of a BFS from s (ties: smallest degree); marks nothing
+    auto far = [&](int32_t s) {
+        std::vector<int32_t> seen_list{s};
+        level[s] = 0;
+        size_t h = 0;
+        int32_t last = s;
+        while (h < seen_list.size()) {
+            const int32_t v = seen_list[h++];
+            if (level[v] > level[last] || (level[v] == level[last] && deg[v] < deg[last])) last = v;
+            for (int32_t q = pat.vptr[v]; q < pat.vptr[v + 1]; ++q) {
+                const int32_t w = pat.vcol[q];
+                if (level[w] < 0) {
+                    level[w] = level[v] + 1;
+                    seen_list.push_back(w);
+                }
+            }
+        }
+        for (int32_t v : seen_list) level[v] = -1;
+        return last;
+    };
+    std::vector<char> done(N, 0);
+    std::vector<int32_t> nb;
+    for (int32_t s0 = 0; s0 < N; ++s0) {
+        if (done[s0]) continue;
+        int32_t s = far(far(s0));
+        size_t h = order.size();
+        order.push_back(s);
+        done[s] = 1;
+        while (h < order.size()) {
+            const int32_t v = order[h++];
+            nb.clear();
+            for (int32_t q = pat.vptr[v]; q < pat.vptr[v + 1]; ++q)
+                if (!done[pat.vcol[q]]) nb.push_back(pat.vcol[q]);
+            std::sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) {
+                return deg[a] != deg[b] ? deg[a] < deg[b] : a < b;
+            });
+            for (int32_t w : nb) {
+                done[w] = 1;
+                order.push_back(w);
+            }
+        }
+    }
+    for (int32_t k = 0; k < N; ++k) perm[order[N - 1 - k]] = k;
+    return perm;
 }
 
 }  // namespace mof

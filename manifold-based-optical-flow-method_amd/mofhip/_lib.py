@@ -25,6 +25,7 @@ MOF_E_NOCONV = -3
 MOF_E_STATE = -4
 
 MOF_GEOM_F32_POINTS = 1
+MOF_NO_REORDER = 2
 MOF_PREC_F64 = 0
 MOF_PREC_MIXED = 1
 MOF_IO_DEVICE = 1

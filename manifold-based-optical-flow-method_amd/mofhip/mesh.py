@@ -24,7 +24,8 @@ def _f64(a):
 class DeviceMesh:
     """One triangle mesh, resident on one or more GPUs (one handle each)."""
 
-    def __init__(self, coordinates, normals, triangles, areas, device: int = 0):
+    def __init__(self, coordinates, normals, triangles, areas, device: int = 0,
+                 reorder: bool = True):
         coords = np.asarray(coordinates)
         tri = np.asarray(triangles)
         if coords.ndim != 2 or coords.shape[1] != 3:
@@ -40,6 +41,7 @@ class DeviceMesh:
         self.M = len(self._tri)
         if self._nrm.shape != (self.N, 3) or len(self._area) != self.M:
             raise ValueError("normals must be (N, 3) and areas (M,)")
+        self.reorder = bool(reorder)  # RCM vertex order on the device (results unaffected)
         self._handles = {}
         self._locks = {}
         self._glock = threading.Lock()
@@ -53,7 +55,8 @@ class DeviceMesh:
             h = self._handles.get(device)
             if h is None:
                 h = ctypes.c_void_p()
-                flags = L.MOF_GEOM_F32_POINTS if self.f32_points else 0
+                flags = ((L.MOF_GEOM_F32_POINTS if self.f32_points else 0)
+                         | (0 if self.reorder else L.MOF_NO_REORDER))
                 L.check(L.lib().mof_mesh_create(
                     L.ptr(self._xyz), L.ptr(self._nrm), L.ptr(self._tri), L.ptr(self._area),
                     self.N, self.M, device, flags, ctypes.byref(h)))

@@ -20,6 +20,8 @@ import numpy as np
 
 __all__ = [
     "icosphere",
+    "random_sphere",
+    "permute_vertices",
     "spherical_cap",
     "vertex_normals",
     "triangle_areas",
@@ -124,6 +126,34 @@ def icosphere(n: int, radius: float = 10.0, jitter: float = 0.0, seed: int = 0):
     return pts, tri.astype(np.int32)
 
 
+def random_sphere(n_points: int, radius: float = 10.0, seed: int = 0):
+    """Irregular closed mesh: convex hull of uniformly random points on a
+    sphere (valence varies, vertex order is random), outward oriented.
+    Stands in for reconstructed cortical surfaces, whose valence and vertex
+    order are not the icosphere's."""
+    from scipy.spatial import ConvexHull
+    rng = np.random.default_rng(seed)
+    p = rng.normal(size=(n_points, 3))
+    p /= np.linalg.norm(p, axis=1, keepdims=True)
+    hull = ConvexHull(p)
+    t = hull.simplices.astype(np.int64)
+    c = np.cross(p[t[:, 1]] - p[t[:, 0]], p[t[:, 2]] - p[t[:, 0]])
+    flip = (c * p[t].mean(axis=1)).sum(axis=1) < 0
+    t[flip] = t[flip][:, [0, 2, 1]]
+    return p * radius, t.astype(np.int32)
+
+
+def permute_vertices(points, triangles, seed: int = 0):
+    """The same mesh with its vertices relabelled by a random permutation
+    (locality stress test). Returns (points, triangles, perm) with
+    new_points[perm[i]] = points[i]."""
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(len(points))
+    out = np.empty_like(points)
+    out[perm] = points
+    return out, perm[np.asarray(triangles)].astype(np.int32), perm
+
+
 def spherical_cap(n: int = 16, radius: float = 10.0, zcut: float = 0.5):
     """Open cap: the triangles of ``icosphere(n)`` whose three vertices all have
     z > zcut * radius, re-indexed (the G2 boundary case)."""
@@ -169,7 +199,16 @@ def travelling_wave(points: np.ndarray, T: int, kappa: float = 3.0,
 def mesh_for_config(name: str):
     """(points, triangles, normals, areas) of a SURVEY.md §8d config mesh.
 
-    C1 has no jitter; the >=32k meshes get 0.5 % radial jitter, seed 0."""
+    C1 has no jitter; the >=32k meshes get 0.5 % radial jitter, seed 0.
+    R3 is an irregular 163,842-vertex random-hull sphere, P3 the C3 mesh
+    with randomly relabelled vertices (locality stress cases)."""
+    if name == "R3":
+        p, t = random_sphere(163842, 10.0, seed=0)
+        return p, t, vertex_normals(p, t), triangle_areas(p, t)
+    if name == "P3":
+        p, t, _, _ = mesh_for_config("C3")
+        p, t, _ = permute_vertices(p, t, seed=1)
+        return p, t, vertex_normals(p, t), triangle_areas(p, t)
     n = CONFIG_FREQ[name]
     jitter = 0.0 if name == "C1" else 0.005
     p, t = icosphere(n, 10.0, jitter=jitter, seed=0)
