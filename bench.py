@@ -55,6 +55,19 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(key, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, made by profiles/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of this bench at the same
+    config; read bytes = 2 x FETCH_SIZE on gfx950). None if not measured."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        entry = json.load(open(path))[key]
+        return round(entry["kernels"][kernel]["hbm_bytes_per_launch"]), entry["source"][0]
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def cpu_baseline(p, t, n, a, lam, frac):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
     host on a bounded sample: Pool(C) runs C timesteps; each assembles the
@@ -155,9 +168,11 @@ def main():
 
     # roofline of the dominant kernel (k_pcg_spmv), live over the timed region
     achieved = agg["spmv_bytes"] / (agg["ms_spmv"] * 1e-3) / 1e9 if agg["ms_spmv"] > 0 else 0.0
+    kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
+    traffic, traffic_src = pmc_traffic("%s/%s/B%d" % (args.config, precision, B), kname)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_pcg_spmv<%s>" % ("float" if precision == "mixed" else "double"),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": traffic_src, "kernel": kname,
                 "bytes_per_launch": round(agg["spmv_bytes"] / max(1, agg["spmv_launches"])),
                 "us_per_launch": round(1e3 * agg["ms_spmv"] / max(1, agg["spmv_launches"]), 2),
                 "launches": agg["spmv_launches"]}
