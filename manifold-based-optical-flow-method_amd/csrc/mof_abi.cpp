@@ -176,8 +176,8 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
             m->tri.upload(tri_new.data(), 3 * (size_t)M, s);
             m->tri_orig.alloc(3 * (size_t)M);
             m->tri_orig.upload(tri_old.data(), 3 * (size_t)M, s);
-            m->inv_d.alloc(N);
-            m->inv_d.upload(m->inv.data(), N, s);
+            m->perm_d.alloc(N);
+            m->perm_d.upload(m->perm.data(), N, s);
             m->area.alloc(M);
             m->area.upload(area_new.data(), M, s);
             auto put = [&](mof::DevArray<int32_t> &d, const std::vector<int32_t> &h) {

@@ -383,18 +383,18 @@ __global__ __launch_bounds__(kWG) void k_assemble_export(
 }
 
 // x64 (interleaved, internal order) -> V (B, 2N) planar in the caller's
-// vertex order; failed systems are NaN-filled.
+// vertex order (one caller vertex per thread: gathered reads, coalesced
+// writes); failed systems are NaN-filled.
 __global__ __launch_bounds__(kWG) void k_to_planar(int32_t N, const double *__restrict__ x,
-                                                   const int32_t *__restrict__ inv,
+                                                   const int32_t *__restrict__ perm,
                                                    const int32_t *__restrict__ sysi,
                                                    double *__restrict__ V) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t o = blockIdx.x * kWG + threadIdx.x;
     const int32_t b = blockIdx.y;
-    if (i >= N) return;
+    if (o >= N) return;
     const bool failed = sysi[b * kSysStride + SI_FAILED] != 0;
-    const double2 v = *reinterpret_cast<const double2 *>(x + 2 * ((int64_t)b * N + i));
+    const double2 v = *reinterpret_cast<const double2 *>(x + 2 * ((int64_t)b * N + perm[o]));
     const double nan = __builtin_nan("");
-    const int32_t o = inv[i];
     V[(int64_t)b * 2 * N + o] = failed ? nan : v.x;
     V[(int64_t)b * 2 * N + N + o] = failed ? nan : v.y;
 }
@@ -408,7 +408,7 @@ void check_mesh_arrays(const mof_mesh *m) {
     const Pattern &P = m->pat;
     const size_t N = m->N, M = m->M;
     auto ok = [](const auto &d, size_t n) { return d.p != nullptr && d.n >= n; };
-    MOF_REQUIRE(ok(m->tri, 3 * M) && ok(m->tri_orig, 3 * M) && ok(m->inv_d, N) && ok(m->area, M),
+    MOF_REQUIRE(ok(m->tri, 3 * M) && ok(m->tri_orig, 3 * M) && ok(m->perm_d, N) && ok(m->area, M),
                 "mesh arrays not uploaded");
     MOF_REQUIRE(ok(m->vptr, N + 1) && ok(m->vcol, P.vcol.size()) && ok(m->cptr, P.cptr.size()) &&
                     ok(m->clist, P.clist.size()) && ok(m->sell_off, P.sell_off.size()) &&
@@ -495,7 +495,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
 
 void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s) {
     dim3 g((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
-    k_to_planar<<<g, kWG, 0, s>>>(m->N, m->ws.x64.p, m->inv_d.p, m->ws.sysi.p, V);
+    k_to_planar<<<g, kWG, 0, s>>>(m->N, m->ws.x64.p, m->perm_d.p, m->ws.sysi.p, V);
     MOF_HIP(hipGetLastError());
 }
 

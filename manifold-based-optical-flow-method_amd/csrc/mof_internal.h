@@ -140,7 +140,7 @@ struct mof_mesh {
     std::vector<int32_t> perm, inv;
     // internal triangle order: tperm[internal] = caller's triangle index
     std::vector<int32_t> tperm, tinv;
-    mof::DevArray<int32_t> inv_d;     // (N) new -> old, for the planar V scatter
+    mof::DevArray<int32_t> perm_d;    // (N) old -> new, for the planar V gather
     mof::DevArray<int32_t> tri_orig;  // (M,3) caller's vertex ids, for gathers of I
     // device mesh data (internal order)
     mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row,
