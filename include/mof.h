@@ -152,6 +152,17 @@ int mof_solve_range(mof_mesh *mesh, const double *I, const double *I2,
                     double lambda, const mof_opts *opts, double *V_out,
                     mof_stats *stats);
 
+/* Replaces S3's epilogue: find_singularity_point.process_V_k(V_k, e)
+ * (find_singularity_point.py:28-69: V_coord[k][i] = V[k][i] e_i^0 +
+ * V[k][i+N] e_i^1) and the speed V_c = sqrt(sum(V_coord**2, axis=2))
+ * (S3…py:130-132), bit-identical to numpy. e (N,2,3), V (K,2N) planar,
+ * V_coord (K,N,3), speed (K,N); either output may be NULL. Host pointers, or
+ * device pointers with MOF_IO_DEVICE in flags (stream: hipStream_t or NULL).
+ * Needs no mesh handle. */
+int mof_velocity_vectors(int32_t device, const double *e, const double *V, int32_t N,
+                         int32_t K, double *V_coord, double *speed, uint32_t flags,
+                         void *stream);
+
 /* Measurement helper for bench.py: launches the PCG SpMV kernel `reps` times
  * back to back on `batch` systems of the last solve's working set, timed with
  * HIP events on the handle's stream. Returns the mean launch time and the

@@ -426,6 +426,38 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
     return rc;
 }
 
+int mof_velocity_vectors(int32_t device, const double *e, const double *V, int32_t N, int32_t K,
+                         double *V_coord, double *speed, uint32_t flags, void *stream) {
+    return guarded([&] {
+        MOF_REQUIRE(e && V && N > 0 && K >= 0, "bad arguments");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DeviceGuard dg(device);
+        if (K == 0 || (!V_coord && !speed)) return;
+        hipStream_t s = (hipStream_t)stream;
+        if (flags & MOF_IO_DEVICE) {
+            mof::launch_velocity_vectors(N, K, e, V, V_coord, speed, s);
+            MOF_HIP(hipStreamSynchronize(s));
+            return;
+        }
+        const size_t nk = (size_t)N * K;
+        mof::DevArray<double> de, dV, dc, dsp;
+        de.alloc(6 * (size_t)N);
+        de.upload(e, 6 * (size_t)N, s);
+        dV.alloc(2 * nk);
+        dV.upload(V, 2 * nk, s);
+        if (V_coord) dc.alloc(3 * nk);
+        if (speed) dsp.alloc(nk);
+        mof::launch_velocity_vectors(N, K, de.p, dV.p, V_coord ? dc.p : nullptr,
+                                     speed ? dsp.p : nullptr, s);
+        if (V_coord)
+            MOF_HIP(hipMemcpyAsync(V_coord, dc.p, 3 * nk * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (speed) MOF_HIP(hipMemcpyAsync(speed, dsp.p, nk * sizeof(double), hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipStreamSynchronize(s));
+    });
+}
+
 int mof_bench_spmv(mof_mesh *m, uint32_t precision, int32_t batch, int32_t reps,
                    double *ms_per_launch, double *bytes_per_launch) {
     return guarded([&] {

@@ -399,6 +399,30 @@ __global__ __launch_bounds__(kWG) void k_to_planar(int32_t N, const double *__re
     V[(int64_t)b * 2 * N + N + o] = failed ? nan : v.y;
 }
 
+// S3's epilogue (find_singularity_point.py:28-69, S3…py:130-132): the 3-D
+// tangent vector V^0 e^0 + V^1 e^1 of every vertex and its length, with
+// numpy's roundings (products, then sums; |v| = sqrt((x^2 + y^2) + z^2)).
+__global__ __launch_bounds__(kWG) void k_velocity_vectors(int32_t N, int64_t total,
+                                                          const double *__restrict__ e,
+                                                          const double *__restrict__ V,
+                                                          double *__restrict__ Vc,
+                                                          double *__restrict__ speed) {
+    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (q >= total) return;
+    const int64_t k = q / N;
+    const int32_t i = (int32_t)(q - k * N);
+    const double v0 = V[2 * k * N + i], v1 = V[2 * k * N + N + i];
+    const double *ei = e + 6 * (int64_t)i;
+    double c[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) c[d] = v0 * ei[d] + v1 * ei[3 + d];
+    if (Vc) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Vc[3 * q + d] = c[d];
+    }
+    if (speed) speed[q] = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+}
+
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
 
 // Host-side guard before any launch: every device array a kernel indexes is
@@ -490,6 +514,14 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
                                                  m->vcol.p, m->cptr.p, m->clist.p, m->iw.p, m->a2.p,
                                                  w.u64.p, w.fc.p, lambda, m->Aexp.p, m->fexp.p);
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double *V, double *Vc,
+                             double *speed, hipStream_t s) {
+    const int64_t total = (int64_t)N * K;
+    if (total == 0) return;
+    k_velocity_vectors<<<grid1(total), kWG, 0, s>>>(N, total, e, V, Vc, speed);
     MOF_HIP(hipGetLastError());
 }
 

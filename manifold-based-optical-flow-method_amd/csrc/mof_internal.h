@@ -181,6 +181,8 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
 void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
                             hipStream_t s);
 void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);  // V in caller order
+void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double *V, double *Vc,
+                             double *speed, hipStream_t s);
 
 struct SpmvTiming {
     int64_t launches = 0;

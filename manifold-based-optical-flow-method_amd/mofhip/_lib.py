@@ -38,7 +38,7 @@ MOF_CSR_A_LAST = 1
 EXPORTS = (
     "mof_version", "mof_last_error", "mof_device_count", "mof_mesh_create",
     "mof_mesh_destroy", "mof_mesh_get_info", "mof_geometry_export", "mof_csr_export",
-    "mof_assemble", "mof_solve_range", "mof_bench_spmv",
+    "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
 )
 
 
@@ -126,6 +126,7 @@ def lib():
             "mof_assemble": ([P, P, P, f64, f64, P], ctypes.c_int),
             "mof_solve_range": ([P, P, P, P, i32, i32, i32, f64, P, P, P], ctypes.c_int),
             "mof_bench_spmv": ([P, u32, i32, i32, P, P], ctypes.c_int),
+            "mof_velocity_vectors": ([i32, P, P, i32, i32, P, P, u32, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

@@ -13,6 +13,9 @@ Cases:
   G3 G1 with float32 coordinates/normals (pyvista dtype fidelity), T=4
   G4 compute_velocity_field with processes_num=2 (list order and shape), T=6
   G5 G1 with t_k = i/512 (S3's t_k = i/SF convention), T=4
+  G6 S3's epilogue on G1's V_k: find_singularity_point.process_V_k(V_k, e)
+     (find_singularity_point.py:28-69) and the speed
+     V_c = sqrt(sum(V_k_coord[:, :, :3] ** 2, axis=2)) (S3…py:130-132)
 
 Run:  python tests/golden/make_golden.py
 """
@@ -34,12 +37,12 @@ from mofhip import synth  # noqa: E402
 REF = "/root/reference"
 
 
-def load_reference():
+def load_reference(name="utils.compute_optical_flow"):
     sys.dont_write_bytecode = True
     sys.modules.setdefault("pyvista", types.ModuleType("pyvista"))
     sys.path.insert(0, REF)
     import importlib
-    mod = importlib.import_module("utils.compute_optical_flow")
+    mod = importlib.import_module(name)
     sys.path.remove(REF)
     return mod
 
@@ -107,6 +110,17 @@ def main():
     run_case(ref, "G4_pool2", p, t, n, a, I[:6], list(range(6)), processes_num=2)
     # G5: t_k = i / SF
     run_case(ref, "G5_dt512", p, t, n, a, I[:4], [i / 512 for i in range(4)], capture_ks=(0,))
+    # G6: S3's epilogue on G1's velocity fields
+    import contextlib
+    import io
+    fsp = load_reference("utils.find_singularity_point")
+    g1 = np.load(os.path.join(HERE, "G1_ico642.npz"))
+    with contextlib.redirect_stdout(io.StringIO()):
+        coord = np.array(fsp.process_V_k(list(g1["V_k"]), g1["e"]))
+    V_c = np.sqrt(np.sum(coord[:, :, :3] ** 2, axis=2))  # S3…py:132
+    np.savez_compressed(os.path.join(HERE, "G6_epilogue.npz"), V_k=g1["V_k"], e=g1["e"],
+                        V_k_coord=coord, V_c=V_c)
+    print("G6_epilogue", coord.shape, V_c.shape)
 
 
 if __name__ == "__main__":

@@ -229,3 +229,40 @@ def test_160k_properties():
     A, f = m.assemble(I[1], I[2], 1.0, 0.01)
     r = f - A @ V64[1]
     assert np.linalg.norm(r) <= 1e-8 * np.linalg.norm(f) * 1.01
+
+
+def test_epilogue_bitexact():
+    """S3's epilogue (process_V_k + speed) vs the reference's, bit for bit."""
+    from mofhip.epilogue import velocity_vectors
+    from utils import find_singularity_point as fsp
+    g = load_golden("G6_epilogue")
+    coord, speed = velocity_vectors(g["V_k"], g["e"])
+    assert np.array_equal(coord, g["V_k_coord"])
+    assert np.array_equal(speed, g["V_c"])
+    assert np.array_equal(np.array(fsp.process_V_k(list(g["V_k"]), g["e"])), g["V_k_coord"])
+    c1, s1 = velocity_vectors(g["V_k"][3], g["e"])  # single timestep
+    assert np.array_equal(c1[0], g["V_k_coord"][3]) and np.array_equal(s1[0], g["V_c"][3])
+
+
+def test_s3_sequence_dropin(tmp_path):
+    """S3's call sequence (S3…py:97-137) on the drop-in modules: geometry,
+    velocity fields, CSV writers, epilogue; outputs match the reference's."""
+    import pandas as pd
+    from utils import compute_optical_flow as cof
+    from utils import find_singularity_point as fsp
+    g = load_golden("G1_ico642")
+    g6 = load_golden("G6_epilogue")
+    a2, gw, e, iw, _ = cof.compute_geometrical_quantities(g["coordinates"], g["normals"],
+                                                          g["triangles"], g["areas"])
+    T = len(g["I"])
+    V_k, _ = cof.compute_velocity_field(32, T, a2, gw, e, iw, g["triangles"], list(g["t_k"]),
+                                        g["areas"], float(g["lambda_"]), g["I"], g["I"])
+    cof.reshape_and_save_data(e, str(tmp_path / "e.csv"))
+    cof.reshape_and_save_data(V_k, str(tmp_path / "V_k.csv"))
+    # pandas' default CSV float parser is not exactly round-trip (<= 1 ulp)
+    assert np.abs(cof.load_potentials(str(tmp_path / "e.csv")) - g["e"].reshape(len(e), 6)).max() < 1e-15
+    assert np.abs(cof.load_potentials(str(tmp_path / "V_k.csv")) - g["V_k"]).max() < VTOL
+    V_k_coord = np.array(fsp.process_V_k(V_k, e))
+    V_c = np.sqrt(np.sum(V_k_coord[:, :, :3] ** 2, axis=2))
+    assert V_c.shape == g6["V_c"].shape
+    assert np.abs(V_c - g6["V_c"]).max() < VTOL
