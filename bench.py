@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=16, help="timesteps per step")
     ap.add_argument("--config", default="C3", choices=sorted(CONFIG_NAMES))
     ap.add_argument("--precision", default=None, choices=["mixed", "f64"])
+    ap.add_argument("--precond", default="jacobi", choices=["jacobi", "amg"],
+                    help="inner preconditioner (amg: mixed precision only)")
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 64,
@@ -136,7 +138,8 @@ def main():
     V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(K_rank + 1, dtype=np.float64)
     torch.cuda.synchronize(dev)
-    opts = dict(precision=precision, batch=B, rtol=args.rtol)
+    opts = dict(precision=precision, batch=B, rtol=args.rtol,
+                precond=args.precond if precision == "mixed" else "jacobi")
 
     def step(s, timed):
         return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), K_rank + 1, tk, s * B,
@@ -193,6 +196,7 @@ def main():
             "data": "synthetic travelling wave sin(3 phi - 0.3 k), dt = 1, lambda = 0.01",
             "config": {"workload": CONFIG_NAMES[args.config], "vertices": N, "triangles": len(t),
                        "timesteps_per_step": B, "timesteps_timed": n_ts, "precision": precision,
+                       "precond": opts["precond"],
                        "rtol": args.rtol, "parallelism": "timestep shards x%d" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,

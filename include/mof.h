@@ -56,6 +56,10 @@ extern "C" {
 #define MOF_NO_BLOCK_JACOBI 2u /* scalar Jacobi instead of 2x2 block Jacobi */
 #define MOF_TIME_SPMV 4u       /* bracket every PCG SpMV launch with HIP events
                                   (fills mof_stats.ms_spmv / spmv_bytes) */
+#define MOF_PRECOND_AMG 8u     /* MOF_PREC_MIXED: aggregation-multigrid V(1,1)
+                                  preconditioner for the inner PCG (built
+                                  once per mesh; meshes of <= 64 vertices
+                                  keep block Jacobi) */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */
@@ -66,7 +70,7 @@ typedef struct mof_mesh mof_mesh;
 typedef struct mof_opts {
     uint32_t struct_size;  /* sizeof(mof_opts) */
     uint32_t precision;    /* MOF_PREC_* */
-    uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI */
+    uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI | MOF_TIME_SPMV | MOF_PRECOND_AMG */
     int32_t batch;         /* timesteps solved together per launch (0: auto) */
     int32_t max_iter;      /* PCG iterations per inner solve (0: 10000) */
     int32_t max_outer;     /* refinement steps, MOF_PREC_MIXED (0: 10) */

@@ -236,6 +236,8 @@ int mof_mesh_destroy(mof_mesh *m) {
             if (m->h_sysi) (void)hipHostFree(m->h_sysi);
             if (m->h_sysd) (void)hipHostFree(m->h_sysd);
             for (auto e : m->spmv_events) (void)hipEventDestroy(e);
+            mof::amg_destroy(m->amg);
+            m->amg = nullptr;
             if (m->stream) (void)hipStreamDestroy(m->stream);
             m->stream = nullptr;
             delete m;  // DevArray destructors free on the current (guarded) device
@@ -351,7 +353,10 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         MOF_REQUIRE(o.precision == MOF_PREC_F64 || o.precision == MOF_PREC_MIXED, "unknown precision");
         mof::SolveParams sp;
         sp.precision = o.precision;
-        sp.block_jacobi = !(o.flags & MOF_NO_BLOCK_JACOBI);
+        sp.amg = (o.flags & MOF_PRECOND_AMG) != 0;
+        MOF_REQUIRE(!sp.amg || o.precision == MOF_PREC_MIXED, "MOF_PRECOND_AMG needs MOF_PREC_MIXED");
+        // the multigrid smoother is the 2x2 block Jacobi
+        sp.block_jacobi = sp.amg || !(o.flags & MOF_NO_BLOCK_JACOBI);
         sp.time_spmv = (o.flags & MOF_TIME_SPMV) != 0;
         mof::SpmvTiming timing;
         sp.max_iter = o.max_iter > 0 ? o.max_iter : 10000;

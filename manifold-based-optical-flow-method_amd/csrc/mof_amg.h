@@ -1,0 +1,68 @@
+// mof_amg.h -- aggregation multigrid preconditioner (host hierarchy + device levels).
+#pragma once
+
+#include <deque>
+
+#include "mof_internal.h"
+
+namespace mof {
+
+struct AmgParams {
+    int32_t max_levels = 10;
+    int32_t max_coarse_dofs = 128;  // coarsest level: dense inverse in LDS (fp64), one workgroup per system
+    float omega = 0.7f;             // damped block-Jacobi smoother
+};
+
+// One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser
+// levels have 3 dofs per node. The transition fields (agg ... gent) describe
+// the restriction to the next level and are empty on the coarsest level.
+struct AmgLevel {
+    int32_t n = 0, bs = 0;
+    std::vector<int32_t> vptr, vcol;               // block adjacency (self included, sorted)
+    std::vector<int32_t> sell_off, sell_col, sell_blk, diag_pos;  // SELL-64 block layout
+    std::vector<int32_t> sell_row;                 // row of each SELL position
+    std::vector<uint8_t> dead;                     // (n*3) dofs without a prolongator column
+    // transition to level + 1
+    std::vector<int32_t> agg;                      // (n) aggregate of each node
+    std::vector<int32_t> mptr, mlist;              // aggregate members, CSR
+    std::vector<int32_t> apos;                     // (n) position of node i in mlist
+    std::vector<float> Q;                          // (n, bs, 3) tentative prolongator rows
+    std::vector<float> Qm;                         // the same rows in member (mlist) order
+    std::vector<int32_t> gptr;                     // (next sell_nb + 1) Galerkin gather ranges
+    std::vector<int32_t> gent;                     // triples {fine SELL pos, i, j}
+    int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
+};
+
+struct AmgHierarchy {
+    std::vector<AmgLevel> levels;
+    int32_t coarse_dofs = 0;
+};
+
+void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,
+               AmgHierarchy &H);
+
+// Device copy of a level. Level 0 borrows the mesh's SELL arrays and the
+// inner solver's A32 / dinv32 / r / z; it owns only its smoother scratch.
+struct AmgDevLevel {
+    int32_t n = 0, bs = 0;
+    int64_t sell_nb = 0;
+    DevArray<int32_t> sell_off, sell_col, sell_row, diag_pos;  // level >= 1
+    DevArray<uint8_t> dead;                          // level >= 1
+    DevArray<int32_t> agg, mptr, apos, gptr, gent;  // transition to level + 1
+    DevArray<float> Q, Qm;
+    // per system, capacity AmgDevice::cap
+    DevArray<float> A, Dinv;     // [B][sell_nb][12], [B][n][12] (level >= 1)
+    DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x, r [B][n][2]
+                                 // r is stored in member order of the next level
+};
+
+struct AmgDevice {
+    bool built = false;
+    int32_t cap = 0;
+    int32_t nc = 0;  // coarsest dofs (dense)
+    float omega = 0.7f;
+    std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
+    DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
+};
+
+}  // namespace mof

@@ -127,6 +127,8 @@ enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3 };
 enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_ITERS = 3 };
 constexpr int kSysStride = 8;
 
+struct AmgDevice;  // mof_amg.h
+
 }  // namespace mof
 
 // The opaque handle of the C ABI.
@@ -164,6 +166,8 @@ struct mof_mesh {
     std::vector<hipEvent_t> spmv_events;
     // PCG iterations the previous batch needed, per (precision, outer step)
     std::vector<int32_t> iter_hint;
+    // aggregation multigrid hierarchy (MOF_PRECOND_AMG), built on first use
+    mof::AmgDevice *amg = nullptr;
 };
 
 namespace mof {
@@ -197,6 +201,7 @@ struct SolveParams {
     uint32_t precision;
     bool block_jacobi;
     bool time_spmv;
+    bool amg;  // mixed precision only: multigrid V-cycle preconditioner
     int32_t max_iter, max_outer;
     double rtol, inner_rtol;
 };
@@ -205,6 +210,19 @@ struct SolveParams {
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
                     int32_t *max_iters, SpmvTiming *timing);
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision);
+// aggregation multigrid preconditioner (mof_amg.hip)
+bool amg_build(mof_mesh *m);  // hierarchy from the mesh (once); false: mesh too small
+void amg_ensure(mof_mesh *m, int32_t B);            // per-system storage
+void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s);  // Galerkin + coarse inverse
+// z = V-cycle(r) on the fp32 inner vectors; writes partial r.z (component 0)
+// into the part_rzrr slot `part_slot`
+void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_slot, int32_t nblk,
+                hipStream_t s);
+void amg_destroy(AmgDevice *g);
+float *amg_level0_x(mof_mesh *m);  // level-0 smoother vector (pre-smoothed x0)
+float amg_omega(const mof_mesh *m);
+int32_t amg_levels(const mof_mesh *m);
+
 double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,
                   double *bytes);
 

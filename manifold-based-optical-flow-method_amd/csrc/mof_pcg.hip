@@ -34,85 +34,10 @@
 #include <cmath>
 
 #include "mof_internal.h"
+#include "mof_rowkern.h"
 
 namespace mof {
 namespace {
-
-template <typename V>
-struct VT;
-template <>
-struct VT<float> {
-    using V2 = float2;
-};
-template <>
-struct VT<double> {
-    using V2 = double2;
-};
-
-// Row kernels: a workgroup covers kRows groups of 256 consecutive vertex rows
-// (thread t takes rows base + 256 r + t, so every group stays 4 whole SELL
-// slices and every access stays coalesced). Fewer, larger workgroups keep the
-// per-workgroup partial sums short: each workgroup of the next launch re-reads
-// all nblk partials of its system, nblk = ceil(N / (256 kRows)).
-constexpr int kRows = 4;
-constexpr int kRowsPerWG = kWG * kRows;
-
-__device__ __forceinline__ void ld_blk(const float *A, int64_t pos, float (&a)[4]) {
-    const float4 v = reinterpret_cast<const float4 *>(A)[pos];
-    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-}
-__device__ __forceinline__ void ld_blk(const double *A, int64_t pos, double (&a)[4]) {
-    const double2 v0 = reinterpret_cast<const double2 *>(A)[2 * pos];
-    const double2 v1 = reinterpret_cast<const double2 *>(A)[2 * pos + 1];
-    a[0] = v0.x; a[1] = v0.y; a[2] = v1.x; a[3] = v1.y;
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    return v;  // valid in lane 0
-}
-
-// Deterministic workgroup sum of NV values; every thread gets the result.
-template <int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = ((lds[k] + lds[NV + k]) + lds[2 * NV + k]) + lds[3 * NV + k];
-    __syncthreads();
-}
-
-// Sum n partials of NV values each (record stride NV) in a fixed order.
-template <int NV>
-__device__ __forceinline__ void reduce_partials(const double *part, int n, double (&out)[NV],
-                                                double *lds) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) out[k] = 0.0;
-    int q = threadIdx.x;
-    for (; q + 3 * kWG < n; q += 4 * kWG) {  // four independent loads in flight
-        double v[4][NV];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) v[u][k] = part[(int64_t)(q + u * kWG) * NV + k];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) out[k] += v[u][k];
-    }
-    for (; q < n; q += kWG) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) out[k] += part[(int64_t)q * NV + k];
-    }
-    block_sum<NV>(out, lds);
-}
 
 // The operator of B systems sharing a mesh.
 template <typename V>
@@ -126,14 +51,6 @@ struct OpArgs {
     const V *u;                          // [B][M+1][6] u_T per system (slot M = 0)
 };
 
-// Materialised A of B systems (inner PCG operator).
-template <typename V>
-struct MatArgs {
-    int64_t sell_nb;
-    const int32_t *sell_off, *sell_col;
-    const V *A;  // [B][sell_nb][4]
-};
-
 template <typename V>
 struct PcgArgs {
     int32_t N, nblk, B;
@@ -144,55 +61,10 @@ struct PcgArgs {
     double *part_rzrr;     // [2][B][nblk][2]
     double *sysd;          // [B][8]
     int32_t *sysi;         // [B][8]
+    int32_t ext;           // z and r.z come from an external preconditioner (AMG)
+    V *x0;                 // ext: pre-smoothed x0 = omega D^-1 r for the V-cycle
+    V omega;
 };
-
-template <typename V>
-__device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
-    return *reinterpret_cast<const typename VT<V>::V2 *>(p);
-}
-
-// y_i = sum_t A_blk(i,t) x_col(i,t) over the SELL-64 row of vertex i.
-// Slots are processed U at a time with every load of a chunk issued before
-// the first use (column indices, then block values, then the x gathers), so
-// a row costs two memory round trips instead of two per slot. Slots past
-// the slice width re-load the last valid slot and are masked out, keeping
-// every load unconditional.
-template <typename V>
-__device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
-                                         const V *__restrict__ x, V &y0, V &y1) {
-    using V2 = typename VT<V>::V2;
-    constexpr int U = sizeof(V) == 4 ? 8 : 4;
-    const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
-    const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = mt.sell_off[s];
-    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
-    V a0 = 0, a1 = 0;
-    for (int32_t t0 = 0; t0 < w; t0 += U) {
-        int32_t j[U];
-        V blk[U][4];
-        V2 xj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t t = min(t0 + u, w - 1);
-            j[u] = mt.sell_col[(int64_t)o + t * kSlice + l];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t t = min(t0 + u, w - 1);
-            ld_blk(A, (int64_t)o + t * kSlice + l, blk[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) xj[u] = ld2(x + 2 * (int64_t)j[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool on = t0 + u < w;
-            a0 += on ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : (V)0;
-            a1 += on ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : (V)0;
-        }
-    }
-    y0 = a0;
-    y1 = a1;
-}
 
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
@@ -265,22 +137,6 @@ __device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int
     y1 = a1;
 }
 
-// XCD-aware workgroup -> (row block, system): workgroups w and w+8 share an
-// XCD (round-robin dispatch; speed only, never correctness). XCD x takes row
-// blocks [x*chunk, (x+1)*chunk) of every system, system by system.
-__device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, int32_t &sys) {
-    const int32_t w = blockIdx.x;
-    const int32_t q = w >> 3;
-    const int32_t chunk = (nblk + 7) >> 3;
-    sys = q / chunk;
-    rb = (w & 7) * chunk + q % chunk;
-    return rb < nblk && sys < B;
-}
-
-inline unsigned xcd_grid(int32_t nblk, int32_t B) {
-    return (unsigned)(8 * B * ((nblk + 7) / 8));
-}
-
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
 
 template <typename V>
@@ -297,12 +153,16 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
         const int64_t vi = (int64_t)b * a.N + i;
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
         const V r0 = (V)f.x, r1 = (V)f.y;
+        *reinterpret_cast<V2 *>(a.r + 2 * vi) = V2{r0, r1};
+        *reinterpret_cast<V2 *>(a.x + 2 * vi) = V2{(V)0, (V)0};
         const V *d = a.dinv + 4 * vi;
         const V z0 = d[0] * r0 + d[1] * r1, z1 = d[2] * r0 + d[3] * r1;
-        *reinterpret_cast<V2 *>(a.r + 2 * vi) = V2{r0, r1};
-        *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
-        *reinterpret_cast<V2 *>(a.x + 2 * vi) = V2{(V)0, (V)0};
-        rz += (double)r0 * z0 + (double)r1 * z1;
+        if (!a.ext) {
+            *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
+            rz += (double)r0 * z0 + (double)r1 * z1;
+        } else {
+            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * z0, a.omega * z1};
+        }
         rr += (double)r0 * r0 + (double)r1 * r1;
     }
     double v[2] = {rz, rr};
@@ -419,17 +279,21 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
         const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
         V2 xi = *reinterpret_cast<const V2 *>(a.x + 2 * vi);
         V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
-        V d[4];
-        ld_blk(a.dinv, vi, d);
         xi.x += alpha * pi.x;
         xi.y += alpha * pi.y;
         ri.x -= alpha * qi.x;
         ri.y -= alpha * qi.y;
-        const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
-        *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
-        rz += (double)ri.x * z0 + (double)ri.y * z1;
+        V d[4];
+        ld_blk(a.dinv, vi, d);
+        const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
+        if (!a.ext) {
+            *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
+            rz += (double)ri.x * z0 + (double)ri.y * z1;
+        } else {
+            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * z0, a.omega * z1};
+        }
         rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
     }
     double v[2] = {rz, rr};
@@ -584,6 +448,9 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.part_rzrr = w.part_rzrr.p;
     a.sysd = w.sysd.p;
     a.sysi = w.sysi.p;
+    a.ext = 0;
+    a.x0 = nullptr;
+    a.omega = (V)0;
     return a;
 }
 
@@ -599,12 +466,26 @@ void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
 template <typename V>
 int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
             double rtol, int32_t max_iter, hipStream_t s, int32_t *max_iters, uint32_t precision,
-            SpmvTiming *timing, int32_t *hint) {
+            SpmvTiming *timing, int32_t *hint, bool amg) {
     PcgArgs<V> a = make_args<V>(m, B, mat, dinv);
+    a.ext = amg ? 1 : 0;
+    if constexpr (sizeof(V) == 4) {
+        if (amg) {
+            a.x0 = amg_level0_x(m);
+            a.omega = amg_omega(m);
+        }
+    }
+    const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
+    // z = M^-1 r for the external preconditioner, r.z into slot `slot`
+    auto precond = [&](int32_t slot) {
+        if constexpr (sizeof(V) == 4)
+            amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, s);
+    };
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B));
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol);
+    if (amg) precond(0);
     MOF_HIP(hipGetLastError());
     // systems active at the start of this solve: the host mirror is current
     // (reset by solve_batch, refreshed by every outer check)
@@ -642,6 +523,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(a, it, 0);
             if (timing) MOF_HIP(hipEventRecord(ev[2 * c + 1], s));
             k_pcg_update<V><<<g, kWG, 0, s>>>(a, it);
+            if (amg) precond((it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -765,6 +647,11 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         si[SI_CONV] = -1;
     }
     if (m->iter_hint.size() < 2 * 16) m->iter_hint.assign(2 * 16, 0);
+    const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && amg_build(m);
+    if (amg) {
+        amg_ensure(m, B);
+        amg_setup_batch(m, B, s);
+    }
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
     int64_t iters = 0;
@@ -775,13 +662,13 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         if (sp.precision == MOF_PREC_MIXED) {
             iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol,
                                 sp.max_iter, s, max_iters, sp.precision, tm,
-                                &m->iter_hint[16 + std::min(o, 15)]);
+                                &m->iter_hint[16 + std::min(o, 15)], amg);
             k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
                                                     w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s, max_iters,
-                                 sp.precision, tm, &m->iter_hint[std::min(o, 15)]);
+                                 sp.precision, tm, &m->iter_hint[std::min(o, 15)], false);
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         k_residual<<<g, kWG, 0, s>>>(o64, w.nblk, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);

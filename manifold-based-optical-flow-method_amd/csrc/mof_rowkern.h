@@ -1,0 +1,161 @@
+// mof_rowkern.h -- device helpers shared by the row kernels of the PCG
+// (mof_pcg.hip) and of the multigrid cycle (mof_amg.hip): block loads,
+// deterministic reductions, the SELL-64 block SpMV row and the XCD-aware
+// (row block, system) mapping.
+#pragma once
+
+#include "mof_internal.h"
+
+namespace mof {
+namespace {
+
+template <typename V>
+struct VT;
+template <>
+struct VT<float> {
+    using V2 = float2;
+};
+template <>
+struct VT<double> {
+    using V2 = double2;
+};
+
+// Row kernels: a workgroup covers kRows groups of 256 consecutive vertex rows
+// (thread t takes rows base + 256 r + t, so every group stays 4 whole SELL
+// slices and every access stays coalesced). Fewer, larger workgroups keep the
+// per-workgroup partial sums short: each workgroup of the next launch re-reads
+// all nblk partials of its system, nblk = ceil(N / (256 kRows)).
+constexpr int kRows = 4;
+constexpr int kRowsPerWG = kWG * kRows;
+
+__device__ __forceinline__ void ld_blk(const float *A, int64_t pos, float (&a)[4]) {
+    const float4 v = reinterpret_cast<const float4 *>(A)[pos];
+    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+}
+__device__ __forceinline__ void ld_blk(const double *A, int64_t pos, double (&a)[4]) {
+    const double2 v0 = reinterpret_cast<const double2 *>(A)[2 * pos];
+    const double2 v1 = reinterpret_cast<const double2 *>(A)[2 * pos + 1];
+    a[0] = v0.x; a[1] = v0.y; a[2] = v1.x; a[3] = v1.y;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;  // valid in lane 0
+}
+
+// Deterministic workgroup sum of NV values; every thread gets the result.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = ((lds[k] + lds[NV + k]) + lds[2 * NV + k]) + lds[3 * NV + k];
+    __syncthreads();
+}
+
+// Sum n partials of NV values each (record stride NV) in a fixed order.
+template <int NV>
+__device__ __forceinline__ void reduce_partials(const double *part, int n, double (&out)[NV],
+                                                double *lds) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = 0.0;
+    int q = threadIdx.x;
+    for (; q + 3 * kWG < n; q += 4 * kWG) {  // four independent loads in flight
+        double v[4][NV];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) v[u][k] = part[(int64_t)(q + u * kWG) * NV + k];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) out[k] += v[u][k];
+    }
+    for (; q < n; q += kWG) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) out[k] += part[(int64_t)q * NV + k];
+    }
+    block_sum<NV>(out, lds);
+}
+
+// Materialised A of B systems (inner PCG operator).
+template <typename V>
+struct MatArgs {
+    int64_t sell_nb;
+    const int32_t *sell_off, *sell_col;
+    const V *A;  // [B][sell_nb][4]
+};
+
+template <typename V>
+__device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
+    return *reinterpret_cast<const typename VT<V>::V2 *>(p);
+}
+
+// y_i = sum_t A_blk(i,t) x_col(i,t) over the SELL-64 row of vertex i.
+// Slots are processed U at a time with every load of a chunk issued before
+// the first use (column indices, then block values, then the x gathers), so
+// a row costs two memory round trips instead of two per slot. Slots past
+// the slice width re-load the last valid slot and are masked out, keeping
+// every load unconditional.
+template <typename V>
+__device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
+                                         const V *__restrict__ x, V &y0, V &y1) {
+    using V2 = typename VT<V>::V2;
+    constexpr int U = sizeof(V) == 4 ? 8 : 4;
+    const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = mt.sell_off[s];
+    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    V a0 = 0, a1 = 0;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U];
+        V blk[U][4];
+        V2 xj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = min(t0 + u, w - 1);
+            j[u] = mt.sell_col[(int64_t)o + t * kSlice + l];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = min(t0 + u, w - 1);
+            ld_blk(A, (int64_t)o + t * kSlice + l, blk[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xj[u] = ld2(x + 2 * (int64_t)j[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool on = t0 + u < w;
+            a0 += on ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : (V)0;
+            a1 += on ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : (V)0;
+        }
+    }
+    y0 = a0;
+    y1 = a1;
+}
+
+// XCD-aware workgroup -> (row block, system): workgroups w and w+8 share an
+// XCD (round-robin dispatch; speed only, never correctness). XCD x takes row
+// blocks [x*chunk, (x+1)*chunk) of every system, system by system.
+__device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, int32_t &sys) {
+    const int32_t w = blockIdx.x;
+    const int32_t q = w >> 3;
+    const int32_t chunk = (nblk + 7) >> 3;
+    sys = q / chunk;
+    rb = (w & 7) * chunk + q % chunk;
+    return rb < nblk && sys < B;
+}
+
+inline unsigned xcd_grid(int32_t nblk, int32_t B) {
+    return (unsigned)(8 * B * ((nblk + 7) / 8));
+}
+
+}  // namespace
+}  // namespace mof

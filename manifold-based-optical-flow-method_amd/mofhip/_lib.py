@@ -31,6 +31,7 @@ MOF_PREC_MIXED = 1
 MOF_IO_DEVICE = 1
 MOF_NO_BLOCK_JACOBI = 2
 MOF_TIME_SPMV = 4
+MOF_PRECOND_AMG = 8
 MOF_CSR_A2 = 0
 MOF_CSR_A_LAST = 1
 

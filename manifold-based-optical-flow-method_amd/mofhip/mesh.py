@@ -141,13 +141,17 @@ class DeviceMesh:
     # -- solves ------------------------------------------------------------
     @staticmethod
     def make_opts(precision="f64", batch=0, rtol=0.0, inner_rtol=0.0, max_iter=0, max_outer=0,
-                  block_jacobi=True, device_io=False, time_spmv=False, stream=None) -> L.MofOpts:
+                  block_jacobi=True, device_io=False, time_spmv=False, stream=None,
+                  precond="jacobi") -> L.MofOpts:
+        """precond: "jacobi" (2x2 block Jacobi) or "amg" (aggregation-multigrid
+        V-cycle; precision="mixed" only)."""
         o = L.MofOpts()
         o.struct_size = ctypes.sizeof(L.MofOpts)
         o.precision = {"f64": L.MOF_PREC_F64, "mixed": L.MOF_PREC_MIXED}[precision]
         o.flags = ((L.MOF_IO_DEVICE if device_io else 0)
                    | (0 if block_jacobi else L.MOF_NO_BLOCK_JACOBI)
-                   | (L.MOF_TIME_SPMV if time_spmv else 0))
+                   | (L.MOF_TIME_SPMV if time_spmv else 0)
+                   | {"jacobi": 0, "amg": L.MOF_PRECOND_AMG}[precond])
         o.batch = int(batch)
         o.max_iter = int(max_iter)
         o.max_outer = int(max_outer)

@@ -1,0 +1,119 @@
+"""The multigrid-preconditioned inner solve (MOF_PRECOND_AMG) against the
+reference's spsolve.
+
+The preconditioner changes the iteration path only: the answer is held to the
+same bars as the block-Jacobi solve (max |V - V_spsolve| < 1e-6, relative true
+residual <= rtol in fp64), and it keeps the determinism guarantees (identical
+bits for any batch size or shard split).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_golden
+from mofhip import DeviceMesh, synth, velocity_field_sharded
+
+pytestmark = pytest.mark.gpu
+
+VTOL = 1e-6
+
+
+def mesh_of(g):
+    return DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+
+
+@pytest.mark.parametrize("case", ["G1_ico642", "G2_cap641", "G3_ico642_f32", "G5_dt512"])
+def test_amg_vs_spsolve_golden(case):
+    g = load_golden(case)
+    m = mesh_of(g)
+    T = len(g["I"])
+    V, st = m.solve_range(g["I"], g["t_k"], 0, T - 1, float(g["lambda_"]), precision="mixed",
+                          precond="amg", rtol=1e-10)
+    ref = g["V_k"]
+    assert st["failed"] == 0
+    assert st["max_rel_residual"] <= 1e-10
+    assert np.abs(V - ref).max() <= VTOL * max(1.0, np.abs(ref).max())
+
+
+def test_amg_fewer_iterations_and_deterministic():
+    g = load_golden("G1_ico642")
+    m = mesh_of(g)
+    I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    Vj, sj = m.solve_range(I, tk, 0, 15, lam, precision="mixed")
+    V1, s1 = m.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg", batch=1)
+    V8, _ = m.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg", batch=8)
+    V15, _ = m.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg", batch=15)
+    assert np.array_equal(V1, V8) and np.array_equal(V1, V15)
+    Vs, _ = velocity_field_sharded(m, I, tk, 0, 15, lam, devices=[0, 0], precision="mixed",
+                                   precond="amg")
+    assert np.array_equal(V1, Vs)
+    assert s1["iterations"] < sj["iterations"]
+    assert np.abs(V1 - Vj).max() < VTOL
+
+
+def test_amg_tiny_mesh_falls_back():
+    """A mesh that does not coarsen (42 vertices) keeps block Jacobi."""
+    p, t = synth.icosphere(1, 10.0)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    I = synth.travelling_wave(p, 3)
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(3.0), 0, 2, 0.01, precision="mixed", precond="amg")
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    for k in range(2):
+        Vo = oracle.worker(k, a2, gw, e, iw, t, [0, 1, 2], a, 0.01, I[k], I[k + 1])
+        assert np.abs(V[k] - Vo).max() < VTOL
+
+
+def test_amg_needs_mixed_precision():
+    g = load_golden("G1_ico642")
+    m = mesh_of(g)
+    with pytest.raises(Exception):
+        m.solve_range(g["I"], g["t_k"], 0, 2, 0.01, precision="f64", precond="amg")
+
+
+@pytest.mark.parametrize("kind", ["random_hull", "permuted_ico", "cap"])
+def test_amg_irregular_meshes(kind):
+    if kind == "random_hull":
+        p, t = synth.random_sphere(3000, 10.0, seed=3)
+    elif kind == "permuted_ico":
+        p, t, _ = synth.permute_vertices(*synth.icosphere(16, 10.0, jitter=0.005), seed=2)
+    else:
+        p, t = synth.spherical_cap(40, 10.0, 0.7)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    I = synth.travelling_wave(p, 4)
+    m = DeviceMesh(p, n, t, a)
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(4.0), 0, 3, 0.01, precision="mixed", precond="amg")
+    assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
+    for k in range(3):
+        Vo = oracle.worker(k, a2, gw, e, iw, t, list(range(4)), a, 0.01, I[k], I[k + 1])
+        assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
+
+
+@pytest.mark.slow
+def test_amg_32k_vs_spsolve():
+    p, t, n, a = synth.mesh_for_config("C2")
+    I = synth.travelling_wave(p, 3)
+    m = DeviceMesh(p, n, t, a)
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    Ao, fo = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[0], I[1], 1.0)
+    from scipy.sparse.linalg import spsolve
+    Vo = spsolve(Ao.tocsc(), fo)
+    V, st = m.solve_range(I, np.arange(3.0), 0, 1, 0.01, precision="mixed", precond="amg")
+    assert np.abs(V[0] - Vo).max() < VTOL
+    assert st["max_rel_residual"] <= 1e-8
+
+
+@pytest.mark.slow
+def test_amg_160k_agrees_with_jacobi():
+    p, t, n, a = synth.mesh_for_config("C3")
+    I = synth.travelling_wave(p, 5)
+    m = DeviceMesh(p, n, t, a)
+    tk = np.arange(5.0)
+    Vj, sj = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", batch=4)
+    Va, sa = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", precond="amg", batch=4)
+    Va2, _ = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", precond="amg", batch=2)
+    assert sa["failed"] == 0 and sa["max_rel_residual"] <= 1e-8
+    assert np.abs(Va - Vj).max() < VTOL
+    assert np.array_equal(Va, Va2)
+    assert sa["iterations"] < sj["iterations"]
