@@ -52,6 +52,7 @@ struct AmgDevLevel {
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap
     DevArray<float> A, Dinv;     // [B][sell_nb][12], [B][n][12] (level >= 1)
+    DevArray<uint32_t> Ah;       // [B][sell_nb][6] bf16 A for the sweeps (not the coarsest)
     DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x, r [B][n][2]
                                  // r is stored in member order of the next level
 };
@@ -63,6 +64,7 @@ struct AmgDevice {
     float omega = 0.7f;
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
+    DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)
 };
 
 }  // namespace mof

@@ -14,16 +14,19 @@
 //                                  order of the next level's aggregates
 //                 k_restrict       b_{l+1} = Q^T r_l (contiguous members),
 //                                  x_{l+1} = w D^-1 b_{l+1} (next pre-smooth)
-//   coarsest:     k_coarse_solve   y = A_c^-1 b
+//   levels with <= 4096 nodes and the coarsest solve y = A_c^-1 b run in
+//   one launch (k_subcycle, one workgroup per system);
 //   per level l:  k_prolong        x_l += Q y_{l+1}
 //                 k_post3 / k_post0  y_l = x_l + w D^-1 (b_l - A_l x_l); at
 //                                  level 0 y = z and the partial r.z of the PCG
-// Every launch covers all B systems and skips retired systems. Level 0 reuses
-// the inner solver's fp32 SELL A, 2x2 D^-1 and row-kernel layout (XCD-aware,
-// batched loads); coarse levels store 3x3 blocks as 12 floats (rows padded to
+// Every launch covers all B systems and skips retired systems. Level 0 sweeps
+// a bf16 copy of the inner solver's SELL A (k_to_bf16, once per batch) with
+// its fp32 2x2 D^-1 and row-kernel layout (XCD-aware, batched loads); coarse levels store 3x3 blocks as 12 floats (rows padded to
 // 4) and vectors as float4. All sums run in a fixed order: the cycle is
 // deterministic and independent of B.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "mof_amg.h"
 #include "mof_rowkern.h"
@@ -110,7 +113,60 @@ __device__ __forceinline__ void st3(float *A, int64_t idx, const float (&a)[3][3
     for (int r = 0; r < 3; ++r) p[r] = make_float4(a[r][0], a[r][1], a[r][2], 0.f);
 }
 
+// bf16 copies of the level-0 operator for the smoother sweeps (the
+// preconditioner only needs an SPD approximation of A; rounding the blocks
+// (i,j) and (j,i)^T alike keeps it symmetric) -- half the bytes of A32.
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;  // round to nearest even
+}
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
+struct MatH {
+    int64_t sell_nb;
+    const int32_t *sell_off, *sell_col;
+    const uint2 *A;  // [B][sell_nb] 4 bf16 per block
+};
+
+// spmv_row of mof_rowkern.h on the bf16 blocks
+__device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i, const float *__restrict__ x,
+                                           float &y0, float &y1) {
+    constexpr int U = 8;
+    const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = mt.sell_off[s];
+    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    float a0 = 0.f, a1 = 0.f;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U];
+        uint2 blk[U];
+        float2 xj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+        for (int u = 0; u < U; ++u) blk[u] = A[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xj[u] = reinterpret_cast<const float2 *>(x)[j[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool on = t0 + u < w;
+            a0 += on ? bf16_lo(blk[u].x) * xj[u].x + bf16_hi(blk[u].x) * xj[u].y : 0.f;
+            a1 += on ? bf16_lo(blk[u].y) * xj[u].x + bf16_hi(blk[u].y) * xj[u].y : 0.f;
+        }
+    }
+    y0 = a0;
+    y1 = a1;
+}
+
 // ---- per-timestep setup --------------------------------------------------
+
+__global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
+    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (q >= n) return;
+    const float4 v = A[q];
+    H[q] = make_uint2(bf16_bits(v.x) | (bf16_bits(v.y) << 16), bf16_bits(v.z) | (bf16_bits(v.w) << 16));
+}
 
 // Block (I, J) at coarse SELL position pos of A_{l+1} = Q^T A_l Q for system
 // b, summed over its gather list in list order; the diagonal block also gets
@@ -120,7 +176,8 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     int64_t c_sell_nb, int32_t nC, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
-    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, float *__restrict__ Dc) {
+    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, float *__restrict__ Dc,
+    uint2 *__restrict__ Ah) {
     const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
     const int32_t b = blockIdx.y;
     if (pos >= c_sell_nb) return;
@@ -170,6 +227,12 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
         st3(Dc, (int64_t)b * nC + I, D);
     }
     st3(Ac, (int64_t)b * c_sell_nb + pos, C);
+    if (Ah) {
+        uint2 *p = Ah + 3 * ((int64_t)b * c_sell_nb + pos);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            p[r] = make_uint2(bf16_bits(C[r][0]) | (bf16_bits(C[r][1]) << 16), bf16_bits(C[r][2]));
+    }
 }
 
 constexpr int kMaxCoarse = 128;
@@ -228,16 +291,16 @@ __global__ __launch_bounds__(kWG) void k_coarse_inverse(int32_t n, const int32_t
         piv = piv != 0.0 ? piv : 1.0;
         const double ip = 1.0 / piv;
         const double akc = rowk[c] * ip;
+        const bool ck = c == k;
+        const double rowfix = ck ? -ip : akc;  // the new row k
+        // branch-free (every LDS read unconditional, so they pipeline):
+        // column k scales by 1/piv, row k is replaced, the rest updates
+        const double f = ck ? 0.0 : akc, sc = ck ? ip : 1.0;
 #pragma unroll
         for (int mm = 0; mm < kSweepRows; ++mm) {
             const int32_t r = h * kSweepRows + mm;
-            const double ark = rowk[r];
-            if (r == k)
-                a[mm] = (c == k) ? -ip : a[mm] * ip;
-            else if (c == k)
-                a[mm] = a[mm] * ip;
-            else
-                a[mm] -= ark * akc;
+            const double v = fma(-rowk[r], f, a[mm]) * sc;
+            a[mm] = (r == k) ? rowfix : v;
         }
         __syncthreads();
     }
@@ -253,9 +316,21 @@ __global__ __launch_bounds__(kWG) void k_coarse_inverse(int32_t n, const int32_t
 
 // ---- V-cycle ---------------------------------------------------------------
 
+// Device view of one level (pointers to system 0; system b adds its stride).
+struct Lvl {
+    int32_t n;
+    int64_t sell_nb;
+    const int32_t *sell_off, *sell_col;  // level >= 1
+    const float *A, *Dinv;               // level >= 1: [B][sell_nb][12], [B][n][12]
+    const uint2 *Ah;                     // bf16 A for the sweeps ([B][sell_nb][3]), or null
+    float *b, *x, *r, *y;                // [B][n][4] (level 0: x, r [B][n][2])
+    const int32_t *agg, *mptr, *apos;    // transition to level + 1
+    const float *Q, *Qm;
+};
+
 // Level 0: r1 = r - A x0 (x0 = w D^-1 r from the PCG update), stored at the
 // member position of each vertex. PCG row layout, XCD-aware grid.
-__global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B, MatArgs<float> mat,
+__global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                               const float *__restrict__ rv, const float *__restrict__ xv,
                                               const int32_t *__restrict__ apos,
                                               const int32_t *__restrict__ sysi, float *__restrict__ r1) {
@@ -267,153 +342,233 @@ __global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         float y0, y1;
-        spmv_row<float>(mat, b, i, xv + 2 * vb, y0, y1);
+        spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
         reinterpret_cast<float2 *>(r1)[vb + apos[i]] = make_float2(ri.x - y0, ri.y - y1);
     }
 }
 
-// Coarse level: r = b - A x, stored at the member position of each node.
-__global__ __launch_bounds__(kWG) void k_res3(int32_t n, const int32_t *__restrict__ sell_off,
-                                              const int32_t *__restrict__ sell_col,
-                                              const float *__restrict__ A, int64_t sell_nb,
-                                              const float *__restrict__ bv, const float *__restrict__ xv,
-                                              const int32_t *__restrict__ apos,
-                                              const int32_t *__restrict__ sysi, float *__restrict__ rv) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
-    if (i >= n || retired(sysi, b)) return;
-    const float *Ab = A + (int64_t)b * sell_nb * kB3;
-    const float *xb = xv + (int64_t)b * n * 4;
-    float acc[3];
-    ldv<3>(bv + (int64_t)b * n * 4, i, acc);
+// (A x)_i of a coarse level, slots U at a time with all loads of a chunk
+// issued first (as spmv_row).
+__device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, const float *__restrict__ xb,
+                                          float (&acc)[3]) {
+    constexpr int U = 4;
+    const float *Ab = L.A + (int64_t)b * L.sell_nb * kB3;
+    const uint2 *Hb = L.Ah + (int64_t)b * L.sell_nb * 3;
+    const bool half = L.Ah != nullptr;
     const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = sell_off[s], w = (sell_off[s + 1] - o) >> 6;
-    for (int32_t t = 0; t < w; ++t) {
-        const int64_t pos = (int64_t)o + t * kSlice + l;
-        float a[3][3], xj[3], ax[3];
-        ldm<3>(Ab, pos, a);
-        ldv<3>(xb, sell_col[pos], xj);
-        matvec<3>(a, xj, ax);
+    const int32_t o = L.sell_off[s], w = (L.sell_off[s + 1] - o) >> 6;
+    acc[0] = acc[1] = acc[2] = 0.f;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U];
+        float a[U][3][3], xj[U][3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) acc[c] -= ax[c];
+        for (int u = 0; u < U; ++u) j[u] = L.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+        if (half) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint2 *p = Hb + 3 * ((int64_t)o + min(t0 + u, w - 1) * kSlice + l);
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const uint2 h = p[r];
+                    a[u][r][0] = bf16_lo(h.x);
+                    a[u][r][1] = bf16_hi(h.x);
+                    a[u][r][2] = bf16_lo(h.y);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) ldm<3>(Ab, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, a[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) ldv<3>(xb, j[u], xj[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool on = t0 + u < w;
+            float ax[3];
+            matvec<3>(a[u], xj[u], ax);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[c] += on ? ax[c] : 0.f;
+        }
     }
-    stv<3>(rv + (int64_t)b * n * 4, apos[i], acc);
 }
 
-// b_{l+1}[I] = sum over the members of aggregate I of Q^T r (member order,
-// contiguous); with D (not the coarsest level) also x_{l+1} = w D^-1 b_{l+1}.
+// coarse level: r = b - A x at the member position of node i
+__device__ __forceinline__ void res3_node(const Lvl &L, int32_t b, int32_t i) {
+    const int64_t vo = (int64_t)b * L.n * 4;
+    float ax[3], bi[3];
+    spmv_row3(L, b, i, L.x + vo, ax);
+    ldv<3>(L.b + vo, i, bi);
+    const float ri[3] = {bi[0] - ax[0], bi[1] - ax[1], bi[2] - ax[2]};
+    stv<3>(L.r + vo, L.apos[i], ri);
+}
+
+// b_C[I] = sum over the members of aggregate I of Q^T r (member order,
+// contiguous, U at a time); with smooth also x_C[I] = w D_C^-1 b_C[I].
 template <int BSF>
-__global__ __launch_bounds__(kWG) void k_restrict(int32_t nF, int32_t nC, const int32_t *__restrict__ mptr,
-                                                  const float *__restrict__ Qm,
-                                                  const float *__restrict__ rv,
-                                                  const float *__restrict__ Dc, float omega,
-                                                  const int32_t *__restrict__ sysi,
-                                                  float *__restrict__ bc, float *__restrict__ xc) {
-    const int32_t I = blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
-    if (I >= nC || retired(sysi, b)) return;
-    const float *rb = rv + (int64_t)b * nF * vstride<BSF>();
+__device__ __forceinline__ void restrict_node(const Lvl &F, const Lvl &C, int32_t b, int32_t I, bool smooth,
+                                              float omega) {
+    constexpr int U = 4;
+    const float *rb = F.r + (int64_t)b * F.n * vstride<BSF>();
     float acc[3] = {0.f, 0.f, 0.f};
-    const int32_t q0 = mptr[I], q1 = mptr[I + 1];
-    for (int32_t q = q0; q < q1; ++q) {
-        float ri[BSF];
-        ldv<BSF>(rb, q, ri);
-        const float *qi = Qm + (int64_t)q * BSF * 3;
+    const int32_t q0 = F.mptr[I], q1 = F.mptr[I + 1];
+    for (int32_t t0 = q0; t0 < q1; t0 += U) {
+        float ri[U][BSF], qm[U][BSF * 3];
 #pragma unroll
-        for (int k = 0; k < BSF; ++k)
+        for (int u = 0; u < U; ++u) ldv<BSF>(rb, min(t0 + u, q1 - 1), ri[u]);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) acc[c] += qi[3 * k + c] * ri[k];
+        for (int u = 0; u < U; ++u) {
+            const float *p = F.Qm + (int64_t)min(t0 + u, q1 - 1) * BSF * 3;
+#pragma unroll
+            for (int k = 0; k < BSF * 3; ++k) qm[u][k] = p[k];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float on = t0 + u < q1 ? 1.f : 0.f;
+#pragma unroll
+            for (int k = 0; k < BSF; ++k)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[c] += qm[u][3 * k + c] * (on * ri[u][k]);
+        }
     }
-    stv<3>(bc + (int64_t)b * nC * 4, I, acc);
-    if (Dc) {
+    const int64_t vo = (int64_t)b * C.n * 4;
+    stv<3>(C.b + vo, I, acc);
+    if (smooth) {
         float d[3][3], x[3];
-        ldm<3>(Dc + (int64_t)b * nC * kB3, I, d);
+        ldm<3>(C.Dinv + (int64_t)b * C.n * kB3, I, d);
         matvec<3>(d, acc, x);
 #pragma unroll
         for (int c = 0; c < 3; ++c) x[c] *= omega;
-        stv<3>(xc + (int64_t)b * nC * 4, I, x);
+        stv<3>(C.x + vo, I, x);
     }
 }
 
-// y = A_c^-1 b on the coarsest level (one workgroup per system)
-__global__ __launch_bounds__(kWG) void k_coarse_solve(int32_t n, const float *__restrict__ cinv,
-                                                      const float *__restrict__ bv,
-                                                      const int32_t *__restrict__ sysi,
-                                                      float *__restrict__ yv) {
-    __shared__ float bl[kMaxCoarse];
-    const int32_t b = blockIdx.x;
-    if (retired(sysi, b)) return;
-    const int32_t nc = 3 * n;
-    for (int32_t q = threadIdx.x; q < nc; q += kWG) bl[q] = bv[(int64_t)b * n * 4 + 4 * (q / 3) + q % 3];
-    __syncthreads();
-    const float *Mi = cinv + (int64_t)b * nc * nc;
-    for (int32_t d = threadIdx.x; d < nc; d += kWG) {
-        float s = 0.f;
-        for (int32_t k = 0; k < nc; ++k) s += Mi[(int64_t)k * nc + d] * bl[k];  // symmetric
-        yv[(int64_t)b * n * 4 + 4 * (d / 3) + d % 3] = s;
-    }
-}
-
-// x_i += Q_i y_{l+1}[agg(i)]
+// x_i += Q_i y_C[agg(i)]
 template <int BSF>
-__global__ __launch_bounds__(kWG) void k_prolong(int32_t nF, int32_t nC, const int32_t *__restrict__ agg,
-                                                 const float *__restrict__ Q,
-                                                 const float *__restrict__ yc,
-                                                 const int32_t *__restrict__ sysi,
-                                                 float *__restrict__ xv) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
-    if (i >= nF || retired(sysi, b)) return;
+__device__ __forceinline__ void prolong_node(const Lvl &F, const Lvl &C, int32_t b, int32_t i) {
     float y[3], xi[BSF];
-    ldv<3>(yc + (int64_t)b * nC * 4, agg[i], y);
-    float *xb = xv + (int64_t)b * nF * vstride<BSF>();
+    ldv<3>(C.y + (int64_t)b * C.n * 4, F.agg[i], y);
+    float *xb = F.x + (int64_t)b * F.n * vstride<BSF>();
     ldv<BSF>(xb, i, xi);
-    const float *qi = Q + (int64_t)i * BSF * 3;
+    const float *qi = F.Q + (int64_t)i * BSF * 3;
 #pragma unroll
     for (int k = 0; k < BSF; ++k) xi[k] += qi[3 * k] * y[0] + qi[3 * k + 1] * y[1] + qi[3 * k + 2] * y[2];
     stv<BSF>(xb, i, xi);
 }
 
-// y = x + w D^-1 (b - A x) on a coarse level (one node per thread)
-__global__ __launch_bounds__(kWG) void k_post3(int32_t n, const int32_t *__restrict__ sell_off,
-                                               const int32_t *__restrict__ sell_col,
-                                               const float *__restrict__ A, int64_t sell_nb,
-                                               const float *__restrict__ Dinv,
-                                               const float *__restrict__ bv,
-                                               const float *__restrict__ xv, float omega,
-                                               const int32_t *__restrict__ sysi,
-                                               float *__restrict__ yv) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
-    if (i >= n || retired(sysi, b)) return;
-    const float *Ab = A + (int64_t)b * sell_nb * kB3;
-    const float *xb = xv + (int64_t)b * n * 4;
-    float res[3], xi[3];
-    ldv<3>(bv + (int64_t)b * n * 4, i, res);
-    ldv<3>(xb, i, xi);
-    const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = sell_off[s], w = (sell_off[s + 1] - o) >> 6;
-    for (int32_t t = 0; t < w; ++t) {
-        const int64_t pos = (int64_t)o + t * kSlice + l;
-        float a[3][3], xj[3], ax[3];
-        ldm<3>(Ab, pos, a);
-        ldv<3>(xb, sell_col[pos], xj);
-        matvec<3>(a, xj, ax);
+// coarse level: y = x + w D^-1 (b - A x)
+__device__ __forceinline__ void post3_node(const Lvl &L, int32_t b, int32_t i, float omega) {
+    const int64_t vo = (int64_t)b * L.n * 4;
+    float ax[3], res[3], xi[3], d[3][3], dr[3];
+    spmv_row3(L, b, i, L.x + vo, ax);
+    ldv<3>(L.b + vo, i, res);
+    ldv<3>(L.x + vo, i, xi);
+    ldm<3>(L.Dinv + (int64_t)b * L.n * kB3, i, d);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) res[c] -= ax[c];
-    }
-    float d[3][3], dr[3];
-    ldm<3>(Dinv + (int64_t)b * n * kB3, i, d);
+    for (int c = 0; c < 3; ++c) res[c] -= ax[c];
     matvec<3>(d, res, dr);
 #pragma unroll
     for (int c = 0; c < 3; ++c) xi[c] += omega * dr[c];
-    stv<3>(yv + (int64_t)b * n * 4, i, xi);
+    stv<3>(L.y + vo, i, xi);
+}
+
+__global__ __launch_bounds__(kWG) void k_res3(Lvl L, const int32_t *__restrict__ sysi) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    if (i >= L.n || retired(sysi, b)) return;
+    res3_node(L, b, i);
+}
+
+template <int BSF>
+__global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, int32_t smooth, float omega,
+                                                  const int32_t *__restrict__ sysi) {
+    const int32_t I = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    if (I >= C.n || retired(sysi, b)) return;
+    restrict_node<BSF>(F, C, b, I, smooth != 0, omega);
+}
+
+template <int BSF>
+__global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__restrict__ sysi) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    if (i >= F.n || retired(sysi, b)) return;
+    prolong_node<BSF>(F, C, b, i);
+}
+
+__global__ __launch_bounds__(kWG) void k_post3(Lvl L, float omega, const int32_t *__restrict__ sysi) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    if (i >= L.n || retired(sysi, b)) return;
+    post3_node(L, b, i, omega);
+}
+
+// The cycle below level S (all levels with <= kSubNodes nodes) in one launch:
+// one workgroup per system walks the tiny levels with barriers in between,
+// replacing ~4 launches per level.
+constexpr int kSubWG = 256;
+constexpr int kSubNodes = 512;
+constexpr int kMaxLevels = 12;
+
+struct SubArgs {
+    int32_t first, last;  // levels first..last (last = coarsest), first >= 1
+    Lvl lv[kMaxLevels];
+    const float *cinv;
+    float omega;
+    const int32_t *sysi;
+};
+
+__global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
+    const int32_t b = blockIdx.x;
+    if (retired(a.sysi, b)) return;
+    const int32_t tid = threadIdx.x;
+    // down: level first already holds b and the pre-smoothed x
+    for (int32_t l = a.first; l < a.last; ++l) {
+        const Lvl &F = a.lv[l], &C = a.lv[l + 1];
+        for (int32_t i = tid; i < F.n; i += kSubWG) res3_node(F, b, i);
+        __syncthreads();
+        for (int32_t I = tid; I < C.n; I += kSubWG) restrict_node<3>(F, C, b, I, l + 1 < a.last, a.omega);
+        __syncthreads();
+    }
+    // coarsest: y = A_c^-1 b (the inverse is symmetric: read by columns);
+    // b staged in LDS, the k range split over the two halves of the
+    // workgroup, 16 independent loads in flight per thread
+    {
+        __shared__ float bl[kMaxCoarse];
+        __shared__ float part[kMaxCoarse];
+        const Lvl &C = a.lv[a.last];
+        const int32_t nc = 3 * C.n;
+        const float *Mi = a.cinv + (int64_t)b * nc * nc;
+        const float *bb = C.b + (int64_t)b * C.n * 4;
+        for (int32_t q = tid; q < nc; q += kSubWG) bl[q] = bb[4 * (q / 3) + q % 3];
+        __syncthreads();
+        const int32_t d = tid % kMaxCoarse, hf = tid / kMaxCoarse;  // kSubWG = 2 * kMaxCoarse
+        const int32_t k0 = hf * ((nc + 1) / 2), k1 = hf ? nc : (nc + 1) / 2;
+        float sum = 0.f;
+        if (d < nc) {
+            constexpr int U = 16;
+            for (int32_t k = k0; k < k1; k += U) {
+                float mv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) mv[u] = Mi[(int64_t)min(k + u, k1 - 1) * nc + d];
+#pragma unroll
+                for (int u = 0; u < U; ++u) sum += (k + u < k1) ? mv[u] * bl[min(k + u, k1 - 1)] : 0.f;
+            }
+        }
+        if (hf) part[d] = sum;
+        __syncthreads();
+        if (!hf && d < nc) C.y[(int64_t)b * C.n * 4 + 4 * (d / 3) + d % 3] = sum + part[d];
+        __syncthreads();
+    }
+    // up
+    for (int32_t l = a.last - 1; l >= a.first; --l) {
+        const Lvl &F = a.lv[l], &C = a.lv[l + 1];
+        for (int32_t i = tid; i < F.n; i += kSubWG) prolong_node<3>(F, C, b, i);
+        __syncthreads();
+        for (int32_t i = tid; i < F.n; i += kSubWG) post3_node(F, b, i, a.omega);
+        __syncthreads();
+    }
 }
 
 // Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
 // of the row block's record). PCG row layout, XCD-aware grid.
-__global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t B, MatArgs<float> mat,
+__global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                const float *__restrict__ Dinv,
                                                const float *__restrict__ rv,
                                                const float *__restrict__ xv, float omega,
@@ -429,7 +584,7 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
         const int32_t i = rb * kRowsPerWG + g * kWG + threadIdx.x;
         if (i >= N) break;
         float y0, y1;
-        spmv_row<float>(mat, b, i, xv + 2 * vb, y0, y1);
+        spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
         const float2 xi = reinterpret_cast<const float2 *>(xv)[vb + i];
         float d[4];
@@ -447,12 +602,12 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
 
-MatArgs<float> level0_mat(mof_mesh *m) {
-    MatArgs<float> mt;
+MatH level0_mat(mof_mesh *m) {
+    MatH mt;
     mt.sell_nb = m->pat.sell_nb();
     mt.sell_off = m->sell_off.p;
     mt.sell_col = m->sell_col.p;
-    mt.A = m->ws.A32.p;
+    mt.A = reinterpret_cast<const uint2 *>(m->amg->A0h.p);
     return mt;
 }
 
@@ -477,6 +632,7 @@ bool amg_build(mof_mesh *m) {
     // a mesh that does not coarsen (<= 42 vertices) keeps block Jacobi
     if (H.levels.size() < 2) return false;
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
+    MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
     auto put_i = [&](DevArray<int32_t> &d, const std::vector<int32_t> &h) {
         d.alloc(h.size());
@@ -512,6 +668,11 @@ bool amg_build(mof_mesh *m) {
     }
     G.nc = H.coarse_dofs;
     G.cap = 0;
+    if (std::getenv("MOF_AMG_VERBOSE")) {
+        for (size_t l = 0; l < H.levels.size(); ++l)
+            std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld\n", l, H.levels[l].n,
+                         H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb());
+    }
     MOF_HIP(hipStreamSynchronize(s));
     return true;
 }
@@ -526,9 +687,14 @@ void amg_ensure(mof_mesh *m, int32_t B) {
         if (l == 0) {
             D.x.alloc(2 * n * B);
             D.r.alloc(2 * n * B);
+            G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
+            if (l + 1 < G.lv.size()) {  // bf16 sweep copy (the coarsest stays fp32)
+                D.Ah.alloc((size_t)6 * D.sell_nb * B);
+                D.Ah.zero(s);
+            }
             D.Dinv.alloc((size_t)kB3 * n * B);
             D.b.alloc(4 * n * B);
             D.x.alloc(4 * n * B);
@@ -544,20 +710,26 @@ void amg_ensure(mof_mesh *m, int32_t B) {
 float *amg_level0_x(mof_mesh *m) { return m->amg->lv[0].x.p; }
 float amg_omega(const mof_mesh *m) { return m->amg->omega; }
 
+static uint2 *ah(AmgDevLevel &C) { return C.Ah.n > 1 ? reinterpret_cast<uint2 *>(C.Ah.p) : nullptr; }
+
 void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     AmgDevice &G = *m->amg;
     Workspace &w = m->ws;
     const size_t L = G.lv.size();
+    const int64_t nb0 = m->pat.sell_nb() * B;
+    k_to_bf16<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
+        nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
         if (l == 0)
             k_galerkin<2><<<grid2(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
-                                                              m->pat.sell_nb(), C.A.p, C.Dinv.p);
+                                                              m->pat.sell_nb(), C.A.p, C.Dinv.p,
+                                                              ah(C));
         else
             k_galerkin<3><<<grid2(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
-                                                              F.sell_nb, C.A.p, C.Dinv.p);
+                                                              F.sell_nb, C.A.p, C.Dinv.p, ah(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];
     k_coarse_inverse<<<dim3((unsigned)B), kWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
@@ -565,43 +737,68 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     MOF_HIP(hipGetLastError());
 }
 
+Lvl level_view(const AmgDevLevel &D) {
+    Lvl v;
+    v.n = D.n;
+    v.sell_nb = D.sell_nb;
+    v.sell_off = D.sell_off.p;
+    v.sell_col = D.sell_col.p;
+    v.A = D.A.p;
+    v.Dinv = D.Dinv.p;
+    v.Ah = D.Ah.n > 1 ? reinterpret_cast<const uint2 *>(D.Ah.p) : nullptr;
+    v.b = D.b.p;
+    v.x = D.x.p;
+    v.r = D.r.p;
+    v.y = D.y.p;
+    v.agg = D.agg.p;
+    v.mptr = D.mptr.p;
+    v.apos = D.apos.p;
+    v.Q = D.Q.p;
+    v.Qm = D.Qm.p;
+    return v;
+}
+
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part_slot, int32_t nblk,
                 hipStream_t s) {
     AmgDevice &G = *m->amg;
     Workspace &w = m->ws;
-    const size_t L = G.lv.size();
+    const int32_t L = (int32_t)G.lv.size();
     const int32_t *sysi = w.sysi.p;
     const float om = G.omega;
-    const MatArgs<float> mat0 = level0_mat(m);
+    const MatH mat0 = level0_mat(m);
     const dim3 gx(xcd_grid(nblk, B));
+    Lvl v[kMaxLevels];
+    for (int32_t l = 0; l < L; ++l) v[l] = level_view(G.lv[l]);
+    // levels S.. run fused in k_subcycle
+    int32_t S = 1;
+    while (S < L - 1 && G.lv[S].n > kSubNodes) ++S;
     // down: residual of the pre-smoothed x, restriction (+ next pre-smooth)
-    for (size_t l = 0; l + 1 < L; ++l) {
-        AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
-        const bool coarsest = l + 2 == L;
-        const float *Dn = coarsest ? nullptr : C.Dinv.p;
+    for (int32_t l = 0; l < S; ++l) {
+        const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
-            k_res0<<<gx, kWG, 0, s>>>(F.n, nblk, B, mat0, r0, F.x.p, F.apos.p, sysi, F.r.p);
-            k_restrict<2><<<grid2(C.n, B), kWG, 0, s>>>(F.n, C.n, F.mptr.p, F.Qm.p, F.r.p, Dn, om, sysi,
-                                                        C.b.p, C.x.p);
+            k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x, v[0].apos, sysi, v[0].r);
+            k_restrict<2><<<grid2(v[1].n, B), kWG, 0, s>>>(v[0], v[1], smooth, om, sysi);
         } else {
-            k_res3<<<grid2(F.n, B), kWG, 0, s>>>(F.n, F.sell_off.p, F.sell_col.p, F.A.p, F.sell_nb, F.b.p,
-                                                 F.x.p, F.apos.p, sysi, F.r.p);
-            k_restrict<3><<<grid2(C.n, B), kWG, 0, s>>>(F.n, C.n, F.mptr.p, F.Qm.p, F.r.p, Dn, om, sysi,
-                                                        C.b.p, C.x.p);
+            k_res3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], sysi);
+            k_restrict<3><<<grid2(v[l + 1].n, B), kWG, 0, s>>>(v[l], v[l + 1], smooth, om, sysi);
         }
     }
-    AmgDevLevel &Lc = G.lv[L - 1];
-    k_coarse_solve<<<dim3((unsigned)B), kWG, 0, s>>>(Lc.n, G.cinv.p, Lc.b.p, sysi, Lc.y.p);
+    SubArgs sa;
+    sa.first = S;
+    sa.last = L - 1;
+    for (int32_t l = 0; l < L; ++l) sa.lv[l] = v[l];
+    sa.cinv = G.cinv.p;
+    sa.omega = om;
+    sa.sysi = sysi;
+    k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
     // up: coarse correction, post-smooth
-    for (size_t l = L - 1; l-- > 0;) {
-        AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
+    for (int32_t l = S - 1; l >= 0; --l) {
         if (l == 0) {
-            k_prolong<2><<<grid2(F.n, B), kWG, 0, s>>>(F.n, C.n, F.agg.p, F.Q.p, C.y.p, sysi, F.x.p);
-            k_post0<<<gx, kWG, 0, s>>>(F.n, nblk, B, mat0, w.dinv32.p, r0, F.x.p, om, sysi, z0, part_slot);
+            k_prolong<2><<<grid2(v[0].n, B), kWG, 0, s>>>(v[0], v[1], sysi);
+            k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, w.dinv32.p, r0, v[0].x, om, sysi, z0, part_slot);
         } else {
-            k_prolong<3><<<grid2(F.n, B), kWG, 0, s>>>(F.n, C.n, F.agg.p, F.Q.p, C.y.p, sysi, F.x.p);
-            k_post3<<<grid2(F.n, B), kWG, 0, s>>>(F.n, F.sell_off.p, F.sell_col.p, F.A.p, F.sell_nb,
-                                                   F.Dinv.p, F.b.p, F.x.p, om, sysi, F.y.p);
+            k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
+            k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om, sysi);
         }
     }
     MOF_HIP(hipGetLastError());
