@@ -186,37 +186,53 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     const float *A = Af + (int64_t)b * f_sell_nb * bstride<BSF>();
     float C[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
-    for (int32_t g = g0; g < g1; ++g) {
-        const int32_t fp = gent[3 * (int64_t)g], i = gent[3 * (int64_t)g + 1],
-                      j = gent[3 * (int64_t)g + 2];
-        float a[BSF][BSF], qi[BSF][3], qj[BSF][3];
-        ldm<BSF>(A, fp, a);
+    // U entries at a time, every load of a chunk issued before use (entries
+    // past the list re-load the last one and are masked out)
+    constexpr int U = 4;
+    for (int32_t t0 = g0; t0 < g1; t0 += U) {
+        int32_t fp[U], ii[U], jj[U];
 #pragma unroll
-        for (int k = 0; k < BSF; ++k)
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = min(t0 + u, g1 - 1);
+            fp[u] = gent[3 * g];
+            ii[u] = gent[3 * g + 1];
+            jj[u] = gent[3 * g + 2];
+        }
+        float a[U][BSF][BSF], qi[U][BSF][3], qj[U][BSF][3];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                qi[k][c] = Q[((int64_t)i * BSF + k) * 3 + c];
-                qj[k][c] = Q[((int64_t)j * BSF + k) * 3 + c];
-            }
-        float T[BSF][3];  // A Q_j
+        for (int u = 0; u < U; ++u) {
+            ldm<BSF>(A, fp[u], a[u]);
 #pragma unroll
-        for (int r = 0; r < BSF; ++r)
+            for (int k = 0; k < BSF; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                float sum = 0.f;
+                for (int c = 0; c < 3; ++c) {
+                    qi[u][k][c] = Q[((int64_t)ii[u] * BSF + k) * 3 + c];
+                    qj[u][k][c] = Q[((int64_t)jj[u] * BSF + k) * 3 + c];
+                }
+        }
 #pragma unroll
-                for (int k = 0; k < BSF; ++k) sum += a[r][k] * qj[k][c];
-                T[r][c] = sum;
-            }
+        for (int u = 0; u < U; ++u) {
+            const float on = t0 + u < g1 ? 1.f : 0.f;
+            float T[BSF][3];  // A Q_j
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+            for (int r = 0; r < BSF; ++r)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                float sum = 0.f;
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
 #pragma unroll
-                for (int k = 0; k < BSF; ++k) sum += qi[k][r] * T[k][c];
-                C[r][c] += sum;
-            }
+                    for (int k = 0; k < BSF; ++k) sum += a[u][r][k] * qj[u][k][c];
+                    T[r][c] = on * sum;
+                }
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < BSF; ++k) sum += qi[u][k][r] * T[k][c];
+                    C[r][c] += sum;
+                }
+        }
     }
     if (pos == c_diag[I]) {
 #pragma unroll
@@ -236,7 +252,8 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
 }
 
 constexpr int kMaxCoarse = 128;
-constexpr int kSweepRows = kMaxCoarse * kMaxCoarse / kWG;  // 64 matrix rows per thread
+constexpr int kInvWG = 1024;
+constexpr int kSweepRows = kMaxCoarse * kMaxCoarse / kInvWG;  // 16 matrix rows per thread
 
 // Inverse of the coarsest operator (nc = 3 n <= 128 dofs) of system b by the
 // symmetric sweep operator: sweeping pivot k maps
@@ -244,8 +261,8 @@ constexpr int kSweepRows = kMaxCoarse * kMaxCoarse / kWG;  // 64 matrix rows per
 //   a_ij -> a_ij - a_ik a_kj / a_kk,
 // and after all pivots the matrix holds -A^-1. Symmetry gives column k =
 // row k, so a step broadcasts one row through LDS. Thread t owns column
-// t % 128 of rows (t / 128) * 64 + [0, 64) in fp64 registers.
-__global__ __launch_bounds__(kWG) void k_coarse_inverse(int32_t n, const int32_t *__restrict__ sell_off,
+// t % 128 of rows (t / 128) * 16 + [0, 16) in fp64 registers.
+__global__ __launch_bounds__(kInvWG) void k_coarse_inverse(int32_t n, const int32_t *__restrict__ sell_off,
                                                         const int32_t *__restrict__ sell_col,
                                                         const float *__restrict__ Ac, int64_t sell_nb,
                                                         float *__restrict__ cinv) {
@@ -253,12 +270,12 @@ __global__ __launch_bounds__(kWG) void k_coarse_inverse(int32_t n, const int32_t
     __shared__ double rowk[kMaxCoarse];
     const int32_t b = blockIdx.x;
     const int32_t nc = 3 * n;
-    for (int32_t q = threadIdx.x; q < kMaxCoarse * kMaxCoarse; q += kWG)
+    for (int32_t q = threadIdx.x; q < kMaxCoarse * kMaxCoarse; q += kInvWG)
         M[q / kMaxCoarse][q % kMaxCoarse] = 0.f;
     __syncthreads();
     const float *A = Ac + (int64_t)b * sell_nb * kB3;
     // one thread per node row: no two threads write the same row
-    for (int32_t I = threadIdx.x; I < n; I += kWG) {
+    for (int32_t I = threadIdx.x; I < n; I += kInvWG) {
         const int32_t s = I >> 6, l = I & 63;
         const int32_t o = sell_off[s], w = (sell_off[s + 1] - o) >> 6;
         for (int32_t t = 0; t < w; ++t) {
@@ -732,7 +749,7 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                                               F.sell_nb, C.A.p, C.Dinv.p, ah(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];
-    k_coarse_inverse<<<dim3((unsigned)B), kWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
+    k_coarse_inverse<<<dim3((unsigned)B), kInvWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
                                                        Lc.sell_nb, G.cinv.p);
     MOF_HIP(hipGetLastError());
 }

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
 // grad_M I and, for each corner a and alpha, u = grad_M I . e_a^alpha and the
 // f term (u (2 dI_a + sum of the other distinct corners' dI) A_T) / 12.
 // Triangle slot M of u / fc stays zero (padding of the incidence lists).
-__global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__restrict__ tri,
+__global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const int32_t *__restrict__ tri,
                                                   const int32_t *__restrict__ tri_orig,
                                                   const double *__restrict__ gw,
                                                   const double *__restrict__ e,
@@ -177,52 +177,60 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, const int32_t *__re
                                                   const double *__restrict__ dt,
                                                   double *__restrict__ u, float *__restrict__ u32,
                                                   double *__restrict__ fc) {
+    // one triangle per thread for all B systems: the geometry is read once
     const int32_t T = blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
     if (T >= M) return;
     const int32_t v[3] = {tri[3 * (int64_t)T], tri[3 * (int64_t)T + 1], tri[3 * (int64_t)T + 2]};
-    const double *g = gw + 9 * (int64_t)T;
-    const double *i0 = I0 + b * ldI;
-    const double *i1 = I1 + b * ldI;
+    double g[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) g[q] = gw[9 * (int64_t)T + q];
     // I rows are indexed by the caller's vertex ids
     const int32_t vo[3] = {tri_orig[3 * (int64_t)T], tri_orig[3 * (int64_t)T + 1],
                            tri_orig[3 * (int64_t)T + 2]};
-    const double a0 = i0[vo[0]], a1 = i0[vo[1]], a2 = i0[vo[2]];
-    double gI[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) gI[d] = (a0 * g[d] + a1 * g[3 + d]) + a2 * g[6 + d];
-    const double h = dt[b];
-    const double pd[3] = {(i1[vo[0]] - a0) / h, (i1[vo[1]] - a1) / h, (i1[vo[2]] - a2) / h};
     const double A = area[T];
-    const int64_t base = 6 * ((int64_t)b * (M + 1) + T);
-    double uo[6], fo[6];
+    double ev[3][6];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        // set(T) - {i}: distinct corners other than vertex v[a], in corner order
-        double po = 0.0;
-        int cnt = 0;
+    for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            bool dup = false;
+        for (int q = 0; q < 6; ++q) ev[a][q] = e[6 * (int64_t)v[a] + q];
+    for (int32_t b = 0; b < B; ++b) {
+        const double *i0 = I0 + b * ldI;
+        const double *i1 = I1 + b * ldI;
+        const double a0 = i0[vo[0]], a1 = i0[vo[1]], a2 = i0[vo[2]];
+        double gI[3];
 #pragma unroll
-            for (int q = 0; q < c; ++q) dup |= (v[q] == v[c]);
-            if (dup || v[c] == v[a]) continue;
-            po = cnt ? po + pd[c] : pd[c];
-            ++cnt;
+        for (int d = 0; d < 3; ++d) gI[d] = (a0 * g[d] + a1 * g[3 + d]) + a2 * g[6 + d];
+        const double h = dt[b];
+        const double pd[3] = {(i1[vo[0]] - a0) / h, (i1[vo[1]] - a1) / h, (i1[vo[2]] - a2) / h};
+        const int64_t base = 6 * ((int64_t)b * (M + 1) + T);
+        double uo[6], fo[6];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            // set(T) - {i}: distinct corners other than vertex v[a], in corner order
+            double po = 0.0;
+            int cnt = 0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                bool dup = false;
+#pragma unroll
+                for (int q = 0; q < c; ++q) dup |= (v[q] == v[c]);
+                if (dup || v[c] == v[a]) continue;
+                po = cnt ? po + pd[c] : pd[c];
+                ++cnt;
+            }
+#pragma unroll
+            for (int al = 0; al < 2; ++al) {
+                const double uu = dot64(gI, &ev[a][3 * al]);
+                uo[2 * a + al] = uu;
+                fo[2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
+            }
         }
-        const double *ea = e + 6 * (int64_t)v[a];
 #pragma unroll
-        for (int al = 0; al < 2; ++al) {
-            const double uu = dot64(gI, ea + 3 * al);
-            uo[2 * a + al] = uu;
-            fo[2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
+        for (int q = 0; q < 6; q += 2) {
+            *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
+            *reinterpret_cast<double2 *>(fc + base + q) = make_double2(fo[q], fo[q + 1]);
+            *reinterpret_cast<float2 *>(u32 + base + q) = make_float2((float)uo[q], (float)uo[q + 1]);
         }
-    }
-#pragma unroll
-    for (int q = 0; q < 6; q += 2) {
-        *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
-        *reinterpret_cast<double2 *>(fc + base + q) = make_double2(fo[q], fo[q + 1]);
-        *reinterpret_cast<float2 *>(u32 + base + q) = make_float2((float)uo[q], (float)uo[q + 1]);
     }
 }
 
@@ -485,8 +493,8 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
                 "assembly workspace / operator not prepared");
     MOF_REQUIRE(precision == MOF_PREC_MIXED ? w.A32.n >= 4 * nbs * B : w.A64.n >= 4 * nbs * B,
                 "assembly target A not allocated");
-    dim3 gt((unsigned)((m->M + kWG - 1) / kWG), (unsigned)B);
-    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
+    dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
+    k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
                                   w.u64.p, w.u32.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
     dim3 gb((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
@@ -508,7 +516,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
                             hipStream_t s) {
     Workspace &w = m->ws;
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
-    k_tri_step<<<gt, kWG, 0, s>>>(m->M, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
+    k_tri_step<<<gt, kWG, 0, s>>>(m->M, 1, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
                                   w.u64.p, w.u32.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
