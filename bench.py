@@ -3,7 +3,7 @@
 
 Metric (BASELINE.json): flow timesteps/sec on the 160k-vertex mesh
 (configs[2]: 163,842-vertex icosphere, fp32-inner PCG with fp64 refinement,
-1 x MI355X), plus the SpMV's achieved GB/s against the HBM roofline.
+aggregation-multigrid preconditioner, 1 x MI355X), plus the SpMV's achieved GB/s against the HBM roofline.
 
 One "step" = one batch of B consecutive timesteps (assembly of a1/f + A for
 every timestep, batched PCG to ||f - A V|| <= 1e-8 ||f||, planar V written
@@ -13,7 +13,8 @@ process per GPU, torchrun) each rank solves its own contiguous timesteps
 max-over-ranks wall time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-                    [--config C3] [--precision mixed|f64] [--no-cpu-baseline]
+                    [--config C3] [--precision mixed|f64] [--precond amg|jacobi]
+                    [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -44,11 +45,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=16, help="timesteps per step")
+    ap.add_argument("--batch", type=int, default=64, help="timesteps per step")
     ap.add_argument("--config", default="C3", choices=sorted(CONFIG_NAMES))
     ap.add_argument("--precision", default=None, choices=["mixed", "f64"])
-    ap.add_argument("--precond", default="jacobi", choices=["jacobi", "amg"],
-                    help="inner preconditioner (amg: mixed precision only)")
+    ap.add_argument("--precond", default=None, choices=["jacobi", "amg"],
+                    help="inner preconditioner (default: amg for mixed, jacobi for f64)")
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 64,
@@ -138,8 +139,8 @@ def main():
     V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(K_rank + 1, dtype=np.float64)
     torch.cuda.synchronize(dev)
-    opts = dict(precision=precision, batch=B, rtol=args.rtol,
-                precond=args.precond if precision == "mixed" else "jacobi")
+    precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
+    opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond)
 
     def step(s, timed):
         return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), K_rank + 1, tk, s * B,
@@ -172,7 +173,7 @@ def main():
     # roofline of the dominant kernel (k_pcg_spmv), live over the timed region
     achieved = agg["spmv_bytes"] / (agg["ms_spmv"] * 1e-3) / 1e9 if agg["ms_spmv"] > 0 else 0.0
     kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
-    traffic, traffic_src = pmc_traffic("%s/%s/B%d" % (args.config, precision, B), kname)
+    traffic, traffic_src = pmc_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), kname)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": traffic_src, "kernel": kname,
