@@ -47,18 +47,28 @@ except Exception:  # pragma: no cover
         pass
 
 # Solver options used by worker / compute_velocity_field. Override with
-# set_solver_options(); MOF_PRECISION=mixed selects fp32-inner PCG.
+# set_solver_options(); MOF_PRECISION=mixed selects fp32-inner PCG (with the
+# multigrid preconditioner unless MOF_PRECOND=jacobi).
 SOLVER_OPTIONS = {
     "precision": os.environ.get("MOF_PRECISION", "f64"),
+    "precond": os.environ.get("MOF_PRECOND", ""),
     "rtol": 1e-8,
     "batch": 0,
 }
 
 
 def set_solver_options(**kw):
-    """Update the PCG options (precision 'f64'|'mixed', rtol, batch, ...)."""
+    """Update the PCG options (precision 'f64'|'mixed', precond 'amg'|'jacobi'
+    (default: amg for mixed, jacobi for f64), rtol, batch, ...)."""
     SOLVER_OPTIONS.update(kw)
     return dict(SOLVER_OPTIONS)
+
+
+def _solver_options():
+    o = dict(SOLVER_OPTIONS)
+    if not o.get("precond"):
+        o["precond"] = "amg" if o.get("precision") == "mixed" else "jacobi"
+    return o
 
 
 def _mesh_of(a2) -> DeviceMesh:
@@ -93,7 +103,7 @@ def worker(k, a2, grad_w, e, integral_wi_wj, triangles, t_k, areas, lambda_, I_k
     mesh = _mesh_of(a2)
     I = np.stack([np.asarray(I_k_k, dtype=np.float64), np.asarray(I_k_kplus1, dtype=np.float64)])
     tk = np.array([t_k[k], t_k[k + 1]], dtype=np.float64)
-    V, st = mesh.solve_range(I, tk, 0, 1, lambda_, **SOLVER_OPTIONS)
+    V, st = mesh.solve_range(I, tk, 0, 1, lambda_, **_solver_options())
     _warn_failed(st["failed"])
     return V[0]
 
@@ -113,7 +123,7 @@ def compute_velocity_field(processes_num, time_steps, a2, grad_w, e, integral_wi
     tk = np.asarray(t_k, dtype=np.float64)
     start = time.time()
     V, stats = velocity_field_sharded(mesh, I, tk, 0, max(K, 0), lambda_, I2=I2,
-                                      devices=range(ndev), **SOLVER_OPTIONS)
+                                      devices=range(ndev), **_solver_options())
     execution_time = time.time() - start
     _warn_failed(sum(s["failed"] for s in stats))
     return [V[k] for k in range(V.shape[0])], execution_time
