@@ -167,6 +167,27 @@ int mof_velocity_vectors(int32_t device, const double *e, const double *V, int32
                          int32_t K, double *V_coord, double *speed, uint32_t flags,
                          void *stream);
 
+/* ---- the S3 CSV files (host threads, no device) ------
+ * mof_csv_write replaces the write of reshape_and_save_data
+ * (compute_optical_flow.py:314-320, pd.DataFrame(data).to_csv(path)):
+ * data (rows, cols) row-major f64, byte-identical to pandas' output (header
+ * ",0,1,...", index column, Python float repr, NaN as an empty field).
+ * mof_csv_shape / mof_csv_read replace load_potentials
+ * (compute_optical_flow.py:203-207, pd.read_csv(path, header='infer',
+ * index_col=0).values): the header line and index column are dropped, empty
+ * fields and pandas' NA strings read as NaN, numbers are parsed exactly as
+ * pandas' default float parser does (bit-identical values).
+ * threads 0 = $MOF_IO_THREADS, else $OMP_NUM_THREADS, else all host cores
+ * (at most 64). */
+int mof_csv_write(const char *path, const double *data, int64_t rows, int64_t cols,
+                  int32_t threads);
+int mof_csv_shape(const char *path, int64_t *rows, int64_t *cols);
+#define MOF_CSV_ROUND_TRIP 1u /* mof_csv_read: correctly rounded parse (pandas
+                                  float_precision='round_trip') instead of
+                                  pandas' default parser */
+int mof_csv_read(const char *path, double *out, int64_t rows, int64_t cols, uint32_t flags,
+                 int32_t threads);
+
 /* Measurement helper for bench.py: launches the PCG SpMV kernel `reps` times
  * back to back on `batch` systems of the last solve's working set, timed with
  * HIP events on the handle's stream. Returns the mean launch time and the

@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <new>
 
 #include "mof_internal.h"
@@ -94,6 +95,9 @@ void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop
 }
 
 }  // namespace
+
+// error handling for the host-only entry points of mof_io.cpp
+int mof_io_guard(const std::function<void()> &f) { return guarded(f); }
 
 extern "C" {
 

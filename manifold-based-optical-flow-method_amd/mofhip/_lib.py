@@ -32,6 +32,7 @@ MOF_IO_DEVICE = 1
 MOF_NO_BLOCK_JACOBI = 2
 MOF_TIME_SPMV = 4
 MOF_PRECOND_AMG = 8
+MOF_CSV_ROUND_TRIP = 1
 MOF_CSR_A2 = 0
 MOF_CSR_A_LAST = 1
 
@@ -40,6 +41,7 @@ EXPORTS = (
     "mof_version", "mof_last_error", "mof_device_count", "mof_mesh_create",
     "mof_mesh_destroy", "mof_mesh_get_info", "mof_geometry_export", "mof_csr_export",
     "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
+    "mof_csv_write", "mof_csv_shape", "mof_csv_read",
 )
 
 
@@ -128,6 +130,9 @@ def lib():
             "mof_solve_range": ([P, P, P, P, i32, i32, i32, f64, P, P, P], ctypes.c_int),
             "mof_bench_spmv": ([P, u32, i32, i32, P, P], ctypes.c_int),
             "mof_velocity_vectors": ([i32, P, P, i32, i32, P, P, u32, P], ctypes.c_int),
+            "mof_csv_write": ([ctypes.c_char_p, P, i64, i64, i32], ctypes.c_int),
+            "mof_csv_shape": ([ctypes.c_char_p, P, P], ctypes.c_int),
+            "mof_csv_read": ([ctypes.c_char_p, P, i64, i64, u32, i32], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

@@ -15,8 +15,9 @@ compute_geometrical_quantities  mesh build on the GPU; ``a2`` is a
 worker (:100-149)              one timestep: GPU assembly + PCG
 compute_velocity_field         timesteps batched per GPU, contiguous
   (:152-194)                     k-shards over ``min(processes_num, #GPUs)``
-load_potentials (:203-207)     same (pandas CSV)
-reshape_and_save_data          same (pandas CSV)
+load_potentials (:203-207)     threaded native reader, pandas' parser
+                                 restated (bit-identical values)
+reshape_and_save_data          threaded native writer, pandas' bytes
   (:314-320)
 compute_orthonormal_basis,     host helpers with the reference's formulas;
 compute_gradient_w, compute_a2,  not on the hot path (the GPU kernels
@@ -137,16 +138,32 @@ def load_surface(surface_path):
 
 
 def load_potentials(csv_path):
-    """(T, N) potentials from the S2 CSV (first column is the index)."""
-    import pandas as pd
-    return pd.read_csv(csv_path, sep=",", header="infer", index_col=0).values
+    """(T, N) potentials from the S2 CSV (reference :203-207,
+    ``pd.read_csv(path, sep=',', header='infer', index_col=0).values``):
+    parsed by libmofhip's threaded reader with pandas' own float parser
+    restated (bit-identical values); a file it cannot read as a numeric
+    table goes to pandas itself."""
+    from mofhip import csvio
+    from mofhip._lib import MofError
+    try:
+        return csvio.read_csv(csv_path)
+    except MofError:
+        import pandas as pd
+        return pd.read_csv(csv_path, sep=",", header="infer", index_col=0).values
 
 
 def reshape_and_save_data(data, file_path):
-    """Flatten to (rows, -1) and write a pandas CSV (e: (N,6); V_k: (T-1, 2N))."""
-    import pandas as pd
+    """Flatten to (rows, -1) and write the CSV (reference :314-320; e: (N,6),
+    V_k: (T-1, 2N)): float data through libmofhip's threaded writer, the
+    same bytes as ``pd.DataFrame(...).to_csv(file_path)``."""
     arr = np.asarray(data)
-    pd.DataFrame(arr.reshape(arr.shape[0], -1)).to_csv(file_path)
+    reshaped = arr.reshape(arr.shape[0], -1)
+    if reshaped.dtype.kind == "f":
+        from mofhip import csvio
+        csvio.write_csv(file_path, reshaped)
+    else:
+        import pandas as pd
+        pd.DataFrame(reshaped).to_csv(file_path)
     print(f"{file_path}文件保存成功。")
 
 
