@@ -188,6 +188,20 @@ int mof_csv_shape(const char *path, int64_t *rows, int64_t *cols);
 int mof_csv_read(const char *path, double *out, int64_t rows, int64_t cols, uint32_t flags,
                  int32_t threads);
 
+/* ---- the S3 surface without pyvista (host) -----------
+ * Replace pv.read(surface_path) and the attributes S3 takes from it
+ * (S3…py:75-84): points (N,3) float32, triangles (M,3) int64 (faces
+ * reshaped), point normals (N,3) float32 (vtkPolyDataNormals restated, or
+ * the file's nx/ny/nz when present), cell areas (M,) float64
+ * (compute_cell_sizes()['Area']). PLY: ascii and binary, triangle faces.
+ * VTK is absent here: these restate its algorithms, parity unpinned. */
+int mof_ply_info(const char *path, int64_t *n_vertices, int64_t *n_faces, uint32_t *has_normals);
+int mof_ply_read(const char *path, float *points, int64_t *triangles, float *normals);
+int mof_point_normals(const float *points, const int64_t *triangles, int64_t N, int64_t M,
+                      float *normals);
+int mof_cell_areas(const float *points, const int64_t *triangles, int64_t N, int64_t M,
+                   double *areas);
+
 /* Measurement helper for bench.py: launches the PCG SpMV kernel `reps` times
  * back to back on `batch` systems of the last solve's working set, timed with
  * HIP events on the handle's stream. Returns the mean launch time and the

@@ -41,7 +41,8 @@ EXPORTS = (
     "mof_version", "mof_last_error", "mof_device_count", "mof_mesh_create",
     "mof_mesh_destroy", "mof_mesh_get_info", "mof_geometry_export", "mof_csr_export",
     "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
-    "mof_csv_write", "mof_csv_shape", "mof_csv_read",
+    "mof_csv_write", "mof_csv_shape", "mof_csv_read", "mof_ply_info", "mof_ply_read",
+    "mof_point_normals", "mof_cell_areas",
 )
 
 
@@ -133,6 +134,10 @@ def lib():
             "mof_csv_write": ([ctypes.c_char_p, P, i64, i64, i32], ctypes.c_int),
             "mof_csv_shape": ([ctypes.c_char_p, P, P], ctypes.c_int),
             "mof_csv_read": ([ctypes.c_char_p, P, i64, i64, u32, i32], ctypes.c_int),
+            "mof_ply_info": ([ctypes.c_char_p, P, P, P], ctypes.c_int),
+            "mof_ply_read": ([ctypes.c_char_p, P, P, P], ctypes.c_int),
+            "mof_point_normals": ([P, P, i64, i64, P], ctypes.c_int),
+            "mof_cell_areas": ([P, P, i64, i64, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

@@ -131,9 +131,14 @@ def compute_velocity_field(processes_num, time_steps, a2, grad_w, e, integral_wi
 
 
 def load_surface(surface_path):
-    """PLY surface via pyvista, as the reference (:197-200); pyvista is an
-    optional dependency."""
-    import pyvista as pv  # noqa: WPS433 (optional)
+    """The surface (reference :197-200, ``pv.read``): pyvista when it is
+    installed, else libmofhip's PLY reader with the attributes S3 uses
+    (``points``, ``faces``, ``point_normals``, ``compute_cell_sizes``)."""
+    try:
+        import pyvista as pv  # noqa: WPS433 (optional)
+    except ImportError:
+        from mofhip.surface import read_surface
+        return read_surface(surface_path)
     return pv.read(surface_path)
 
 
