@@ -167,6 +167,22 @@ int mof_velocity_vectors(int32_t device, const double *e, const double *V, int32
                          int32_t K, double *V_coord, double *speed, uint32_t flags,
                          void *stream);
 
+/* find_singularity_points(coordinates, triangles, V_now,
+ * eps) (find_singularity_point.py:140-189) for K velocity fields V_coord
+ * (K,N,3) at once. coords (N,3) f64, or f32 with MOF_COORDS_F32 (pyvista
+ * points; the triangle normal is then formed in float32 as numpy does);
+ * triangles (M,3) int32. Outputs: vmax (K) = v_length_max (bit-identical),
+ * vertex_flag (K,N) = |V_i/vmax| <= eps (bit-identical), triangle_flag (K,M)
+ * = zero inside the triangle (has_zero_velocity_interior, skipped when a
+ * corner is flagged) with its barycentric (lam, mu) in lam_mu (K,M,2) (the
+ * reference's np.linalg.lstsq is restated by QR + 2x2 SVD: equal to
+ * rounding). Host pointers, or device pointers with MOF_IO_DEVICE. */
+#define MOF_COORDS_F32 32u      /* mof_singularities: coords are float32 */
+int mof_singularities(int32_t device, const void *coords, const int32_t *triangles, int32_t N,
+                      int32_t M, const double *V_coord, int32_t K, double eps, uint32_t flags,
+                      void *stream, double *vmax, uint8_t *vertex_flag, uint8_t *triangle_flag,
+                      double *lam_mu);
+
 /* ---- the S3 CSV files (host threads, no device) ------
  * mof_csv_write replaces the write of reshape_and_save_data
  * (compute_optical_flow.py:314-320, pd.DataFrame(data).to_csv(path)):

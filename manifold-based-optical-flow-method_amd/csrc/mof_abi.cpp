@@ -467,6 +467,57 @@ int mof_velocity_vectors(int32_t device, const double *e, const double *V, int32
     });
 }
 
+int mof_singularities(int32_t device, const void *coords, const int32_t *triangles, int32_t N, int32_t M,
+                      const double *V_coord, int32_t K, double eps, uint32_t flags, void *stream,
+                      double *vmax, uint8_t *vertex_flag, uint8_t *triangle_flag, double *lam_mu) {
+    return guarded([&] {
+        MOF_REQUIRE(coords && V_coord && vmax && vertex_flag && N > 0 && M >= 0 && K >= 0,
+                    "bad arguments");
+        MOF_REQUIRE(M == 0 || (triangles && triangle_flag && lam_mu), "NULL triangle argument");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DeviceGuard dg(device);
+        if (K == 0) return;
+        hipStream_t s = (hipStream_t)stream;
+        const bool f32 = (flags & MOF_COORDS_F32) != 0;
+        const size_t cb = 3 * (size_t)N * (f32 ? sizeof(float) : sizeof(double));
+        if (!(flags & MOF_IO_DEVICE)) {
+            // triangle indices checked on the host before any gather
+            for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+                MOF_REQUIRE(triangles[q] >= 0 && triangles[q] < N, "triangle index out of range");
+        }
+        if (flags & MOF_IO_DEVICE) {
+            mof::launch_singularities(N, M, K, coords, f32, triangles, V_coord, eps, vmax, vertex_flag,
+                                      triangle_flag, lam_mu, s);
+            MOF_HIP(hipStreamSynchronize(s));
+            return;
+        }
+        const size_t nk = (size_t)N * K, mk = (size_t)M * K;
+        mof::DevArray<uint8_t> dc, dvf, dtf;
+        mof::DevArray<int32_t> dt;
+        mof::DevArray<double> dV, dmax, dlm;
+        dc.alloc(cb);
+        MOF_HIP(hipMemcpyAsync(dc.p, coords, cb, hipMemcpyHostToDevice, s));
+        dt.alloc(3 * (size_t)M);
+        if (M) dt.upload(triangles, 3 * (size_t)M, s);
+        dV.alloc(3 * nk);
+        dV.upload(V_coord, 3 * nk, s);
+        dmax.alloc(K);
+        dvf.alloc(nk);
+        dtf.alloc(mk);
+        dlm.alloc(2 * mk);
+        mof::launch_singularities(N, M, K, dc.p, f32, dt.p, dV.p, eps, dmax.p, dvf.p, dtf.p, dlm.p, s);
+        MOF_HIP(hipMemcpyAsync(vmax, dmax.p, K * sizeof(double), hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipMemcpyAsync(vertex_flag, dvf.p, nk, hipMemcpyDeviceToHost, s));
+        if (M) {
+            MOF_HIP(hipMemcpyAsync(triangle_flag, dtf.p, mk, hipMemcpyDeviceToHost, s));
+            MOF_HIP(hipMemcpyAsync(lam_mu, dlm.p, 2 * mk * sizeof(double), hipMemcpyDeviceToHost, s));
+        }
+        MOF_HIP(hipStreamSynchronize(s));
+    });
+}
+
 int mof_bench_spmv(mof_mesh *m, uint32_t precision, int32_t batch, int32_t reps,
                    double *ms_per_launch, double *bytes_per_launch) {
     return guarded([&] {

@@ -185,6 +185,10 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
 void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
                             hipStream_t s);
 void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);  // V in caller order
+// find_singularity_points for K fields (mof_sing.hip); device pointers
+void launch_singularities(int32_t N, int32_t M, int32_t K, const void *coords, bool f32, const int32_t *tri,
+                          const double *V, double eps, double *vmax, uint8_t *vflag, uint8_t *tflag,
+                          double *lam_mu, hipStream_t s);
 void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double *V, double *Vc,
                              double *speed, hipStream_t s);
 

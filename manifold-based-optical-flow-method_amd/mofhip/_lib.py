@@ -33,6 +33,7 @@ MOF_NO_BLOCK_JACOBI = 2
 MOF_TIME_SPMV = 4
 MOF_PRECOND_AMG = 8
 MOF_CSV_ROUND_TRIP = 1
+MOF_COORDS_F32 = 32
 MOF_CSR_A2 = 0
 MOF_CSR_A_LAST = 1
 
@@ -42,7 +43,7 @@ EXPORTS = (
     "mof_mesh_destroy", "mof_mesh_get_info", "mof_geometry_export", "mof_csr_export",
     "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
     "mof_csv_write", "mof_csv_shape", "mof_csv_read", "mof_ply_info", "mof_ply_read",
-    "mof_point_normals", "mof_cell_areas",
+    "mof_point_normals", "mof_cell_areas", "mof_singularities",
 )
 
 
@@ -138,6 +139,8 @@ def lib():
             "mof_ply_read": ([ctypes.c_char_p, P, P, P], ctypes.c_int),
             "mof_point_normals": ([P, P, i64, i64, P], ctypes.c_int),
             "mof_cell_areas": ([P, P, i64, i64, P], ctypes.c_int),
+            "mof_singularities": ([i32, P, P, i32, i32, P, i32, f64, u32, P, P, P, P, P],
+                                  ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

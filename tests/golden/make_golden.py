@@ -16,8 +16,12 @@ Cases:
   G6 S3's epilogue on G1's V_k: find_singularity_point.process_V_k(V_k, e)
      (find_singularity_point.py:28-69) and the speed
      V_c = sqrt(sum(V_k_coord[:, :, :3] ** 2, axis=2)) (S3…py:130-132)
+  G7 find_singularity_point.find_singularity_points (:140-189) on G1's mesh
+     (float64 points) and G3's (float32 points) for G6's 15 fields plus 3
+     synthetic tangent fields with many zeros, eps 1e-3 and 0.05: v_length_max,
+     zero-vertex flags, zero-triangle flags and (lam, mu)
 
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py [G7]
 """
 from __future__ import annotations
 
@@ -90,7 +94,56 @@ def run_case(ref, name, coords, tris, normals, areas, I, t_k, capture_ks=(0,), l
     print(name, {k: getattr(v, "shape", ()) for k, v in out.items()})
 
 
+def tangent_fields(p, K, seed=0):
+    """K smooth ambient fields projected on the sphere's tangent planes."""
+    rng = np.random.default_rng(seed)
+    n = p / np.linalg.norm(p, axis=1, keepdims=True)
+    out = []
+    for _ in range(K):
+        f = rng.uniform(0.2, 0.6, 3)
+        ph = rng.uniform(0, 6.28, 3)
+        a = np.stack([np.sin(f[0] * p[:, 1] + ph[0]), np.cos(f[1] * p[:, 2] + ph[1]),
+                      np.sin(f[2] * p[:, 0] + ph[2])], axis=1)
+        out.append(a - np.sum(a * n, axis=1, keepdims=True) * n)
+    return np.asarray(out)
+
+
+def make_g7():
+    import contextlib
+    import io
+    fsp = load_reference("utils.find_singularity_point")
+    g1 = np.load(os.path.join(HERE, "G1_ico642.npz"))
+    g6 = np.load(os.path.join(HERE, "G6_epilogue.npz"))
+    g3 = np.load(os.path.join(HERE, "G3_ico642_f32.npz"))
+    tri = g1["triangles"]
+    V = np.concatenate([g6["V_k_coord"], tangent_fields(g1["coordinates"], 3)])
+    out = {"triangles": tri, "V": V, "eps": np.array([1e-3, 0.05])}
+    for tag, coords in (("f64", g1["coordinates"]), ("f32", g3["coordinates"])):
+        out["coords_" + tag] = coords
+        for ei, eps in enumerate(out["eps"]):
+            K, N, M = len(V), len(coords), len(tri)
+            vmax, vf = np.zeros(K), np.zeros((K, N), bool)
+            tf, lm = np.zeros((K, M), bool), np.zeros((K, M, 2))
+            for k in range(K):
+                with contextlib.redirect_stdout(io.StringIO()):
+                    sv, si, vm = fsp.find_singularity_points(coords, tri, V[k], eps)
+                vmax[k] = vm
+                for i, _ in sv:
+                    vf[k, i] = True
+                for rec in si:
+                    tf[k, rec[0]] = True
+                    lm[k, rec[0]] = rec[3][:2]
+            key = "%s_e%d" % (tag, ei)
+            out["vmax_" + key], out["vflag_" + key] = vmax, vf
+            out["tflag_" + key], out["lam_mu_" + key] = tf, lm
+            print("G7", key, "vertices", int(vf.sum()), "interiors", int(tf.sum()))
+    np.savez_compressed(os.path.join(HERE, "G7_singularities.npz"), **out)
+
+
 def main():
+    if sys.argv[1:] == ["G7"]:
+        make_g7()
+        return
     ref = load_reference()
     # G1
     p, t = synth.icosphere(8, 10.0)
@@ -121,6 +174,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "G6_epilogue.npz"), V_k=g1["V_k"], e=g1["e"],
                         V_k_coord=coord, V_c=V_c)
     print("G6_epilogue", coord.shape, V_c.shape)
+    make_g7()
 
 
 if __name__ == "__main__":
