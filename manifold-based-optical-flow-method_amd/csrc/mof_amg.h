@@ -10,7 +10,7 @@ namespace mof {
 struct AmgParams {
     int32_t max_levels = 10;
     int32_t max_coarse_dofs = 128;  // coarsest level: dense inverse in LDS (fp64), one workgroup per system
-    float omega = 0.7f;             // damped block-Jacobi smoother
+    float omega = 0.85f;            // damped block-Jacobi smoother (1.0 diverges on irregular meshes)
 };
 
 // One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser
@@ -61,7 +61,7 @@ struct AmgDevice {
     bool built = false;
     int32_t cap = 0;
     int32_t nc = 0;  // coarsest dofs (dense)
-    float omega = 0.7f;
+    float omega = 0.85f;
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)

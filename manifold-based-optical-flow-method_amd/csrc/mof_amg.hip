@@ -173,13 +173,15 @@ __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__rest
 // 1 on dead dofs and stores its 3x3 inverse for the smoother.
 template <int BSF>
 __global__ __launch_bounds__(kWG) void k_galerkin(
-    int64_t c_sell_nb, int32_t nC, const int32_t *__restrict__ c_sell_row,
+    int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, float *__restrict__ Dc,
     uint2 *__restrict__ Ah) {
-    const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
+    // XCD-aware tiles: the B systems of a tile share its gather lists and Q
+    int32_t tile, b;
+    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= c_sell_nb) return;
     const int32_t I = c_sell_row[pos];
     if (I >= nC) return;  // rows past n in the last slice
@@ -618,6 +620,7 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
 }
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
+inline dim3 gtile(int64_t n, int32_t B) { return dim3(xcd_grid((int32_t)((n + kWG - 1) / kWG), B)); }
 
 MatH level0_mat(mof_mesh *m) {
     MatH mt;
@@ -633,7 +636,8 @@ MatH level0_mat(mof_mesh *m) {
 // ---- host side ---------------------------------------------------------------
 
 bool amg_build(mof_mesh *m) {
-    const AmgParams prm;
+    AmgParams prm;
+    if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knob
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
     AmgDevice &G = *m->amg;
@@ -739,12 +743,12 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
         if (l == 0)
-            k_galerkin<2><<<grid2(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, C.sell_row.p, C.diag_pos.p,
+            k_galerkin<2><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
                                                               m->pat.sell_nb(), C.A.p, C.Dinv.p,
                                                               ah(C));
         else
-            k_galerkin<3><<<grid2(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, C.sell_row.p, C.diag_pos.p,
+            k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
                                                               F.sell_nb, C.A.p, C.Dinv.p, ah(C));
     }

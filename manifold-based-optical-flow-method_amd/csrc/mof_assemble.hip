@@ -10,6 +10,7 @@
 // All per-timestep accumulation is a gather in triangle order over the
 // pre-built contribution lists (mof_pattern.cpp): deterministic, no atomics.
 #include "mof_internal.h"
+#include "mof_rowkern.h"
 
 namespace mof {
 namespace {
@@ -244,14 +245,17 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
 // trip per term. SELL padding is never written and stays zero.
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_assemble_blocks(
-    int64_t sell_nb, int32_t N, int32_t M, const int32_t *__restrict__ sell_blk,
+    int64_t sell_nb, int32_t N, int32_t M, int32_t B, const int32_t *__restrict__ sell_blk,
     const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
     const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
     const double *__restrict__ iw, const double *__restrict__ a2s, const double *__restrict__ u,
     const double *__restrict__ fc, int block_jacobi, V *__restrict__ A,
     double *__restrict__ dinv64, float *__restrict__ dinv32, double *__restrict__ rhs) {
-    const int64_t pos = (int64_t)blockIdx.x * kWG + threadIdx.x;
-    const int32_t b = blockIdx.y;
+    // XCD-aware tiles: the B systems of a 256-slot tile run back to back on
+    // one XCD and share the tile's structure, lambda a2 and iw in its L2
+    int32_t tile, b;
+    if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= sell_nb) return;
     const int32_t p = sell_blk[pos];
     if (p < 0) return;
@@ -497,15 +501,15 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
                                   w.u64.p, w.u32.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
-    dim3 gb((unsigned)((snb + kWG - 1) / kWG), (unsigned)B);
+    const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B));
     const int bj = block_jacobi ? 1 : 0;
     if (precision == MOF_PREC_MIXED)
-        k_assemble_blocks<float><<<gb, kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
+        k_assemble_blocks<float><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
                                                     m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
                                                     m->a2s64.p, w.u64.p, w.fc.p, bj, w.A32.p,
                                                     w.dinv64.p, w.dinv32.p, w.rhs.p);
     else
-        k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
+        k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
                                                      m->a2s64.p, w.u64.p, w.fc.p, bj, w.A64.p,
                                                      w.dinv64.p, w.dinv32.p, w.rhs.p);

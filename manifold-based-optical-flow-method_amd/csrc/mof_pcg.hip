@@ -326,21 +326,21 @@ __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
 // partial |r|^2 and |f|^2.
-__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk,
+__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B,
                                                   const double *__restrict__ rhs,
                                                   const double *__restrict__ x64,
                                                   const int32_t *__restrict__ sysi,
                                                   double *__restrict__ r64,
                                                   double *__restrict__ part) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.y;
-    if (!sysi[b * kSysStride + SI_ACTIVE]) return;
+    int32_t rb, b;  // XCD-aware: the systems of a row block share its a2 blocks in L2
+    if (!xcd_map(nblk, B, rb, b) || !sysi[b * kSysStride + SI_ACTIVE]) return;
     const int32_t N = op.N;
     const int64_t vb = (int64_t)b * N;
     double rr = 0.0, ff = 0.0;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-        const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         double y0, y1;
         apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
     double v[2] = {rr, ff};
     block_sum<2>(v, lds);
     if (threadIdx.x == 0) {
-        double *o = part + 2 * ((int64_t)b * nblk + blockIdx.x);
+        double *o = part + 2 * ((int64_t)b * nblk + rb);
         o[0] = v[0];
         o[1] = v[1];
     }
@@ -671,7 +671,8 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
                                  sp.precision, tm, &m->iter_hint[std::min(o, 15)], false);
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
-        k_residual<<<g, kWG, 0, s>>>(o64, w.nblk, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
+        k_residual<<<dim3(xcd_grid(w.nblk, B)), kWG, 0, s>>>(o64, w.nblk, B, w.rhs.p, w.x64.p, w.sysi.p,
+                                                              w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(w.nblk, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
         MOF_HIP(hipGetLastError());

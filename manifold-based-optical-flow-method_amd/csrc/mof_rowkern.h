@@ -143,14 +143,17 @@ __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_
 
 // XCD-aware workgroup -> (row block, system): workgroups w and w+8 share an
 // XCD (round-robin dispatch; speed only, never correctness). XCD x takes row
-// blocks [x*chunk, (x+1)*chunk) of every system, system by system.
+// blocks [x*chunk, (x+1)*chunk) of every system, row block by row block with
+// the B systems of a row block back to back: the workgroups in flight on an
+// XCD then share the row block's column indices (and any other per-row data
+// common to all systems) in that XCD's L2.
 __device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, int32_t &sys) {
     const int32_t w = blockIdx.x;
     const int32_t q = w >> 3;
     const int32_t chunk = (nblk + 7) >> 3;
-    sys = q / chunk;
-    rb = (w & 7) * chunk + q % chunk;
-    return rb < nblk && sys < B;
+    sys = q % B;
+    rb = (w & 7) * chunk + q / B;
+    return rb < nblk && q / B < chunk;
 }
 
 inline unsigned xcd_grid(int32_t nblk, int32_t B) {
