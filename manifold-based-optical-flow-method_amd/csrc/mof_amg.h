@@ -49,6 +49,8 @@ struct AmgDevLevel {
     DevArray<int32_t> sell_off, sell_col, sell_row, diag_pos;  // level >= 1
     DevArray<uint8_t> dead;                          // level >= 1
     DevArray<int32_t> agg, mptr, apos, gptr, gent;  // transition to level + 1
+    DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
+    int32_t ngrp = 0;
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap
     DevArray<float> A, Dinv;     // [B][sell_nb][12], [B][n][12] (level >= 1)

@@ -497,12 +497,57 @@ __global__ __launch_bounds__(kWG) void k_res3(Lvl L, const int32_t *__restrict__
     res3_node(L, b, i);
 }
 
+// Restriction by aggregate groups: a workgroup takes whole aggregates with
+// at most kRG members in total (group boundaries built on the host), reads
+// its members' r and Q rows coalesced (one member per thread), stages the
+// per-member contributions Q_q^T r_q in LDS, and one thread per aggregate
+// sums them in member order (deterministic). An aggregate with more than
+// kRG members forms its own group and is summed straight from memory.
+constexpr int kRG = 1024;
+
 template <int BSF>
-__global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, int32_t smooth, float omega,
+__global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
+                                                  int32_t B, int32_t smooth, float omega,
                                                   const int32_t *__restrict__ sysi) {
-    const int32_t I = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
-    if (I >= C.n || retired(sysi, b)) return;
-    restrict_node<BSF>(F, C, b, I, smooth != 0, omega);
+    __shared__ float con[3][kRG];
+    int32_t g, b;
+    if (!xcd_map(ngrp, B, g, b) || retired(sysi, b)) return;
+    const int32_t I0 = grp[g], I1 = grp[g + 1];
+    const int32_t q0 = F.mptr[I0], q1 = F.mptr[I1];
+    if (q1 - q0 > kRG) {  // one oversized aggregate
+        if (threadIdx.x == 0) restrict_node<BSF>(F, C, b, I0, smooth != 0, omega);
+        return;
+    }
+    const float *rb = F.r + (int64_t)b * F.n * vstride<BSF>();
+    for (int32_t q = q0 + threadIdx.x; q < q1; q += kWG) {
+        float ri[BSF];
+        ldv<BSF>(rb, q, ri);
+        const float *qm = F.Qm + (int64_t)q * BSF * 3;
+        float c3[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < BSF; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) c3[c] += qm[3 * k + c] * ri[k];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) con[c][q - q0] = c3[c];
+    }
+    __syncthreads();
+    for (int32_t I = I0 + threadIdx.x; I < I1; I += kWG) {
+        float acc[3] = {0.f, 0.f, 0.f};
+        for (int32_t q = F.mptr[I]; q < F.mptr[I + 1]; ++q)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[c] += con[c][q - q0];
+        const int64_t vo = (int64_t)b * C.n * 4;
+        stv<3>(C.b + vo, I, acc);
+        if (smooth) {
+            float d[3][3], x[3];
+            ldm<3>(C.Dinv + (int64_t)b * C.n * kB3, I, d);
+            matvec<3>(d, acc, x);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] *= omega;
+            stv<3>(C.x + vo, I, x);
+        }
+    }
 }
 
 template <int BSF>
@@ -685,6 +730,16 @@ bool amg_build(mof_mesh *m) {
             put_i(D.gent, L.gent);
             put_f(D.Q, L.Q);
             put_f(D.Qm, L.Qm);
+            // restriction groups: whole aggregates, <= kRG members each
+            std::vector<int32_t> grp{0};
+            const int32_t na = (int32_t)L.mptr.size() - 1;
+            for (int32_t I = 0; I < na; ++I) {
+                const int32_t g0 = grp.back();
+                if (I > g0 && L.mptr[I + 1] - L.mptr[g0] > kRG) grp.push_back(I);
+            }
+            grp.push_back(na);
+            D.ngrp = (int32_t)grp.size() - 1;
+            put_i(D.rgrp, grp);
         }
     }
     G.nc = H.coarse_dofs;
@@ -798,10 +853,12 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
             k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x, v[0].apos, sysi, v[0].r);
-            k_restrict<2><<<grid2(v[1].n, B), kWG, 0, s>>>(v[0], v[1], smooth, om, sysi);
+            k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B)), kWG, 0, s>>>(
+                v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om, sysi);
         } else {
             k_res3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], sysi);
-            k_restrict<3><<<grid2(v[l + 1].n, B), kWG, 0, s>>>(v[l], v[l + 1], smooth, om, sysi);
+            k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B)), kWG, 0, s>>>(
+                v[l], v[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om, sysi);
         }
     }
     SubArgs sa;
