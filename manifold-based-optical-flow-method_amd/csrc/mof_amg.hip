@@ -113,52 +113,6 @@ __device__ __forceinline__ void st3(float *A, int64_t idx, const float (&a)[3][3
     for (int r = 0; r < 3; ++r) p[r] = make_float4(a[r][0], a[r][1], a[r][2], 0.f);
 }
 
-// bf16 copies of the level-0 operator for the smoother sweeps (the
-// preconditioner only needs an SPD approximation of A; rounding the blocks
-// (i,j) and (j,i)^T alike keeps it symmetric) -- half the bytes of A32.
-__device__ __forceinline__ uint32_t bf16_bits(float f) {
-    const uint32_t u = __float_as_uint(f);
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;  // round to nearest even
-}
-__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
-
-struct MatH {
-    int64_t sell_nb;
-    const int32_t *sell_off, *sell_col;
-    const uint2 *A;  // [B][sell_nb] 4 bf16 per block
-};
-
-// spmv_row of mof_rowkern.h on the bf16 blocks
-__device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i, const float *__restrict__ x,
-                                           float &y0, float &y1) {
-    constexpr int U = 8;
-    const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
-    const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = mt.sell_off[s];
-    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
-    float a0 = 0.f, a1 = 0.f;
-    for (int32_t t0 = 0; t0 < w; t0 += U) {
-        int32_t j[U];
-        uint2 blk[U];
-        float2 xj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-#pragma unroll
-        for (int u = 0; u < U; ++u) blk[u] = A[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-#pragma unroll
-        for (int u = 0; u < U; ++u) xj[u] = reinterpret_cast<const float2 *>(x)[j[u]];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool on = t0 + u < w;
-            a0 += on ? bf16_lo(blk[u].x) * xj[u].x + bf16_hi(blk[u].x) * xj[u].y : 0.f;
-            a1 += on ? bf16_lo(blk[u].y) * xj[u].x + bf16_hi(blk[u].y) * xj[u].y : 0.f;
-        }
-    }
-    y0 = a0;
-    y1 = a1;
-}
-
 // ---- per-timestep setup --------------------------------------------------
 
 __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
@@ -633,7 +587,7 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 // Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
 // of the row block's record). PCG row layout, XCD-aware grid.
 __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
-                                               const float *__restrict__ Dinv,
+                                               const uint2 *__restrict__ Dh,
                                                const float *__restrict__ rv,
                                                const float *__restrict__ xv, float omega,
                                                const int32_t *__restrict__ sysi,
@@ -651,11 +605,9 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
         spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
         const float2 xi = reinterpret_cast<const float2 *>(xv)[vb + i];
-        float d[4];
-        ld_blk(Dinv, vb + i, d);
-        const float s0 = ri.x - y0, s1 = ri.y - y1;
-        const float z0 = xi.x + omega * (d[0] * s0 + d[1] * s1);
-        const float z1 = xi.y + omega * (d[2] * s0 + d[3] * s1);
+        const float2 ds = bf16_mat2(Dh[vb + i], ri.x - y0, ri.y - y1);
+        const float z0 = xi.x + omega * ds.x;
+        const float z1 = xi.y + omega * ds.y;
         reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
         rz += (double)ri.x * z0 + (double)ri.y * z1;
     }
@@ -764,6 +716,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.x.alloc(2 * n * B);
             D.r.alloc(2 * n * B);
             G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
+            G.D0h.alloc(2 * n * B);
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
@@ -783,8 +736,14 @@ void amg_ensure(mof_mesh *m, int32_t B) {
     MOF_HIP(hipStreamSynchronize(s));
 }
 
-float *amg_level0_x(mof_mesh *m) { return m->amg->lv[0].x.p; }
-float amg_omega(const mof_mesh *m) { return m->amg->omega; }
+AmgFine amg_fine(mof_mesh *m) {
+    AmgDevice &G = *m->amg;
+    AmgFine f;
+    f.D0h = G.D0h.p;
+    f.x0 = G.lv[0].x.p;
+    f.omega = G.omega;
+    return f;
+}
 
 static uint2 *ah(AmgDevLevel &C) { return C.Ah.n > 1 ? reinterpret_cast<uint2 *>(C.Ah.p) : nullptr; }
 
@@ -795,6 +754,9 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     const int64_t nb0 = m->pat.sell_nb() * B;
     k_to_bf16<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
         nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
+    const int64_t nd0 = (int64_t)m->N * B;
+    k_to_bf16<<<dim3((unsigned)((nd0 + kWG - 1) / kWG)), kWG, 0, s>>>(
+        nd0, reinterpret_cast<const float4 *>(w.dinv32.p), reinterpret_cast<uint2 *>(G.D0h.p));
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
         if (l == 0)
@@ -873,7 +835,8 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = S - 1; l >= 0; --l) {
         if (l == 0) {
             k_prolong<2><<<grid2(v[0].n, B), kWG, 0, s>>>(v[0], v[1], sysi);
-            k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, w.dinv32.p, r0, v[0].x, om, sysi, z0, part_slot);
+            k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, reinterpret_cast<const uint2 *>(G.D0h.p), r0,
+                                       v[0].x, om, sysi, z0, part_slot);
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
             k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om, sysi);

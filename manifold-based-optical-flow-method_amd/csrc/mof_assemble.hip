@@ -176,8 +176,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
                                                   const double *__restrict__ I0,
                                                   const double *__restrict__ I1, int64_t ldI,
                                                   const double *__restrict__ dt,
-                                                  double *__restrict__ u, float *__restrict__ u32,
-                                                  double *__restrict__ fc) {
+                                                  double *__restrict__ u, double *__restrict__ fc) {
     // one triangle per thread for all B systems: the geometry is read once
     const int32_t T = blockIdx.x * kWG + threadIdx.x;
     if (T >= M) return;
@@ -230,7 +229,6 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
         for (int q = 0; q < 6; q += 2) {
             *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
             *reinterpret_cast<double2 *>(fc + base + q) = make_double2(fo[q], fo[q + 1]);
-            *reinterpret_cast<float2 *>(u32 + base + q) = make_float2((float)uo[q], (float)uo[q + 1]);
         }
     }
 }
@@ -492,14 +490,14 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     Workspace &w = m->ws;
     check_mesh_arrays(m);
     const size_t nbs = (size_t)m->pat.sell_nb(), mu = 6 * ((size_t)m->M + 1) * B;
-    MOF_REQUIRE(B >= 1 && B <= w.cap && I0 && I1 && w.u64.n >= mu && w.u32.n >= mu && w.fc.n >= mu &&
+    MOF_REQUIRE(B >= 1 && B <= w.cap && I0 && I1 && w.u64.n >= mu && w.fc.n >= mu &&
                     w.dt.n >= (size_t)B && m->a2s_valid,
                 "assembly workspace / operator not prepared");
     MOF_REQUIRE(precision == MOF_PREC_MIXED ? w.A32.n >= 4 * nbs * B : w.A64.n >= 4 * nbs * B,
                 "assembly target A not allocated");
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
-                                  w.u64.p, w.u32.p, w.fc.p);
+                                  w.u64.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B));
     const int bj = block_jacobi ? 1 : 0;
@@ -521,7 +519,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
     Workspace &w = m->ws;
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, 1, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
-                                  w.u64.p, w.u32.p, w.fc.p);
+                                  w.u64.p, w.fc.p);
     const int64_t snb = m->pat.sell_nb();
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
                                                  m->vcol.p, m->cptr.p, m->clist.p, m->iw.p, m->a2.p,

@@ -104,7 +104,6 @@ struct Workspace {
     int32_t cap = 0;        // systems
     int32_t nblk = 0;       // workgroups per system for row kernels
     DevArray<double> u64, fc;          // [B][M+1][6] per-triangle u = grad_M I . e, f terms
-    DevArray<float> u32;               // [B][M+1][6] fp32 copy of u
     DevArray<float> A32;               // [B][sell_nb][4] A_b in fp32 (MOF_PREC_MIXED)
     DevArray<double> A64;              // [B][sell_nb][4] A_b in fp64 (MOF_PREC_F64), lazily
     DevArray<double> dinv64;           // [B][N][4] 2x2 block-Jacobi inverses
@@ -222,9 +221,15 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s);  // Galerkin + coar
 // into the part_rzrr slot `part_slot`
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_slot, int32_t nblk,
                 hipStream_t s);
+// level-0 smoother data the PCG update / init write the pre-smoothing with
+struct AmgFine {
+    const void *D0h;  // bf16 2x2 D^-1 [B][N] (uint2 each)
+    float *x0;        // smoother x
+    float omega;
+};
+AmgFine amg_fine(mof_mesh *m);
 void amg_destroy(AmgDevice *g);
-float *amg_level0_x(mof_mesh *m);  // level-0 smoother vector (pre-smoothed x0)
-float amg_omega(const mof_mesh *m);
+
 int32_t amg_levels(const mof_mesh *m);
 
 double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,

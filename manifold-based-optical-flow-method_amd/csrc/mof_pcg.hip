@@ -64,6 +64,7 @@ struct PcgArgs {
     int32_t ext;           // z and r.z come from an external preconditioner (AMG)
     V *x0;                 // ext: pre-smoothed x0 = omega D^-1 r for the V-cycle
     V omega;
+    const uint2 *dh;       // ext (multigrid, fp32): the smoother's 2x2 D^-1, 4 bf16 [B][N]
 };
 
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
@@ -155,13 +156,15 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
         const V r0 = (V)f.x, r1 = (V)f.y;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = V2{r0, r1};
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = V2{(V)0, (V)0};
-        const V *d = a.dinv + 4 * vi;
-        const V z0 = d[0] * r0 + d[1] * r1, z1 = d[2] * r0 + d[3] * r1;
         if (!a.ext) {
+            const V *d = a.dinv + 4 * vi;
+            const V z0 = d[0] * r0 + d[1] * r1, z1 = d[2] * r0 + d[3] * r1;
             *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
             rz += (double)r0 * z0 + (double)r1 * z1;
-        } else {
-            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * z0, a.omega * z1};
+        } else if constexpr (sizeof(V) == 4) {
+            // the smoother's D^-1 (bf16), as in every later sweep
+            const float2 d = bf16_mat2(a.dh[vi], r0, r1);
+            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * d.x, a.omega * d.y};
         }
         rr += (double)r0 * r0 + (double)r1 * r1;
     }
@@ -285,14 +288,16 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
         ri.y -= alpha * qi.y;
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
-        V d[4];
-        ld_blk(a.dinv, vi, d);
-        const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
         if (!a.ext) {
+            V d[4];
+            ld_blk(a.dinv, vi, d);
+            const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
             *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
             rz += (double)ri.x * z0 + (double)ri.y * z1;
-        } else {
-            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * z0, a.omega * z1};
+        } else if constexpr (sizeof(V) == 4) {
+            // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
+            const float2 d = bf16_mat2(a.dh[vi], ri.x, ri.y);
+            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * d.x, a.omega * d.y};
         }
         rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
     }
@@ -451,6 +456,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.ext = 0;
     a.x0 = nullptr;
     a.omega = (V)0;
+    a.dh = nullptr;
     return a;
 }
 
@@ -471,15 +477,16 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     a.ext = amg ? 1 : 0;
     if constexpr (sizeof(V) == 4) {
         if (amg) {
-            a.x0 = amg_level0_x(m);
-            a.omega = amg_omega(m);
+            AmgFine f = amg_fine(m);
+            a.x0 = f.x0;
+            a.omega = f.omega;
+            a.dh = static_cast<const uint2 *>(f.D0h);
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
     // z = M^-1 r for the external preconditioner, r.z into slot `slot`
     auto precond = [&](int32_t slot) {
-        if constexpr (sizeof(V) == 4)
-            amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, s);
+        if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, s);
     };
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B));
@@ -599,10 +606,8 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.nblk = (int32_t)((N + kRowsPerWG - 1) / kRowsPerWG);
     // triangle slot M of u / fc stays zero: the padding of the incidence lists
     w.u64.alloc(6 * (M + 1) * B);
-    w.u32.alloc(6 * (M + 1) * B);
     w.fc.alloc(6 * (M + 1) * B);
     w.u64.zero(m->stream);
-    w.u32.zero(m->stream);
     w.fc.zero(m->stream);
     w.dinv64.alloc(4 * N * B);
     w.dinv32.alloc(4 * N * B);

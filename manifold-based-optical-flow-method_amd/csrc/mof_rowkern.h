@@ -160,5 +160,66 @@ inline unsigned xcd_grid(int32_t nblk, int32_t B) {
     return (unsigned)(8 * B * ((nblk + 7) / 8));
 }
 
+
+// bf16 copies of the level-0 operator for the multigrid smoother sweeps (the
+// preconditioner only needs an SPD approximation of A; rounding the blocks
+// (i,j) and (j,i)^T alike keeps it symmetric) -- half the bytes of A32.
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;  // round to nearest even
+}
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+__device__ __forceinline__ uint2 bf16x4(float a, float b, float c, float d) {
+    return make_uint2(bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16));
+}
+
+struct MatH {
+    int64_t sell_nb;
+    const int32_t *sell_off, *sell_col;
+    const uint2 *A;  // [B][sell_nb] 4 bf16 per block
+};
+
+// spmv_row on the bf16 blocks; the operand of column j comes from
+// xload(j) (a plain gather, or a value formed on the fly)
+template <int U = 8, typename XL>
+__device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
+                                            float &y1) {
+    const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = mt.sell_off[s];
+    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    float a0 = 0.f, a1 = 0.f;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U];
+        uint2 blk[U];
+        float2 xj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+        for (int u = 0; u < U; ++u) blk[u] = A[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xj[u] = xload(j[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool on = t0 + u < w;
+            a0 += on ? bf16_lo(blk[u].x) * xj[u].x + bf16_hi(blk[u].x) * xj[u].y : 0.f;
+            a1 += on ? bf16_lo(blk[u].y) * xj[u].x + bf16_hi(blk[u].y) * xj[u].y : 0.f;
+        }
+    }
+    y0 = a0;
+    y1 = a1;
+}
+
+__device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i, const float *__restrict__ x,
+                                           float &y0, float &y1) {
+    spmv_row_hx(mt, b, i, [x](int32_t j) { return reinterpret_cast<const float2 *>(x)[j]; }, y0, y1);
+}
+
+// 2x2 block stored as 4 bf16: y = D v
+__device__ __forceinline__ float2 bf16_mat2(uint2 d, float v0, float v1) {
+    return make_float2(bf16_lo(d.x) * v0 + bf16_hi(d.x) * v1, bf16_lo(d.y) * v0 + bf16_hi(d.y) * v1);
+}
+
 }  // namespace
 }  // namespace mof
