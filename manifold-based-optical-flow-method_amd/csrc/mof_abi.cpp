@@ -374,7 +374,16 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         const int32_t K = k1 - k0;
         mof_stats st{};
         if (K > 0) {
-            const int32_t Bmax = o.batch > 0 ? o.batch : 16;
+            int32_t Bmax = o.batch;
+            if (Bmax <= 0) {
+                // auto: 64 timesteps per launch sequence, fewer when a quarter
+                // of the free device memory cannot hold their workspace
+                // (~700 B per vertex and system with the multigrid levels)
+                size_t free_b = 0, total_b = 0;
+                MOF_HIP(hipMemGetInfo(&free_b, &total_b));
+                const double per_sys = 700.0 * (double)m->N + 1.0;
+                Bmax = (int32_t)std::max(1.0, std::min(64.0, 0.25 * (double)free_b / per_sys));
+            }
             const int32_t B = std::min(K, Bmax);
             mof::ensure_workspace(m, B, sp.precision);
             mof::Workspace &w = m->ws;
