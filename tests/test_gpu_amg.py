@@ -117,3 +117,33 @@ def test_amg_160k_agrees_with_jacobi():
     assert np.abs(Va - Vj).max() < VTOL
     assert np.array_equal(Va, Va2)
     assert sa["iterations"] < sj["iterations"]
+
+
+def test_amg_singular_system_is_nan():
+    """An unreferenced vertex makes A singular (zero diagonal block): the
+    multigrid path must report the system failed with a NaN V, not hang or
+    return garbage (spsolve's MatrixRankWarning behaviour)."""
+    g = load_golden("G1_ico642")
+    coords = np.vstack([g["coordinates"], [[0.0, 0.0, 20.0]]])
+    normals = np.vstack([g["normals"], [[0.0, 0.0, 1.0]]])
+    m = DeviceMesh(coords, normals, g["triangles"], g["areas"])
+    I = np.hstack([g["I"][:3], np.zeros((3, 1))])
+    V, st = m.solve_range(I, np.arange(3.0), 0, 2, 0.01, precision="mixed", precond="amg")
+    assert st["failed"] == 2
+    assert np.isnan(V).all()
+
+
+def test_amg_unordered_mesh_and_repeat():
+    """MOF_NO_REORDER (caller order inside: other aggregates, other iteration
+    path) agrees with the default order to the solve tolerance; a second solve
+    on the same handle (hierarchy reused) is bit-identical."""
+    g = load_golden("G1_ico642")
+    I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    m0 = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"], reorder=False)
+    m1 = mesh_of(g)
+    V0, s0 = m0.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg")
+    V1, _ = m1.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg")
+    V1b, _ = m1.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg")
+    assert s0["failed"] == 0
+    assert np.array_equal(V1, V1b)
+    assert np.abs(V0 - V1).max() < VTOL
