@@ -108,6 +108,11 @@ def main():
     args = parse()
     from mofhip.dist import max_over_ranks, rank_env, rank_k_range, sum_over_ranks
     rank, world, local = rank_env()
+    # MOF_BENCH_REHEARSE=1: every rank on GPU 0 over gloo -- exercises the
+    # N-rank path on a 1-GPU box (RCCL refuses two ranks on one GPU)
+    rehearse = os.environ.get("MOF_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     precision = args.precision or ("f64" if args.config == "C2" else "mixed")
 
     import torch
@@ -115,7 +120,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
     from mofhip import DeviceMesh, synth
 
@@ -165,8 +173,9 @@ def main():
         agg["max_rel_residual"] = max(agg["max_rel_residual"], st["max_rel_residual"])
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dist, dev)
-    agg["failed"] = int(sum_over_ranks(agg["failed"], dist, dev))
+    cdev = torch.device("cpu") if rehearse else dev
+    elapsed = max_over_ranks(elapsed, dist, cdev)
+    agg["failed"] = int(sum_over_ranks(agg["failed"], dist, cdev))
     n_ts = world * args.steps * B
     value = n_ts / elapsed
 
