@@ -48,10 +48,12 @@ except Exception:  # pragma: no cover
         pass
 
 # Solver options used by worker / compute_velocity_field. Override with
-# set_solver_options(); MOF_PRECISION=mixed selects fp32-inner PCG (with the
-# multigrid preconditioner unless MOF_PRECOND=jacobi).
+# set_solver_options() or the environment. Default: fp32 inner PCG with the
+# multigrid preconditioner and fp64 iterative refinement to
+# ||f - A V|| <= 1e-8 ||f|| in fp64 (MOF_PRECISION=f64: fp64 PCG with block
+# Jacobi; MOF_PRECOND=jacobi: block Jacobi in the inner solve).
 SOLVER_OPTIONS = {
-    "precision": os.environ.get("MOF_PRECISION", "f64"),
+    "precision": os.environ.get("MOF_PRECISION", "mixed"),
     "precond": os.environ.get("MOF_PRECOND", ""),
     "rtol": 1e-8,
     "batch": 0,
