@@ -16,7 +16,8 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
 CSRC_DIR = os.path.join(ROOT_DIR, "csrc")
-LIB_PATH = os.path.join(PKG_DIR, "libmofhip.so")
+# MOFHIP_LIB: another in-tree build of the same library (A/B measurements)
+LIB_PATH = os.environ.get("MOFHIP_LIB") or os.path.join(PKG_DIR, "libmofhip.so")
 
 MOF_OK = 0
 MOF_E_ARG = -1
