@@ -176,7 +176,8 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
                                                   const double *__restrict__ I0,
                                                   const double *__restrict__ I1, int64_t ldI,
                                                   const double *__restrict__ dt,
-                                                  double *__restrict__ u, double *__restrict__ fc) {
+                                                  double *__restrict__ u, double *__restrict__ fc,
+                                                  float *__restrict__ u32) {
     // one triangle per thread for all B systems: the geometry is read once
     const int32_t T = blockIdx.x * kWG + threadIdx.x;
     if (T >= M) return;
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
         for (int q = 0; q < 6; q += 2) {
             *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
             *reinterpret_cast<double2 *>(fc + base + q) = make_double2(fo[q], fo[q + 1]);
+            if (u32) *reinterpret_cast<float2 *>(u32 + base + q) = make_float2((float)uo[q], (float)uo[q + 1]);
         }
     }
 }
@@ -325,6 +327,85 @@ __global__ __launch_bounds__(kWG) void k_assemble_blocks(
 
 // lambda * a2 for the solve operator (fp64 copy bit-identical to the
 // reference's lambda_ * a2, :144) and its fp32 rounding.
+// Mixed-precision solve path: A32 = a1 + lambda a2 folded in fp32 from the
+// fp32 copy of u (half the gathered bytes of the fp64 fold; the inner PCG
+// runs on fp32 A anyway and the fp64 refinement uses the exact operator).
+// The diagonal slot still folds f in fp64 from the f terms (bit-identical
+// to the reference's f) and writes the fp32 2x2 block-Jacobi inverse.
+__global__ __launch_bounds__(kWG) void k_assemble_mixed(
+    int64_t sell_nb, int32_t N, int32_t M, int32_t B, const int32_t *__restrict__ sell_blk,
+    const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
+    const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
+    const float *__restrict__ w12, const float *__restrict__ a2s, const float *__restrict__ u,
+    const double *__restrict__ fc, int block_jacobi, float *__restrict__ A,
+    float *__restrict__ dinv32, double *__restrict__ rhs) {
+    int32_t tile, b;
+    if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
+    if (pos >= sell_nb) return;
+    const int32_t p = sell_blk[pos];
+    if (p < 0) return;
+    const int32_t i = blk_row[p];
+    const bool diag = (vcol[p] == i);
+    const float *ub = u + 6 * (int64_t)b * (M + 1);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int32_t c0 = cptr[p], c1 = cptr[p + 1];
+    constexpr int U = 4;
+    for (int32_t c = c0; c < c1; c += U) {
+        int32_t T[U], a[U], bb[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int32_t code = clist[min(c + q, c1 - 1)];
+            T[q] = code / 9;
+            a[q] = (code % 9) / 3;
+            bb[q] = code % 3;
+        }
+        float2 ua[U], uv[U];
+        float wq[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            ua[q] = *reinterpret_cast<const float2 *>(ub + 6 * (int64_t)T[q] + 2 * a[q]);
+            uv[q] = *reinterpret_cast<const float2 *>(ub + 6 * (int64_t)T[q] + 2 * bb[q]);
+            wq[q] = w12[T[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const float integ = (c + q < c1) ? (diag ? 2.f * wq[q] : wq[q]) : 0.f;
+            acc[0] += ua[q].x * uv[q].x * integ;
+            acc[1] += ua[q].x * uv[q].y * integ;
+            acc[2] += ua[q].y * uv[q].x * integ;
+            acc[3] += ua[q].y * uv[q].y * integ;
+        }
+    }
+    const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
+    const float Av[4] = {acc[0] + s4.x, acc[1] + s4.y, acc[2] + s4.z, acc[3] + s4.w};
+    reinterpret_cast<float4 *>(A)[(int64_t)b * sell_nb + pos] = make_float4(Av[0], Av[1], Av[2], Av[3]);
+    if (!diag) return;
+    // f_i in fp64, in the reference's triangle order
+    const double *fb = fc + 6 * (int64_t)b * (M + 1);
+    double f0 = 0.0, f1 = 0.0;
+    for (int32_t c = c0; c < c1; ++c) {
+        const int32_t code = clist[c];
+        const int32_t a = (code % 9) / 3;
+        if (a != code % 3) continue;
+        const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)(code / 9) + 2 * a);
+        f0 += fv.x;
+        f1 += fv.y;
+    }
+    double inv[4];
+    const double d0 = Av[0], d1 = Av[1], d2 = Av[2], d3 = Av[3];
+    if (block_jacobi) {
+        const double det = d0 * d3 - d1 * d2;
+        inv[0] = d3 / det; inv[1] = -d1 / det; inv[2] = -d2 / det; inv[3] = d0 / det;
+    } else {
+        inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
+    }
+    const int64_t vi = (int64_t)b * N + i;
+    reinterpret_cast<float4 *>(dinv32)[vi] =
+        make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+    *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
+}
+
 __global__ __launch_bounds__(kWG) void k_scale_a2(int64_t n, double lambda,
                                                   const double *__restrict__ a2,
                                                   double *__restrict__ s64,
@@ -497,15 +578,14 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
                 "assembly target A not allocated");
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
-                                  w.u64.p, w.fc.p);
+                                  w.u64.p, w.fc.p, precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B));
     const int bj = block_jacobi ? 1 : 0;
     if (precision == MOF_PREC_MIXED)
-        k_assemble_blocks<float><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
-                                                    m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
-                                                    m->a2s64.p, w.u64.p, w.fc.p, bj, w.A32.p,
-                                                    w.dinv64.p, w.dinv32.p, w.rhs.p);
+        k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
+                                            m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,
+                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p);
     else
         k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
@@ -519,7 +599,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
     Workspace &w = m->ws;
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, 1, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
-                                  w.u64.p, w.fc.p);
+                                  w.u64.p, w.fc.p, nullptr);
     const int64_t snb = m->pat.sell_nb();
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
                                                  m->vcol.p, m->cptr.p, m->clist.p, m->iw.p, m->a2.p,

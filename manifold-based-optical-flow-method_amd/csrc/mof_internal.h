@@ -104,6 +104,7 @@ struct Workspace {
     int32_t cap = 0;        // systems
     int32_t nblk = 0;       // workgroups per system for row kernels
     DevArray<double> u64, fc;          // [B][M+1][6] per-triangle u = grad_M I . e, f terms
+    DevArray<float> u32;               // [B][M+1][6] fp32 u (mixed-precision assembly)
     DevArray<float> A32;               // [B][sell_nb][4] A_b in fp32 (MOF_PREC_MIXED)
     DevArray<double> A64;              // [B][sell_nb][4] A_b in fp64 (MOF_PREC_F64), lazily
     DevArray<double> dinv64;           // [B][N][4] 2x2 block-Jacobi inverses

@@ -606,8 +606,10 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.nblk = (int32_t)((N + kRowsPerWG - 1) / kRowsPerWG);
     // triangle slot M of u / fc stays zero: the padding of the incidence lists
     w.u64.alloc(6 * (M + 1) * B);
+    w.u32.alloc(6 * (M + 1) * B);
     w.fc.alloc(6 * (M + 1) * B);
     w.u64.zero(m->stream);
+    w.u32.zero(m->stream);
     w.fc.zero(m->stream);
     w.dinv64.alloc(4 * N * B);
     w.dinv32.alloc(4 * N * B);
