@@ -493,25 +493,47 @@ __global__ __launch_bounds__(kWG) void k_to_planar(int32_t N, const double *__re
 // S3's epilogue (find_singularity_point.py:28-69, S3…py:130-132): the 3-D
 // tangent vector V^0 e^0 + V^1 e^1 of every vertex and its length, with
 // numpy's roundings (products, then sums; |v| = sqrt((x^2 + y^2) + z^2)).
-__global__ __launch_bounds__(kWG) void k_velocity_vectors(int32_t N, int64_t total,
-                                                          const double *__restrict__ e,
+constexpr int kVVFields = 4;  // fields per thread: e_i loaded once for all of them
+
+__global__ __launch_bounds__(kWG) void k_velocity_vectors(int32_t N, int32_t K, const double *__restrict__ e,
                                                           const double *__restrict__ V,
                                                           double *__restrict__ Vc,
                                                           double *__restrict__ speed) {
-    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
-    if (q >= total) return;
-    const int64_t k = q / N;
-    const int32_t i = (int32_t)(q - k * N);
-    const double v0 = V[2 * k * N + i], v1 = V[2 * k * N + N + i];
-    const double *ei = e + 6 * (int64_t)i;
-    double c[3];
+    // vertex i of fields kVVFields*blockIdx.y + f; the (N,3) output of the
+    // workgroup's 256 vertices is staged in LDS and stored as 16-B chunks
+    __shared__ double st[3 * kWG];
+    const int32_t i0 = blockIdx.x * kWG;
+    const int32_t i = i0 + threadIdx.x;
+    double ei[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (i < N) {
 #pragma unroll
-    for (int d = 0; d < 3; ++d) c[d] = v0 * ei[d] + v1 * ei[3 + d];
-    if (Vc) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) Vc[3 * q + d] = c[d];
+        for (int d = 0; d < 6; ++d) ei[d] = e[6 * (int64_t)i + d];
     }
-    if (speed) speed[q] = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const int32_t nv = min(kWG, N - i0);
+    for (int f = 0; f < kVVFields; ++f) {
+        const int64_t k = (int64_t)blockIdx.y * kVVFields + f;
+        if (k >= K) break;
+        double c[3] = {0.0, 0.0, 0.0};
+        if (i < N) {
+            const double v0 = V[2 * k * N + i], v1 = V[2 * k * N + N + i];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) c[d] = v0 * ei[d] + v1 * ei[3 + d];
+            if (speed) speed[k * N + i] = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+        }
+        if (!Vc) continue;
+        __syncthreads();  // st reuse across fields
+#pragma unroll
+        for (int d = 0; d < 3; ++d) st[3 * threadIdx.x + d] = c[d];
+        __syncthreads();
+        double *out = Vc + 3 * (k * N + i0);
+        if (((3 * (k * N + i0)) & 1) == 0) {  // 16-B aligned
+            for (int32_t q = threadIdx.x; 2 * q + 1 < 3 * nv; q += kWG)
+                reinterpret_cast<double2 *>(out)[q] = make_double2(st[2 * q], st[2 * q + 1]);
+            if (((3 * nv) & 1) && threadIdx.x == 0) out[3 * nv - 1] = st[3 * nv - 1];
+        } else {
+            for (int32_t q = threadIdx.x; q < 3 * nv; q += kWG) out[q] = st[q];
+        }
+    }
 }
 
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
@@ -611,7 +633,13 @@ void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double
                              double *speed, hipStream_t s) {
     const int64_t total = (int64_t)N * K;
     if (total == 0) return;
-    k_velocity_vectors<<<grid1(total), kWG, 0, s>>>(N, total, e, V, Vc, speed);
+    const int64_t step = 65535LL * kVVFields;  // grid.y limit
+    for (int64_t k0 = 0; k0 < K; k0 += step) {
+        const int32_t kn = (int32_t)std::min<int64_t>(step, K - k0);
+        k_velocity_vectors<<<dim3((unsigned)((N + kWG - 1) / kWG), (unsigned)((kn + kVVFields - 1) / kVVFields)),
+                             kWG, 0, s>>>(N, kn, e, V + 2 * k0 * N, Vc ? Vc + 3 * k0 * N : nullptr,
+                                          speed ? speed + k0 * N : nullptr);
+    }
     MOF_HIP(hipGetLastError());
 }
 
