@@ -2,7 +2,8 @@
 //
 // Host orchestration only: argument checks, device uploads, batching of
 // timesteps, and result copies. All arithmetic runs in the HIP kernels of
-// mof_assemble.hip / mof_pcg.hip.
+// mof_assemble.hip / mof_pcg.hip / mof_amg.hip / mof_sing.hip (the CSV and
+// PLY entry points are host code: mof_io.cpp, mof_ply.cpp).
 #include <algorithm>
 #include <chrono>
 #include <cmath>

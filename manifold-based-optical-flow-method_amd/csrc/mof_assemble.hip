@@ -235,10 +235,10 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
     }
 }
 
-// Solve-path A_b = a1_b + lambda a2 of B systems, one SELL position per
-// thread (coalesced stores): the a1 block is folded in fp64 over its terms in
-// triangle order exactly as the export path does, then stored in the inner
-// solver's precision (fp32 for MOF_PREC_MIXED, fp64 otherwise). The thread
+// Solve-path A_b = a1_b + lambda a2 of B systems (fp64 PCG), one SELL
+// position per thread (coalesced stores): the a1 block is folded in fp64 over
+// its terms in triangle order exactly as the export path does (the mixed
+// path uses k_assemble_mixed below). The thread
 // holding a diagonal block also folds f_i (bit-identical to the reference's
 // f) and writes the 2x2 block-Jacobi inverse of vertex i. Terms are fetched
 // four at a time (indices, then u pairs) so the fold is not one memory round

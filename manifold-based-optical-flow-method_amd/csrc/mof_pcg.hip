@@ -1,12 +1,14 @@
-// mof_pcg.hip -- batched block-Jacobi preconditioned CG on gfx950.
+// mof_pcg.hip -- batched preconditioned CG on gfx950 (2x2 block Jacobi, or
+// the aggregation-multigrid V-cycle of mof_amg.hip).
 //
 // Replaces scipy.sparse.linalg.spsolve (compute_optical_flow.py:147) for B
 // timesteps at once: every launch covers all B systems, so the per-iteration
 // launch cost is shared. A_b is materialised per system in SELL-64 2x2 blocks
 // (16 B per block in fp32, read with one dwordx4 per lane, 1 KiB per
 // wave-instruction). The SpMV grid is XCD-aware: each XCD owns one
-// contiguous eighth of the vertex rows of every system, so the z gathers of
-// a row block hit rows that the same XCD's L2 already holds.
+// contiguous eighth of the vertex rows of every system and walks it row
+// block by row block, the B systems of a row block back to back, so the
+// row block's column indices are read once per XCD (mof_rowkern.h).
 //
 // The fp64 residual of the refinement (k_residual) applies A without the
 // materialised blocks: lambda a2 (shared SELL blocks) plus a1 per incident
@@ -15,11 +17,13 @@
 // compute_optical_flow.py:127-141):
 //   (a1 x)_i = sum_{T ni i} u_{T,i} (A_T/12) (2 s_i + s_j + s_k),  s_v = u_{T,v} . x_v
 //
-// One CG iteration = two launches:
+// One CG iteration = two launches (+ the V-cycle with MOF_PRECOND_AMG):
 //   k_pcg_spmv    w = A z ; q = w + beta q ; p = z + beta p ; partial p.q
 //                 (q = A p without a separate p update: A(z + beta p) =
 //                  A z + beta A p)
 //   k_pcg_update  x += alpha p ; r -= alpha q ; z = D^-1 r ; partial r.z, r.r
+//                 (multigrid: x0 = omega D^-1 r, the V-cycle's pre-smoothing,
+//                  and partial r.r; the V-cycle's last kernel writes z, r.z)
 // Scalars (alpha, beta, |r|) are never sent to the host: every workgroup
 // re-reduces the per-workgroup partials of the previous launch in one fixed
 // order, so all workgroups (and every run, on any GPU count) agree bit for
@@ -27,8 +31,9 @@
 // few iterations.
 //
 // MOF_PREC_MIXED: the inner CG runs on fp32 A and fp32 vectors (dot products
-// in fp64) for the correction d of A d = r64, and an fp64 SpMV refreshes
-// r64 = f - A64 x64 between inner solves (iterative refinement).
+// in fp64) for the correction d of A d = r64, and the fp64 matrix-free
+// residual refreshes r64 = f - A x64 between inner solves (iterative
+// refinement).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
