@@ -54,7 +54,8 @@ struct AmgDevLevel {
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap
     DevArray<float> A, Dinv;     // [B][sell_nb][12], [B][n][12] (level >= 1)
-    DevArray<uint32_t> Ah;       // [B][sell_nb][6] bf16 A for the sweeps (not the coarsest)
+    DevArray<uint32_t> Ah;       // [B][sell_nb][4] bf16 A entries 0..7 for the sweeps (not the coarsest)
+    DevArray<uint16_t> Ah22;     // [B][sell_nb] bf16 entry (2,2)
     DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x, r [B][n][2]
                                  // r is stored in member order of the next level
 };

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, float *__restrict__ Dc,
-    uint2 *__restrict__ Ah) {
+    uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
     // XCD-aware tiles: the B systems of a tile share its gather lists and Q
     int32_t tile, b;
     if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b)) return;
@@ -199,11 +199,13 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
         st3(Dc, (int64_t)b * nC + I, D);
     }
     st3(Ac, (int64_t)b * c_sell_nb + pos, C);
-    if (Ah) {
-        uint2 *p = Ah + 3 * ((int64_t)b * c_sell_nb + pos);
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-            p[r] = make_uint2(bf16_bits(C[r][0]) | (bf16_bits(C[r][1]) << 16), bf16_bits(C[r][2]));
+    if (Ah) {  // bf16 sweep copy: 8 entries in 16 B + a22 in 2 B
+        const int64_t q = (int64_t)b * c_sell_nb + pos;
+        Ah[q] = make_uint4(bf16_bits(C[0][0]) | (bf16_bits(C[0][1]) << 16),
+                           bf16_bits(C[0][2]) | (bf16_bits(C[1][0]) << 16),
+                           bf16_bits(C[1][1]) | (bf16_bits(C[1][2]) << 16),
+                           bf16_bits(C[2][0]) | (bf16_bits(C[2][1]) << 16));
+        Ah22[q] = (uint16_t)bf16_bits(C[2][2]);
     }
 }
 
@@ -295,7 +297,8 @@ struct Lvl {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;  // level >= 1
     const float *A, *Dinv;               // level >= 1: [B][sell_nb][12], [B][n][12]
-    const uint2 *Ah;                     // bf16 A for the sweeps ([B][sell_nb][3]), or null
+    const uint4 *Ah;                     // bf16 A for the sweeps: [B][sell_nb] entries 0..7, or null
+    const uint16_t *Ah22;                // [B][sell_nb] entry (2,2)
     float *b, *x, *r, *y;                // [B][n][4] (level 0: x, r [B][n][2])
     const int32_t *agg, *mptr, *apos;    // transition to level + 1
     const float *Q, *Qm;
@@ -327,7 +330,8 @@ __device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, co
                                           float (&acc)[3]) {
     constexpr int U = 4;
     const float *Ab = L.A + (int64_t)b * L.sell_nb * kB3;
-    const uint2 *Hb = L.Ah + (int64_t)b * L.sell_nb * 3;
+    const uint4 *Hb = L.Ah + (int64_t)b * L.sell_nb;
+    const uint16_t *H22 = L.Ah22 + (int64_t)b * L.sell_nb;
     const bool half = L.Ah != nullptr;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = L.sell_off[s], w = (L.sell_off[s + 1] - o) >> 6;
@@ -340,14 +344,17 @@ __device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, co
         if (half) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint2 *p = Hb + 3 * ((int64_t)o + min(t0 + u, w - 1) * kSlice + l);
-#pragma unroll
-                for (int r = 0; r < 3; ++r) {
-                    const uint2 h = p[r];
-                    a[u][r][0] = bf16_lo(h.x);
-                    a[u][r][1] = bf16_hi(h.x);
-                    a[u][r][2] = bf16_lo(h.y);
-                }
+                const int64_t q = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
+                const uint4 h = Hb[q];
+                a[u][0][0] = bf16_lo(h.x);
+                a[u][0][1] = bf16_hi(h.x);
+                a[u][0][2] = bf16_lo(h.y);
+                a[u][1][0] = bf16_hi(h.y);
+                a[u][1][1] = bf16_lo(h.z);
+                a[u][1][2] = bf16_hi(h.z);
+                a[u][2][0] = bf16_lo(h.w);
+                a[u][2][1] = bf16_hi(h.w);
+                a[u][2][2] = bf16_lo((uint32_t)H22[q]);
             }
         } else {
 #pragma unroll
@@ -721,8 +728,10 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
             if (l + 1 < G.lv.size()) {  // bf16 sweep copy (the coarsest stays fp32)
-                D.Ah.alloc((size_t)6 * D.sell_nb * B);
+                D.Ah.alloc((size_t)4 * D.sell_nb * B);
                 D.Ah.zero(s);
+                D.Ah22.alloc((size_t)D.sell_nb * B);
+                D.Ah22.zero(s);
             }
             D.Dinv.alloc((size_t)kB3 * n * B);
             D.b.alloc(4 * n * B);
@@ -745,7 +754,8 @@ AmgFine amg_fine(mof_mesh *m) {
     return f;
 }
 
-static uint2 *ah(AmgDevLevel &C) { return C.Ah.n > 1 ? reinterpret_cast<uint2 *>(C.Ah.p) : nullptr; }
+static uint4 *ah(AmgDevLevel &C) { return C.Ah.n > 1 ? reinterpret_cast<uint4 *>(C.Ah.p) : nullptr; }
+static uint16_t *ah22(AmgDevLevel &C) { return C.Ah22.n > 1 ? C.Ah22.p : nullptr; }
 
 void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     AmgDevice &G = *m->amg;
@@ -763,11 +773,11 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
             k_galerkin<2><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
                                                               m->pat.sell_nb(), C.A.p, C.Dinv.p,
-                                                              ah(C));
+                                                              ah(C), ah22(C));
         else
             k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
-                                                              F.sell_nb, C.A.p, C.Dinv.p, ah(C));
+                                                              F.sell_nb, C.A.p, C.Dinv.p, ah(C), ah22(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];
     k_coarse_inverse<<<dim3((unsigned)B), kInvWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
@@ -783,7 +793,8 @@ Lvl level_view(const AmgDevLevel &D) {
     v.sell_col = D.sell_col.p;
     v.A = D.A.p;
     v.Dinv = D.Dinv.p;
-    v.Ah = D.Ah.n > 1 ? reinterpret_cast<const uint2 *>(D.Ah.p) : nullptr;
+    v.Ah = D.Ah.n > 1 ? reinterpret_cast<const uint4 *>(D.Ah.p) : nullptr;
+    v.Ah22 = D.Ah22.n > 1 ? D.Ah22.p : nullptr;
     v.b = D.b.p;
     v.x = D.x.p;
     v.r = D.r.p;
