@@ -219,6 +219,15 @@ int mof_point_normals(const float *points, const int64_t *triangles, int64_t N, 
 int mof_cell_areas(const float *points, const int64_t *triangles, int64_t N, int64_t M,
                    double *areas);
 
+/* Diagnostic (host only, no device): the multigrid hierarchy the solver would
+ * build for this mesh in the caller's vertex order -- vertex adjacency, greedy
+ * aggregation, tentative prolongators from e (N,2,3) -- for tests of the host
+ * setup without a GPU. level_nodes[0..*n_levels) receives the node count of
+ * each level (at most 16 levels); qtq_err the largest |Q^T Q - I| entry over
+ * the level-0 aggregates (orthonormal prolongator columns). */
+int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
+                  int32_t *level_nodes, double *qtq_err);
+
 /* Measurement helper for bench.py: launches the PCG SpMV kernel `reps` times
  * back to back on `batch` systems of the last solve's working set, timed with
  * HIP events on the handle's stream. Returns the mean launch time and the

@@ -11,6 +11,7 @@
 #include <functional>
 #include <new>
 
+#include "mof_amg.h"
 #include "mof_internal.h"
 
 namespace {
@@ -525,6 +526,39 @@ int mof_singularities(int32_t device, const void *coords, const int32_t *triangl
             MOF_HIP(hipMemcpyAsync(lam_mu, dlm.p, 2 * mk * sizeof(double), hipMemcpyDeviceToHost, s));
         }
         MOF_HIP(hipStreamSynchronize(s));
+    });
+}
+
+int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
+                  int32_t *level_nodes, double *qtq_err) {
+    return guarded([&] {
+        MOF_REQUIRE(tri && e && n_levels && level_nodes && N > 0 && M > 0, "bad arguments");
+        for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+            MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
+        mof::Pattern pat;
+        mof::build_pattern(tri, N, M, pat);
+        mof::AmgHierarchy H;
+        mof::build_amg(pat, e, mof::AmgParams{}, H);
+        *n_levels = (int32_t)std::min<size_t>(16, H.levels.size());
+        for (int32_t l = 0; l < *n_levels; ++l) level_nodes[l] = H.levels[l].n;
+        if (qtq_err) {
+            double err = 0.0;
+            const mof::AmgLevel &F = H.levels[0];
+            for (size_t I = 0; I + 1 < F.mptr.size(); ++I)
+                for (int a = 0; a < 3; ++a)
+                    for (int c = 0; c < 3; ++c) {
+                        double sum = 0.0;
+                        for (int32_t q = F.mptr[I]; q < F.mptr[I + 1]; ++q) {
+                            const int32_t i = F.mlist[q];
+                            for (int r = 0; r < 2; ++r)
+                                sum += (double)F.Q[(size_t)i * 6 + 3 * r + a] * F.Q[(size_t)i * 6 + 3 * r + c];
+                        }
+                        const bool dead_col = H.levels.size() > 1 && H.levels[1].dead[3 * I + a];
+                        const double want = (a == c && !dead_col) ? 1.0 : 0.0;
+                        err = std::max(err, std::fabs(sum - want));
+                    }
+            *qtq_err = err;
+        }
     });
 }
 

@@ -44,7 +44,7 @@ EXPORTS = (
     "mof_mesh_destroy", "mof_mesh_get_info", "mof_geometry_export", "mof_csr_export",
     "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
     "mof_csv_write", "mof_csv_shape", "mof_csv_read", "mof_ply_info", "mof_ply_read",
-    "mof_point_normals", "mof_cell_areas", "mof_singularities",
+    "mof_point_normals", "mof_cell_areas", "mof_singularities", "mof_amg_probe",
 )
 
 
@@ -142,6 +142,7 @@ def lib():
             "mof_cell_areas": ([P, P, i64, i64, P], ctypes.c_int),
             "mof_singularities": ([i32, P, P, i32, i32, P, i32, f64, u32, P, P, P, P, P],
                                   ctypes.c_int),
+            "mof_amg_probe": ([P, P, i32, i32, P, P, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

@@ -1,0 +1,59 @@
+"""The multigrid's host setup (csrc/mof_amg_host.cpp) on the CPU, through
+the host-only diagnostic entry point mof_amg_probe (no device needed):
+coarsening ratios, coarsest size bound, orthonormal tentative prolongators,
+determinism, and the tiny-mesh case that keeps block Jacobi."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from mofhip import _lib as L
+from mofhip import synth
+
+
+def probe(p, t):
+    n = synth.vertex_normals(p, t)
+    a = synth.triangle_areas(p, t)
+    _, _, e, _ = oracle.geometry(p, n, t, a)
+    T = np.ascontiguousarray(t, dtype=np.int32)
+    E = np.ascontiguousarray(e, dtype=np.float64)
+    nl = ctypes.c_int32(0)
+    sizes = np.zeros(16, dtype=np.int32)
+    err = ctypes.c_double(0.0)
+    L.check(L.lib().mof_amg_probe(L.ptr(T), L.ptr(E), len(p), len(t), ctypes.byref(nl), L.ptr(sizes),
+                                  ctypes.byref(err)))
+    return list(sizes[:nl.value]), err.value
+
+
+@pytest.mark.parametrize("mesh", ["ico", "random", "cap"])
+def test_hierarchy_shape(mesh):
+    if mesh == "ico":
+        p, t = synth.icosphere(24, 10.0, jitter=0.005)
+    elif mesh == "random":
+        p, t = synth.random_sphere(4000, 10.0, seed=1)
+    else:
+        p, t = synth.spherical_cap(30, 10.0, 0.6)
+    sizes, err = probe(p, t)
+    assert sizes[0] == len(p)
+    assert len(sizes) >= 2
+    for a, b in zip(sizes, sizes[1:]):
+        assert b < a / 3  # aggregates of several vertices
+    assert 3 * sizes[-1] <= 128  # coarsest solved densely (<= 128 dofs)
+    assert err < 1e-5  # fp32 Q rows, orthonormal columns per aggregate
+
+
+def test_hierarchy_deterministic_and_tiny():
+    p, t = synth.icosphere(12, 10.0)
+    assert probe(p, t) == probe(p, t)
+    p1, t1 = synth.icosphere(1, 10.0)  # 12 vertices, 24 dofs: does not coarsen
+    sizes, _ = probe(p1, t1)
+    assert sizes == [len(p1)]
+
+
+def test_probe_rejects_bad_input():
+    p, t = synth.icosphere(2, 10.0)
+    bad = t.copy()
+    bad[0, 0] = len(p)
+    with pytest.raises(L.MofError):
+        probe(p, bad)

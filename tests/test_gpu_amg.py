@@ -52,7 +52,7 @@ def test_amg_fewer_iterations_and_deterministic():
 
 
 def test_amg_tiny_mesh_falls_back():
-    """A mesh that does not coarsen (42 vertices) keeps block Jacobi."""
+    """A mesh that does not coarsen (12 vertices) keeps block Jacobi."""
     p, t = synth.icosphere(1, 10.0)
     n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
     I = synth.travelling_wave(p, 3)
