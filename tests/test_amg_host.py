@@ -53,7 +53,10 @@ def test_hierarchy_deterministic_and_tiny():
 
 def test_probe_rejects_bad_input():
     p, t = synth.icosphere(2, 10.0)
-    bad = t.copy()
+    bad = np.ascontiguousarray(t, dtype=np.int32)
     bad[0, 0] = len(p)
+    E = np.zeros((len(p), 2, 3))
+    nl, sizes = ctypes.c_int32(0), np.zeros(16, dtype=np.int32)
+    rc = L.lib().mof_amg_probe(L.ptr(bad), L.ptr(E), len(p), len(t), ctypes.byref(nl), L.ptr(sizes), None)
     with pytest.raises(L.MofError):
-        probe(p, bad)
+        L.check(rc)
