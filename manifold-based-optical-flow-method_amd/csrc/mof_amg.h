@@ -53,7 +53,9 @@ struct AmgDevLevel {
     int32_t ngrp = 0;
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap
-    DevArray<float> A, Dinv;     // [B][sell_nb][12], [B][n][12] (level >= 1)
+    DevArray<float> A;           // [B][sell_nb][12] (level >= 1)
+    DevArray<uint32_t> Dh;       // [B][n][4] 3x3 D^-1 bf16 entries 0..7 (level >= 1)
+    DevArray<uint16_t> Dh22;     // [B][n] entry (2,2)
     DevArray<uint32_t> Ah;       // [B][sell_nb][4] bf16 A entries 0..7 for the sweeps (not the coarsest)
     DevArray<uint16_t> Ah22;     // [B][sell_nb] bf16 entry (2,2)
     DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x, r [B][n][2]

@@ -113,6 +113,12 @@ __device__ __forceinline__ void st3(float *A, int64_t idx, const float (&a)[3][3
     for (int r = 0; r < 3; ++r) p[r] = make_float4(a[r][0], a[r][1], a[r][2], 0.f);
 }
 
+__device__ __forceinline__ void st_h9(uint4 *H, uint16_t *H22, int64_t q, const float (&c)[3][3]) {
+    H[q] = make_uint4(bf16_bits(c[0][0]) | (bf16_bits(c[0][1]) << 16), bf16_bits(c[0][2]) | (bf16_bits(c[1][0]) << 16),
+                      bf16_bits(c[1][1]) | (bf16_bits(c[1][2]) << 16), bf16_bits(c[2][0]) | (bf16_bits(c[2][1]) << 16));
+    H22[q] = (uint16_t)bf16_bits(c[2][2]);
+}
+
 // ---- per-timestep setup --------------------------------------------------
 
 __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
@@ -130,8 +136,8 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
-    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, float *__restrict__ Dc,
-    uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
+    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
+    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
     // XCD-aware tiles: the B systems of a tile share its gather lists and Q
     int32_t tile, b;
     if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b)) return;
@@ -196,17 +202,10 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
             if (c_dead[3 * (int64_t)I + d]) C[d][d] += 1.f;
         float D[3][3];
         inv3(C, D);
-        st3(Dc, (int64_t)b * nC + I, D);
+        st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
     }
     st3(Ac, (int64_t)b * c_sell_nb + pos, C);
-    if (Ah) {  // bf16 sweep copy: 8 entries in 16 B + a22 in 2 B
-        const int64_t q = (int64_t)b * c_sell_nb + pos;
-        Ah[q] = make_uint4(bf16_bits(C[0][0]) | (bf16_bits(C[0][1]) << 16),
-                           bf16_bits(C[0][2]) | (bf16_bits(C[1][0]) << 16),
-                           bf16_bits(C[1][1]) | (bf16_bits(C[1][2]) << 16),
-                           bf16_bits(C[2][0]) | (bf16_bits(C[2][1]) << 16));
-        Ah22[q] = (uint16_t)bf16_bits(C[2][2]);
-    }
+    if (Ah) st_h9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, C);  // bf16 sweep copy
 }
 
 constexpr int kMaxCoarse = 128;
@@ -296,13 +295,33 @@ struct Lvl {
     int32_t n;
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;  // level >= 1
-    const float *A, *Dinv;               // level >= 1: [B][sell_nb][12], [B][n][12]
+    const float *A;                      // level >= 1: [B][sell_nb][12]
+    const uint4 *Dh;                     // level >= 1: 3x3 D^-1, bf16 entries 0..7 [B][n]
+    const uint16_t *Dh22;                // and entry (2,2)
     const uint4 *Ah;                     // bf16 A for the sweeps: [B][sell_nb] entries 0..7, or null
     const uint16_t *Ah22;                // [B][sell_nb] entry (2,2)
     float *b, *x, *r, *y;                // [B][n][4] (level 0: x, r [B][n][2])
     const int32_t *agg, *mptr, *apos;    // transition to level + 1
     const float *Q, *Qm;
 };
+
+// 3x3 bf16 block stored as 8 entries in 16 B + entry (2,2) in 2 B
+__device__ __forceinline__ void ld_h9(const uint4 *H, const uint16_t *H22, int64_t q, float (&a)[3][3]) {
+    const uint4 h = H[q];
+    a[0][0] = bf16_lo(h.x);
+    a[0][1] = bf16_hi(h.x);
+    a[0][2] = bf16_lo(h.y);
+    a[1][0] = bf16_hi(h.y);
+    a[1][1] = bf16_lo(h.z);
+    a[1][2] = bf16_hi(h.z);
+    a[2][0] = bf16_lo(h.w);
+    a[2][1] = bf16_hi(h.w);
+    a[2][2] = bf16_lo((uint32_t)H22[q]);
+}
+// the smoother's 3x3 D^-1 of node i of system b
+__device__ __forceinline__ void ld_dh(const Lvl &L, int32_t b, int32_t i, float (&d)[3][3]) {
+    ld_h9(L.Dh, L.Dh22, (int64_t)b * L.n + i, d);
+}
 
 // Level 0: r1 = r - A x0 (x0 = w D^-1 r from the PCG update), stored at the
 // member position of each vertex. PCG row layout, XCD-aware grid.
@@ -343,19 +362,7 @@ __device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, co
         for (int u = 0; u < U; ++u) j[u] = L.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
         if (half) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t q = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
-                const uint4 h = Hb[q];
-                a[u][0][0] = bf16_lo(h.x);
-                a[u][0][1] = bf16_hi(h.x);
-                a[u][0][2] = bf16_lo(h.y);
-                a[u][1][0] = bf16_hi(h.y);
-                a[u][1][1] = bf16_lo(h.z);
-                a[u][1][2] = bf16_hi(h.z);
-                a[u][2][0] = bf16_lo(h.w);
-                a[u][2][1] = bf16_hi(h.w);
-                a[u][2][2] = bf16_lo((uint32_t)H22[q]);
-            }
+            for (int u = 0; u < U; ++u) ld_h9(Hb, H22, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, a[u]);
         } else {
 #pragma unroll
             for (int u = 0; u < U; ++u) ldm<3>(Ab, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, a[u]);
@@ -415,7 +422,7 @@ __device__ __forceinline__ void restrict_node(const Lvl &F, const Lvl &C, int32_
     stv<3>(C.b + vo, I, acc);
     if (smooth) {
         float d[3][3], x[3];
-        ldm<3>(C.Dinv + (int64_t)b * C.n * kB3, I, d);
+        ld_dh(C, b, I, d);
         matvec<3>(d, acc, x);
 #pragma unroll
         for (int c = 0; c < 3; ++c) x[c] *= omega;
@@ -443,7 +450,7 @@ __device__ __forceinline__ void post3_node(const Lvl &L, int32_t b, int32_t i, f
     spmv_row3(L, b, i, L.x + vo, ax);
     ldv<3>(L.b + vo, i, res);
     ldv<3>(L.x + vo, i, xi);
-    ldm<3>(L.Dinv + (int64_t)b * L.n * kB3, i, d);
+    ld_dh(L, b, i, d);
 #pragma unroll
     for (int c = 0; c < 3; ++c) res[c] -= ax[c];
     matvec<3>(d, res, dr);
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
         stv<3>(C.b + vo, I, acc);
         if (smooth) {
             float d[3][3], x[3];
-            ldm<3>(C.Dinv + (int64_t)b * C.n * kB3, I, d);
+            ld_dh(C, b, I, d);
             matvec<3>(d, acc, x);
 #pragma unroll
             for (int c = 0; c < 3; ++c) x[c] *= omega;
@@ -733,7 +740,8 @@ void amg_ensure(mof_mesh *m, int32_t B) {
                 D.Ah22.alloc((size_t)D.sell_nb * B);
                 D.Ah22.zero(s);
             }
-            D.Dinv.alloc((size_t)kB3 * n * B);
+            D.Dh.alloc((size_t)4 * n * B);
+            D.Dh22.alloc((size_t)n * B);
             D.b.alloc(4 * n * B);
             D.x.alloc(4 * n * B);
             D.r.alloc(4 * n * B);
@@ -756,6 +764,7 @@ AmgFine amg_fine(mof_mesh *m) {
 
 static uint4 *ah(AmgDevLevel &C) { return C.Ah.n > 1 ? reinterpret_cast<uint4 *>(C.Ah.p) : nullptr; }
 static uint16_t *ah22(AmgDevLevel &C) { return C.Ah22.n > 1 ? C.Ah22.p : nullptr; }
+static uint4 *dh(AmgDevLevel &C) { return reinterpret_cast<uint4 *>(C.Dh.p); }
 
 void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     AmgDevice &G = *m->amg;
@@ -772,12 +781,12 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
         if (l == 0)
             k_galerkin<2><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
-                                                              m->pat.sell_nb(), C.A.p, C.Dinv.p,
+                                                              m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p,
                                                               ah(C), ah22(C));
         else
             k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
-                                                              F.sell_nb, C.A.p, C.Dinv.p, ah(C), ah22(C));
+                                                              F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];
     k_coarse_inverse<<<dim3((unsigned)B), kInvWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
@@ -792,7 +801,8 @@ Lvl level_view(const AmgDevLevel &D) {
     v.sell_off = D.sell_off.p;
     v.sell_col = D.sell_col.p;
     v.A = D.A.p;
-    v.Dinv = D.Dinv.p;
+    v.Dh = reinterpret_cast<const uint4 *>(D.Dh.p);
+    v.Dh22 = D.Dh22.p;
     v.Ah = D.Ah.n > 1 ? reinterpret_cast<const uint4 *>(D.Ah.p) : nullptr;
     v.Ah22 = D.Ah22.n > 1 ? D.Ah22.p : nullptr;
     v.b = D.b.p;
