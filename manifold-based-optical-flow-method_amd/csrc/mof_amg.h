@@ -58,7 +58,7 @@ struct AmgDevLevel {
     DevArray<uint16_t> Dh22;     // [B][n] entry (2,2)
     DevArray<uint32_t> Ah;       // [B][sell_nb][4] bf16 A entries 0..7 for the sweeps (not the coarsest)
     DevArray<uint16_t> Ah22;     // [B][sell_nb] bf16 entry (2,2)
-    DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x, r [B][n][2]
+    DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x [B][n][2], r bf16 pairs [B][n]
                                  // r is stored in member order of the next level
 };
 

@@ -51,6 +51,18 @@ __device__ __forceinline__ void ldv(const float *v, int64_t node, float (&x)[BS]
         x[0] = t.x; x[1] = t.y; x[2] = t.z;
     }
 }
+// the restricted residual of level BSF: level 0 keeps it as a bf16 pair
+// (4 B per vertex, written once by k_res0 and read once by the restriction)
+template <int BSF>
+__device__ __forceinline__ void ldr(const float *r, int64_t b, int64_t n, int64_t q, float (&x)[BSF]) {
+    if constexpr (BSF == 2) {
+        const uint32_t h = reinterpret_cast<const uint32_t *>(r)[b * n + q];
+        x[0] = bf16_lo(h);
+        x[1] = bf16_hi(h);
+    } else {
+        ldv<BSF>(r + b * n * 4, q, x);
+    }
+}
 template <int BS>
 __device__ __forceinline__ void stv(float *v, int64_t node, const float (&x)[BS]) {
     if constexpr (BS == 2)
@@ -300,7 +312,7 @@ struct Lvl {
     const uint16_t *Dh22;                // and entry (2,2)
     const uint4 *Ah;                     // bf16 A for the sweeps: [B][sell_nb] entries 0..7, or null
     const uint16_t *Ah22;                // [B][sell_nb] entry (2,2)
-    float *b, *x, *r, *y;                // [B][n][4] (level 0: x, r [B][n][2])
+    float *b, *x, *r, *y;                // [B][n][4] (level 0: x [B][n][2], r bf16 [B][n][2])
     const int32_t *agg, *mptr, *apos;    // transition to level + 1
     const float *Q, *Qm;
 };
@@ -339,7 +351,7 @@ __global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B
         float y0, y1;
         spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-        reinterpret_cast<float2 *>(r1)[vb + apos[i]] = make_float2(ri.x - y0, ri.y - y1);
+        reinterpret_cast<uint32_t *>(r1)[vb + apos[i]] = bf16_bits(ri.x - y0) | (bf16_bits(ri.y - y1) << 16);
     }
 }
 
@@ -396,13 +408,12 @@ template <int BSF>
 __device__ __forceinline__ void restrict_node(const Lvl &F, const Lvl &C, int32_t b, int32_t I, bool smooth,
                                               float omega) {
     constexpr int U = 4;
-    const float *rb = F.r + (int64_t)b * F.n * vstride<BSF>();
     float acc[3] = {0.f, 0.f, 0.f};
     const int32_t q0 = F.mptr[I], q1 = F.mptr[I + 1];
     for (int32_t t0 = q0; t0 < q1; t0 += U) {
         float ri[U][BSF], qm[U][BSF * 3];
 #pragma unroll
-        for (int u = 0; u < U; ++u) ldv<BSF>(rb, min(t0 + u, q1 - 1), ri[u]);
+        for (int u = 0; u < U; ++u) ldr<BSF>(F.r, b, F.n, min(t0 + u, q1 - 1), ri[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float *p = F.Qm + (int64_t)min(t0 + u, q1 - 1) * BSF * 3;
@@ -486,10 +497,9 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
         if (threadIdx.x == 0) restrict_node<BSF>(F, C, b, I0, smooth != 0, omega);
         return;
     }
-    const float *rb = F.r + (int64_t)b * F.n * vstride<BSF>();
     for (int32_t q = q0 + threadIdx.x; q < q1; q += kWG) {
         float ri[BSF];
-        ldv<BSF>(rb, q, ri);
+        ldr<BSF>(F.r, b, F.n, q, ri);
         const float *qm = F.Qm + (int64_t)q * BSF * 3;
         float c3[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -728,7 +738,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
         const size_t n = D.n;
         if (l == 0) {
             D.x.alloc(2 * n * B);
-            D.r.alloc(2 * n * B);
+            D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
             G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
             G.D0h.alloc(2 * n * B);
         } else {
