@@ -228,6 +228,68 @@ int mof_cell_areas(const float *points, const int64_t *triangles, int64_t N, int
 int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
                   int32_t *level_nodes, double *qtq_err);
 
+/* ---- one timestep's system decomposed over P
+ * vertex parts (stretch; timestep shards stay the throughput path) --------
+ * A part owns vertices (both unknowns of each); its local mesh is every
+ * triangle with an owned corner, in the caller's triangle order, so its rows
+ * of A and f are the reference's (compute_optical_flow.py:100-146) bit for
+ * bit. The PCG iterations run in lockstep: the SpMV operand's ghost rows are
+ * exchanged before every product, the CG scalars are reduced over all parts
+ * in one fixed order (every part takes the same decisions; V is deterministic
+ * for a given partition and within the solve tolerance of mof_solve_range).
+ * Preconditioner: 2x2 block Jacobi (MOF_PRECOND_AMG is rejected). */
+typedef struct mof_dd mof_dd;
+
+typedef struct mof_dd_info {
+    int32_t nparts;         /* P */
+    int32_t local_parts;    /* parts this handle drives (P in-process, 1 per rank) */
+    int32_t rank;           /* RCCL rank, -1 in-process */
+    int32_t max_neighbours; /* most neighbour parts of any part */
+    int32_t max_owned;      /* largest part (vertices) */
+    int32_t pad_;
+    int64_t ghost_rows;     /* ghost vertices summed over parts (halo volume) */
+    int64_t send_rows;      /* rows sent per exchange, summed over parts */
+    double ms_setup;        /* partition, plans and part meshes */
+} mof_dd_info;
+
+#define MOF_DD_ID_BYTES 128
+
+/* Recursive coordinate bisection of the vertices into nparts parts of
+ * floor/ceil(N/nparts) vertices (host): part (N). */
+int mof_partition_rcb(const double *xyz, int32_t N, int32_t nparts, int32_t *part);
+
+/* Host-only diagnostic of the halo plan of a partition: per part (nparts
+ * entries each) owned vertices, ghost vertices, neighbour parts, local
+ * triangles and rows sent per exchange. */
+int mof_dd_plan_info(const int32_t *tri, int32_t N, int32_t M, int32_t nparts, const int32_t *part,
+                     int32_t *n_own, int32_t *n_ghost, int32_t *n_nbr, int32_t *n_tri,
+                     int64_t *n_send);
+
+/* All nparts parts in this process on one device (in-process transport: halo
+ * by one gather kernel, shared partial sums). part (N) NULL: RCB. Arguments as
+ * mof_mesh_create (flags: MOF_GEOM_F32_POINTS). */
+int mof_dd_create(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
+                  int32_t N, int32_t M, int32_t nparts, const int32_t *part, int32_t device,
+                  uint32_t flags, mof_dd **out);
+
+/* RCCL transport, one process (rank) per GPU and one part per rank: rank 0
+ * makes the id, the caller broadcasts it (e.g. torch.distributed), every rank
+ * calls mof_dd_create_rank with the same mesh and partition. Halo by
+ * ncclSend/ncclRecv with the neighbour ranks, partial sums by ncclAllGather
+ * (librccl is loaded at run time; $MOF_RCCL_LIB overrides its path). */
+int mof_dd_unique_id(uint8_t *id /* MOF_DD_ID_BYTES */);
+int mof_dd_create_rank(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
+                       int32_t N, int32_t M, int32_t nranks, const int32_t *part, int32_t rank,
+                       const uint8_t *id, int32_t device, uint32_t flags, mof_dd **out);
+int mof_dd_destroy(mof_dd *dd);
+int mof_dd_get_info(const mof_dd *dd, mof_dd_info *info);
+
+/* mof_solve_range on the decomposed system (same arguments and results; with
+ * RCCL every rank passes the same k-range and receives the whole V). */
+int mof_dd_solve_range(mof_dd *dd, const double *I, const double *I2, const double *t_k,
+                       int32_t T, int32_t k0, int32_t k1, double lambda, const mof_opts *opts,
+                       double *V_out, mof_stats *stats);
+
 /* Measurement helper for bench.py: launches the PCG SpMV kernel `reps` times
  * back to back on `batch` systems of the last solve's working set, timed with
  * HIP events on the handle's stream. Returns the mean launch time and the

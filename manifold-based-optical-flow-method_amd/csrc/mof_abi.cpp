@@ -12,6 +12,7 @@
 #include <new>
 
 #include "mof_amg.h"
+#include "mof_dd.h"
 #include "mof_internal.h"
 
 namespace {
@@ -101,6 +102,116 @@ void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop
 // error handling for the host-only entry points of mof_io.cpp
 int mof_io_guard(const std::function<void()> &f) { return guarded(f); }
 
+namespace mof {
+
+void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t *tri,
+                const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
+                const int32_t *perm_in, const int32_t *tri_ids) {
+    m->N = N;
+    m->M = M;
+    m->device = device;
+    m->flags = flags;
+    double t0 = now_ms();
+    MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
+    for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+        MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
+    // internal vertex order (RCM) and triangle order (by smallest
+    // internal vertex id), and the relabelled inputs
+    m->perm.resize(N);
+    m->tperm.resize(M);
+    for (int32_t i = 0; i < N; ++i) m->perm[i] = i;
+    for (int32_t T = 0; T < M; ++T) m->tperm[T] = T;
+    if (perm_in || !(flags & MOF_NO_REORDER)) {
+        if (perm_in) {
+            m->perm.assign(perm_in, perm_in + N);
+        } else {
+            mof::Pattern adj;
+            mof::build_pattern(tri, N, M, adj);
+            m->perm = mof::rcm_order(adj);
+        }
+        std::vector<int32_t> key(M);
+        for (int32_t T = 0; T < M; ++T)
+            key[T] = std::min({m->perm[tri[3 * (size_t)T]], m->perm[tri[3 * (size_t)T + 1]],
+                               m->perm[tri[3 * (size_t)T + 2]]});
+        std::stable_sort(m->tperm.begin(), m->tperm.end(),
+                         [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    }
+    m->inv.resize(N);
+    for (int32_t i = 0; i < N; ++i) m->inv[m->perm[i]] = i;
+    m->tinv.resize(M);
+    for (int32_t T = 0; T < M; ++T) m->tinv[m->tperm[T]] = T;
+    std::vector<int32_t> tri_new(3 * (size_t)M), tri_old(3 * (size_t)M);
+    std::vector<double> area_new(M);
+    for (int32_t T = 0; T < M; ++T) {
+        const int32_t To = m->tperm[T];
+        for (int c = 0; c < 3; ++c) {
+            tri_old[3 * (size_t)T + c] = (tri_ids ? tri_ids : tri)[3 * (size_t)To + c];
+            tri_new[3 * (size_t)T + c] = m->perm[tri[3 * (size_t)To + c]];
+        }
+        area_new[T] = area[To];
+    }
+    std::vector<double> xyz_new(3 * (size_t)N), nrm_new(3 * (size_t)N);
+    for (int32_t i = 0; i < N; ++i)
+        for (int d = 0; d < 3; ++d) {
+            xyz_new[3 * (size_t)m->perm[i] + d] = xyz[3 * (size_t)i + d];
+            nrm_new[3 * (size_t)m->perm[i] + d] = nrm[3 * (size_t)i + d];
+        }
+    mof::build_pattern(tri_new.data(), N, M, m->pat, m->tinv.data());
+    m->ms_pattern = now_ms() - t0;
+    MOF_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+    hipStream_t s = m->stream;
+    const mof::Pattern &P = m->pat;
+    m->tri.alloc(3 * (size_t)M);
+    m->tri.upload(tri_new.data(), 3 * (size_t)M, s);
+    m->tri_orig.alloc(3 * (size_t)M);
+    m->tri_orig.upload(tri_old.data(), 3 * (size_t)M, s);
+    m->perm_d.alloc(N);
+    m->perm_d.upload(m->perm.data(), N, s);
+    m->area.alloc(M);
+    m->area.upload(area_new.data(), M, s);
+    auto put = [&](mof::DevArray<int32_t> &d, const std::vector<int32_t> &h) {
+        d.alloc(h.size());
+        d.upload(h.data(), h.size(), s);
+    };
+    put(m->vptr, P.vptr);
+    put(m->vcol, P.vcol);
+    put(m->cptr, P.cptr);
+    put(m->clist, P.clist);
+    put(m->sell_off, P.sell_off);
+    put(m->sell_col, P.sell_col);
+    put(m->sell_blk, P.sell_blk);
+    put(m->blk_row, P.blk_row);
+    put(m->diag_pos, P.diag_pos);
+    put(m->tsell_off, P.tsell_off);
+    put(m->tinc, P.tinc);
+    mof::DevArray<double> dxyz, dnrm;
+    dxyz.alloc(3 * (size_t)N);
+    dxyz.upload(xyz_new.data(), 3 * (size_t)N, s);
+    dnrm.alloc(3 * (size_t)N);
+    dnrm.upload(nrm_new.data(), 3 * (size_t)N, s);
+    m->e.alloc(6 * (size_t)N);
+    m->gw.alloc(9 * (size_t)M);
+    m->iw.alloc(2 * (size_t)M);
+    m->a2.alloc(4 * (size_t)P.sell_nb());
+    m->a2.zero(s);
+    m->a2s64.alloc(4 * (size_t)P.sell_nb());
+    m->a2s32.alloc(4 * (size_t)P.sell_nb());
+    m->w12_64.alloc((size_t)M + 1);
+    m->w12_32.alloc((size_t)M + 1);
+    m->Aexp.alloc(4 * (size_t)P.sell_nb());
+    m->Aexp.zero(s);
+    m->fexp.alloc(2 * (size_t)N);
+    Events ev;
+    MOF_HIP(hipEventRecord(ev.e[0], s));
+    mof::launch_geometry(m, dxyz.p, dnrm.p, (flags & MOF_GEOM_F32_POINTS) != 0);
+    mof::launch_a2(m);
+    MOF_HIP(hipEventRecord(ev.e[1], s));
+    MOF_HIP(hipStreamSynchronize(s));
+    m->ms_geometry = ev.ms(0, 1);
+}
+
+}  // namespace mof
+
 extern "C" {
 
 const char *mof_version(void) { return "mofhip 0.1 (gfx950, abi 1)"; }
@@ -128,103 +239,7 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
         DeviceGuard dg(device);
         auto *m = new mof_mesh();
         try {
-            m->N = N;
-            m->M = M;
-            m->device = device;
-            m->flags = flags;
-            double t0 = now_ms();
-            MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
-            for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
-                MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
-            // internal vertex order (RCM) and triangle order (by smallest
-            // internal vertex id), and the relabelled inputs
-            m->perm.resize(N);
-            m->tperm.resize(M);
-            for (int32_t i = 0; i < N; ++i) m->perm[i] = i;
-            for (int32_t T = 0; T < M; ++T) m->tperm[T] = T;
-            if (!(flags & MOF_NO_REORDER)) {
-                mof::Pattern adj;
-                mof::build_pattern(tri, N, M, adj);
-                m->perm = mof::rcm_order(adj);
-                std::vector<int32_t> key(M);
-                for (int32_t T = 0; T < M; ++T)
-                    key[T] = std::min({m->perm[tri[3 * (size_t)T]], m->perm[tri[3 * (size_t)T + 1]],
-                                       m->perm[tri[3 * (size_t)T + 2]]});
-                std::stable_sort(m->tperm.begin(), m->tperm.end(),
-                                 [&](int32_t a, int32_t b) { return key[a] < key[b]; });
-            }
-            m->inv.resize(N);
-            for (int32_t i = 0; i < N; ++i) m->inv[m->perm[i]] = i;
-            m->tinv.resize(M);
-            for (int32_t T = 0; T < M; ++T) m->tinv[m->tperm[T]] = T;
-            std::vector<int32_t> tri_new(3 * (size_t)M), tri_old(3 * (size_t)M);
-            std::vector<double> area_new(M);
-            for (int32_t T = 0; T < M; ++T) {
-                const int32_t To = m->tperm[T];
-                for (int c = 0; c < 3; ++c) {
-                    tri_old[3 * (size_t)T + c] = tri[3 * (size_t)To + c];
-                    tri_new[3 * (size_t)T + c] = m->perm[tri[3 * (size_t)To + c]];
-                }
-                area_new[T] = area[To];
-            }
-            std::vector<double> xyz_new(3 * (size_t)N), nrm_new(3 * (size_t)N);
-            for (int32_t i = 0; i < N; ++i)
-                for (int d = 0; d < 3; ++d) {
-                    xyz_new[3 * (size_t)m->perm[i] + d] = xyz[3 * (size_t)i + d];
-                    nrm_new[3 * (size_t)m->perm[i] + d] = nrm[3 * (size_t)i + d];
-                }
-            mof::build_pattern(tri_new.data(), N, M, m->pat, m->tinv.data());
-            m->ms_pattern = now_ms() - t0;
-            MOF_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
-            hipStream_t s = m->stream;
-            const mof::Pattern &P = m->pat;
-            m->tri.alloc(3 * (size_t)M);
-            m->tri.upload(tri_new.data(), 3 * (size_t)M, s);
-            m->tri_orig.alloc(3 * (size_t)M);
-            m->tri_orig.upload(tri_old.data(), 3 * (size_t)M, s);
-            m->perm_d.alloc(N);
-            m->perm_d.upload(m->perm.data(), N, s);
-            m->area.alloc(M);
-            m->area.upload(area_new.data(), M, s);
-            auto put = [&](mof::DevArray<int32_t> &d, const std::vector<int32_t> &h) {
-                d.alloc(h.size());
-                d.upload(h.data(), h.size(), s);
-            };
-            put(m->vptr, P.vptr);
-            put(m->vcol, P.vcol);
-            put(m->cptr, P.cptr);
-            put(m->clist, P.clist);
-            put(m->sell_off, P.sell_off);
-            put(m->sell_col, P.sell_col);
-            put(m->sell_blk, P.sell_blk);
-            put(m->blk_row, P.blk_row);
-            put(m->diag_pos, P.diag_pos);
-            put(m->tsell_off, P.tsell_off);
-            put(m->tinc, P.tinc);
-            mof::DevArray<double> dxyz, dnrm;
-            dxyz.alloc(3 * (size_t)N);
-            dxyz.upload(xyz_new.data(), 3 * (size_t)N, s);
-            dnrm.alloc(3 * (size_t)N);
-            dnrm.upload(nrm_new.data(), 3 * (size_t)N, s);
-            m->e.alloc(6 * (size_t)N);
-            m->gw.alloc(9 * (size_t)M);
-            m->iw.alloc(2 * (size_t)M);
-            m->a2.alloc(4 * (size_t)P.sell_nb());
-            m->a2.zero(s);
-            m->a2s64.alloc(4 * (size_t)P.sell_nb());
-            m->a2s32.alloc(4 * (size_t)P.sell_nb());
-            m->w12_64.alloc((size_t)M + 1);
-            m->w12_32.alloc((size_t)M + 1);
-            m->Aexp.alloc(4 * (size_t)P.sell_nb());
-            m->Aexp.zero(s);
-            m->fexp.alloc(2 * (size_t)N);
-            Events ev;
-            MOF_HIP(hipEventRecord(ev.e[0], s));
-            mof::launch_geometry(m, dxyz.p, dnrm.p, (flags & MOF_GEOM_F32_POINTS) != 0);
-            mof::launch_a2(m);
-            MOF_HIP(hipEventRecord(ev.e[1], s));
-            MOF_HIP(hipStreamSynchronize(s));
-            m->ms_geometry = ev.ms(0, 1);
+            mof::mesh_build(m, xyz, nrm, tri, area, N, M, device, flags, nullptr, nullptr);
         } catch (...) {
             mof_mesh_destroy(m);
             throw;

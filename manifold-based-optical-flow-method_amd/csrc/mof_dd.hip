@@ -1,0 +1,672 @@
+// mof_dd.hip -- domain-decomposed solve of one timestep over P vertex parts
+// (mof_dd.h): halo kernels, the two transports
+// (in-process on one device, RCCL with one process per GPU) and the mof_dd_*
+// entry points of include/mof.h.
+//
+// Halo (in-process): one gather launch covers the ghost rows of every part,
+//   z_p[b][n_own_p + g] = z_q[b][ghost_src]   (one entry per ghost row).
+// Halo (RCCL): pack the rows each neighbour reads into [B][rows][2] segments,
+//   ncclSend/ncclRecv with all neighbours inside one group, unpack into the
+//   ghost rows (they are grouped by owner, so a received segment is one
+//   contiguous ghost range per system).
+// Partial sums: every PCG kernel writes its part's records of the shared
+//   [P][B][nmax] array; with RCCL each rank then all-gathers them in place.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <type_traits>
+
+#include <rccl/rccl.h>
+
+#include "mof_dd.h"
+#include "mof_internal.h"
+#include "mof_rowkern.h"
+
+int mof_io_guard(const std::function<void()> &f);  // mof_abi.cpp
+
+namespace mof {
+
+// ---- RCCL, opened at run time (only the RCCL transport needs it) ----------
+// The entry points this file calls, with rccl.h's types.
+struct RcclApi {
+    void *h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+
+namespace {
+
+RcclApi *rccl_open() {
+    static RcclApi api;
+    static bool tried = false;
+    if (api.h) return &api;
+    MOF_REQUIRE(!tried, "librccl could not be loaded");
+    tried = true;
+    const char *env = getenv("MOF_RCCL_LIB");
+    const char *names[] = {env, "librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
+    for (const char *n : names) {
+        if (!n) continue;
+        api.h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+        if (api.h) break;
+    }
+    if (!api.h) throw Error{MOF_E_HIP, std::string("cannot load librccl: ") + dlerror()};
+    auto sym = [&](const char *s) {
+        void *f = dlsym(api.h, s);
+        if (!f) throw Error{MOF_E_HIP, std::string("librccl lacks ") + s};
+        return f;
+    };
+    auto load = [&](auto &fn, const char *name) { fn = reinterpret_cast<std::decay_t<decltype(fn)>>(sym(name)); };
+    load(api.get_unique_id, "ncclGetUniqueId");
+    load(api.comm_init_rank, "ncclCommInitRank");
+    load(api.comm_destroy, "ncclCommDestroy");
+    load(api.all_gather, "ncclAllGather");
+    load(api.send, "ncclSend");
+    load(api.recv, "ncclRecv");
+    load(api.group_start, "ncclGroupStart");
+    load(api.group_end, "ncclGroupEnd");
+    load(api.error_string, "ncclGetErrorString");
+    return &api;
+}
+
+void nccl_check(RcclApi *a, ncclResult_t rc, const char *what) {
+    if (rc != ncclSuccess) throw Error{MOF_E_HIP, std::string(what) + " failed: " + a->error_string(rc)};
+}
+
+// ---- kernels ----------------------------------------------------------------
+
+// z_dst[b][dst row] = z_src[b][src row] for every ghost row of every part
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_halo_pull(int64_t n, int32_t B, const int4 *__restrict__ ent,
+                                                   void *const *__restrict__ base,
+                                                   const int32_t *__restrict__ nloc) {
+    const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (e >= n) return;
+    using V2 = typename std::conditional<sizeof(V) == 4, float2, double2>::type;
+    const int4 q = ent[e];
+    V2 *dst = reinterpret_cast<V2 *>(base[q.x]);
+    const V2 *src = reinterpret_cast<const V2 *>(base[q.z]);
+    const int64_t ld = nloc[q.x], ls = nloc[q.z];
+    for (int32_t b = 0; b < B; ++b) dst[b * ld + q.y] = src[b * ls + q.w];
+}
+
+// sendbuf segment k (rows [off_k, off_k + cnt_k) of the send list) as
+// [B][cnt_k][2] at element offset 2 B off_k; ent = {row, off_k, cnt_k, -}
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_halo_pack(int64_t n, int32_t B, int32_t nloc,
+                                                   const int4 *__restrict__ ent, const V *__restrict__ x,
+                                                   V *__restrict__ buf) {
+    const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (e >= n) return;
+    const int4 q = ent[e];
+    for (int32_t b = 0; b < B; ++b) {
+        const int64_t o = 2 * ((int64_t)B * q.y + (int64_t)b * q.z + (e - q.y));
+        buf[o] = x[2 * ((int64_t)b * nloc + q.x)];
+        buf[o + 1] = x[2 * ((int64_t)b * nloc + q.x) + 1];
+    }
+}
+
+// ghost row g (= entry e) of the local part from the receive buffer; ent =
+// {n_own + g, off_k, cnt_k, -}
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_halo_unpack(int64_t n, int32_t B, int32_t nloc,
+                                                     const int4 *__restrict__ ent, const V *__restrict__ buf,
+                                                     V *__restrict__ x) {
+    const int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (e >= n) return;
+    const int4 q = ent[e];
+    for (int32_t b = 0; b < B; ++b) {
+        const int64_t o = 2 * ((int64_t)B * q.y + (int64_t)b * q.z + (e - q.y));
+        x[2 * ((int64_t)b * nloc + q.x)] = buf[o];
+        x[2 * ((int64_t)b * nloc + q.x) + 1] = buf[o + 1];
+    }
+}
+
+// planar V rows of one part's owned vertices (caller order; failed systems
+// NaN-filled): V[b][g] = x[b][i].0, V[b][N + g] = x[b][i].1
+__global__ __launch_bounds__(kWG) void k_dd_scatter(int32_t n_own, int32_t nloc, int32_t N,
+                                                    const int32_t *__restrict__ l2g,
+                                                    const double *__restrict__ x,
+                                                    const int32_t *__restrict__ sysi,
+                                                    double *__restrict__ V) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= n_own) return;
+    const bool failed = sysi[b * kSysStride + SI_FAILED] != 0;
+    const double2 v = *reinterpret_cast<const double2 *>(x + 2 * ((int64_t)b * nloc + i));
+    const int32_t g = l2g[i];
+    const double nan = __builtin_nan("");
+    V[(int64_t)b * 2 * N + g] = failed ? nan : v.x;
+    V[(int64_t)b * 2 * N + N + g] = failed ? nan : v.y;
+}
+
+// RCCL: owned x64 rows -> this rank's [B][nmax_own][2] record of vgather
+__global__ __launch_bounds__(kWG) void k_dd_own_pack(int32_t n_own, int32_t nloc, int32_t nmax_own,
+                                                     const double *__restrict__ x,
+                                                     const int32_t *__restrict__ sysi,
+                                                     double *__restrict__ out) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= n_own) return;
+    const bool failed = sysi[b * kSysStride + SI_FAILED] != 0;
+    double2 v = *reinterpret_cast<const double2 *>(x + 2 * ((int64_t)b * nloc + i));
+    if (failed) v = make_double2(__builtin_nan(""), __builtin_nan(""));
+    *reinterpret_cast<double2 *>(out + 2 * ((int64_t)b * nmax_own + i)) = v;
+}
+
+// RCCL: all parts' gathered owned rows -> planar V
+__global__ __launch_bounds__(kWG) void k_dd_own_scatter(int32_t P, int32_t B, int32_t nmax_own, int32_t N,
+                                                        const int32_t *__restrict__ l2g,
+                                                        const double *__restrict__ in,
+                                                        double *__restrict__ V) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= nmax_own) return;
+    for (int32_t q = 0; q < P; ++q) {
+        const int32_t g = l2g[(int64_t)q * nmax_own + i];
+        if (g < 0) continue;
+        const double2 v = *reinterpret_cast<const double2 *>(in + 2 * (((int64_t)q * B + b) * nmax_own + i));
+        V[(int64_t)b * 2 * N + g] = v.x;
+        V[(int64_t)b * 2 * N + N + g] = v.y;
+    }
+}
+
+inline unsigned blocks(int64_t n) { return (unsigned)((n + kWG - 1) / kWG); }
+
+}  // namespace
+
+// ---- transport hooks ---------------------------------------------------------
+
+void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s) {
+    if (d->rank < 0 || d->P == 1) return;  // in-process: one shared array
+    nccl_check(d->nccl,
+               d->nccl->all_gather(base + per_part * (size_t)d->rank, base, per_part, ncclFloat64, static_cast<ncclComm_t>(d->comm), s),
+               "ncclAllGather(partials)");
+}
+
+void dd_halo(mof_dd *d, int32_t B, bool f32, int which, hipStream_t s) {
+    if (d->P == 1) return;
+    if (d->rank < 0) {
+        const int64_t n = d->n_halo;
+        if (n == 0) return;
+        void *const *tab = d->vbase.p + (which ? d->P : 0);
+        if (f32)
+            k_halo_pull<float><<<blocks(n), kWG, 0, s>>>(n, B, d->halo.p, tab, d->nloc.p);
+        else
+            k_halo_pull<double><<<blocks(n), kWG, 0, s>>>(n, B, d->halo.p, tab, d->nloc.p);
+        MOF_HIP(hipGetLastError());
+        return;
+    }
+    const DdPart &D = d->plan.parts[d->rank];
+    const int32_t nloc = D.n_loc();
+    const int64_t ns = (int64_t)D.send_idx.size(), ng = D.n_ghost;
+    const size_t esz = f32 ? 4 : 8;
+    void *vec = which ? (void *)d->parts[0]->ws.x64.p : (void *)d->parts[0]->ws.vz.p;
+    const ncclDataType_t dt = f32 ? ncclFloat32 : ncclFloat64;
+    if (ns > 0) {
+        if (f32)
+            k_halo_pack<float><<<blocks(ns), kWG, 0, s>>>(ns, B, nloc, d->send_ent.p,
+                                                          static_cast<const float *>(vec),
+                                                          reinterpret_cast<float *>(d->sendbuf.p));
+        else
+            k_halo_pack<double><<<blocks(ns), kWG, 0, s>>>(ns, B, nloc, d->send_ent.p,
+                                                           static_cast<const double *>(vec), d->sendbuf.p);
+        MOF_HIP(hipGetLastError());
+    }
+    RcclApi *a = d->nccl;
+    nccl_check(a, a->group_start(), "ncclGroupStart");
+    for (size_t k = 0; k < D.nbr.size(); ++k) {
+        const size_t so = 2 * (size_t)B * D.send_off[k], sc = 2 * (size_t)B * (D.send_off[k + 1] - D.send_off[k]);
+        const size_t ro = 2 * (size_t)B * D.recv_off[k], rc = 2 * (size_t)B * (D.recv_off[k + 1] - D.recv_off[k]);
+        char *sb = reinterpret_cast<char *>(d->sendbuf.p), *rb = reinterpret_cast<char *>(d->recvbuf.p);
+        if (sc) nccl_check(a, a->send(sb + so * esz, sc, dt, D.nbr[k], static_cast<ncclComm_t>(d->comm), s), "ncclSend");
+        if (rc) nccl_check(a, a->recv(rb + ro * esz, rc, dt, D.nbr[k], static_cast<ncclComm_t>(d->comm), s), "ncclRecv");
+    }
+    nccl_check(a, a->group_end(), "ncclGroupEnd");
+    if (ng > 0) {
+        if (f32)
+            k_halo_unpack<float><<<blocks(ng), kWG, 0, s>>>(ng, B, nloc, d->recv_ent.p,
+                                                            reinterpret_cast<const float *>(d->recvbuf.p),
+                                                            static_cast<float *>(vec));
+        else
+            k_halo_unpack<double><<<blocks(ng), kWG, 0, s>>>(ng, B, nloc, d->recv_ent.p, d->recvbuf.p,
+                                                             static_cast<double *>(vec));
+        MOF_HIP(hipGetLastError());
+    }
+}
+
+void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s) {
+    if (d->rank < 0) {
+        for (size_t l = 0; l < d->parts.size(); ++l) {
+            const DdPart &D = d->plan.parts[d->part_ids[l]];
+            mof_mesh *m = d->parts[l];
+            k_dd_scatter<<<dim3(blocks(D.n_own), (unsigned)B), kWG, 0, s>>>(
+                D.n_own, D.n_loc(), d->N, d->own_l2g.p + d->own_off[l], m->ws.x64.p, m->ws.sysi.p, V);
+        }
+        MOF_HIP(hipGetLastError());
+        return;
+    }
+    const DdPart &D = d->plan.parts[d->rank];
+    mof_mesh *m = d->parts[0];
+    const size_t per = 2 * (size_t)B * d->nmax_own;
+    k_dd_own_pack<<<dim3(blocks(D.n_own), (unsigned)B), kWG, 0, s>>>(D.n_own, D.n_loc(), d->nmax_own, m->ws.x64.p,
+                                                                     m->ws.sysi.p, d->vgather.p + per * d->rank);
+    MOF_HIP(hipGetLastError());
+    if (d->P > 1)
+        nccl_check(d->nccl, d->nccl->all_gather(d->vgather.p + per * d->rank, d->vgather.p, per, ncclFloat64,
+                                                static_cast<ncclComm_t>(d->comm), s),
+                   "ncclAllGather(V)");
+    k_dd_own_scatter<<<dim3(blocks(d->nmax_own), (unsigned)B), kWG, 0, s>>>(d->P, B, d->nmax_own, d->N,
+                                                                            d->all_l2g.p, d->vgather.p, V);
+    MOF_HIP(hipGetLastError());
+}
+
+void dd_ensure(mof_dd *d, int32_t B, uint32_t precision) {
+    for (mof_mesh *m : d->parts) ensure_workspace(m, B, precision);
+    if (d->rank < 0) {
+        // halo pointer tables (the workspaces may have been reallocated)
+        std::vector<void *> tab(2 * (size_t)d->P);
+        for (int32_t p = 0; p < d->P; ++p) {
+            tab[p] = d->parts[p]->ws.vz.p;
+            tab[d->P + p] = d->parts[p]->ws.x64.p;
+        }
+        MOF_HIP(hipMemcpy(d->vbase.p, tab.data(), sizeof(void *) * tab.size(), hipMemcpyHostToDevice));
+    }
+    if (d->cap >= B) return;
+    d->cap = B;
+    int32_t nmax = 0;
+    for (const DdPart &D : d->plan.parts)
+        nmax = std::max(nmax, (int32_t)((D.n_loc() + kRowsPerWG - 1) / kRowsPerWG));
+    d->nmax = nmax;
+    const size_t rec = (size_t)d->P * B * nmax;
+    d->part_pq.alloc(rec);
+    d->part_rzrr.alloc(4 * rec);
+    d->part_rr0.alloc(2 * rec);
+    if (d->rank >= 0) {
+        const DdPart &D = d->plan.parts[d->rank];
+        d->sendbuf.alloc(2 * (size_t)B * std::max<size_t>(1, D.send_idx.size()));
+        d->recvbuf.alloc(2 * (size_t)B * std::max<int32_t>(1, D.n_ghost));
+        d->vgather.alloc(2 * (size_t)d->P * B * d->nmax_own);
+    }
+}
+
+}  // namespace mof
+
+namespace {
+
+double dd_now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+struct DevGuard {
+    int prev = 0;
+    explicit DevGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        MOF_HIP(hipSetDevice(dev));
+    }
+    ~DevGuard() { (void)hipSetDevice(prev); }
+};
+
+// host halo/plan tables and the part meshes of one mof_dd
+void dd_setup(mof_dd *d, const double *xyz, const double *nrm, const int32_t *tri, const double *area,
+              const int32_t *part_in) {
+    using namespace mof;
+    const double t0 = dd_now_ms();
+    const int32_t N = d->N, M = d->M, P = d->P;
+    std::vector<int32_t> part(N);
+    if (part_in)
+        std::copy(part_in, part_in + N, part.begin());
+    else
+        partition_rcb(xyz, N, P, part.data());
+    // global RCM position orders the rows inside each part
+    Pattern adj;
+    build_pattern(tri, N, M, adj);
+    const std::vector<int32_t> key = rcm_order(adj);
+    build_dd_plan(tri, N, M, P, part.data(), key.data(), d->plan);
+    MOF_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    if (d->rank < 0)
+        for (int32_t p = 0; p < P; ++p) d->part_ids.push_back(p);
+    else
+        d->part_ids.push_back(d->rank);
+    std::vector<int32_t> own;
+    for (int32_t p : d->part_ids) {
+        const DdPart &D = d->plan.parts[p];
+        const int32_t nl = D.n_loc(), ml = (int32_t)D.tris.size();
+        std::vector<double> lx(3 * (size_t)nl), ln(3 * (size_t)nl), la(ml);
+        std::vector<int32_t> lt(3 * (size_t)ml), gt(3 * (size_t)ml), loc(N, -1), ident(nl);
+        for (int32_t r = 0; r < nl; ++r) {
+            loc[D.l2g[r]] = r;
+            ident[r] = r;
+            for (int c = 0; c < 3; ++c) {
+                lx[3 * (size_t)r + c] = xyz[3 * (size_t)D.l2g[r] + c];
+                ln[3 * (size_t)r + c] = nrm[3 * (size_t)D.l2g[r] + c];
+            }
+        }
+        for (int32_t t = 0; t < ml; ++t) {
+            const int32_t T = D.tris[t];
+            la[t] = area[T];
+            for (int c = 0; c < 3; ++c) {
+                gt[3 * (size_t)t + c] = tri[3 * (size_t)T + c];
+                lt[3 * (size_t)t + c] = loc[tri[3 * (size_t)T + c]];
+            }
+        }
+        auto *m = new mof_mesh();
+        d->parts.push_back(m);
+        // local order fixed (owned first); triangles keep the caller's order for
+        // the folds; I is gathered by the caller's (global) vertex ids
+        mesh_build(m, lx.data(), ln.data(), lt.data(), la.data(), nl, ml, d->device, d->flags, ident.data(),
+                   gt.data());
+        d->own_off.push_back((int64_t)own.size());
+        own.insert(own.end(), D.l2g.begin(), D.l2g.begin() + D.n_own);
+    }
+    d->own_l2g.alloc(own.size());
+    d->own_l2g.upload(own.data(), own.size(), d->stream);
+    if (d->rank < 0) {
+        std::vector<int4> ent;
+        for (int32_t p = 0; p < P; ++p) {
+            const DdPart &D = d->plan.parts[p];
+            for (int32_t g = 0; g < D.n_ghost; ++g)
+                ent.push_back(make_int4(p, D.n_own + g, d->plan.part[D.l2g[D.n_own + g]], D.ghost_src[g]));
+        }
+        d->n_halo = (int64_t)ent.size();
+        d->halo.alloc(std::max<size_t>(1, ent.size()));
+        if (!ent.empty()) d->halo.upload(ent.data(), ent.size(), d->stream);
+        std::vector<int32_t> nl(P);
+        for (int32_t p = 0; p < P; ++p) nl[p] = d->plan.parts[p].n_loc();
+        d->nloc.alloc(P);
+        d->nloc.upload(nl.data(), P, d->stream);
+        d->vbase.alloc(2 * (size_t)P);
+    } else {
+        const DdPart &D = d->plan.parts[d->rank];
+        std::vector<int4> se, re;
+        for (size_t k = 0; k < D.nbr.size(); ++k) {
+            for (int32_t e = D.send_off[k]; e < D.send_off[k + 1]; ++e)
+                se.push_back(make_int4(D.send_idx[e], D.send_off[k], D.send_off[k + 1] - D.send_off[k], 0));
+            for (int32_t g = D.recv_off[k]; g < D.recv_off[k + 1]; ++g)
+                re.push_back(make_int4(D.n_own + g, D.recv_off[k], D.recv_off[k + 1] - D.recv_off[k], 0));
+        }
+        d->send_ent.alloc(std::max<size_t>(1, se.size()));
+        if (!se.empty()) d->send_ent.upload(se.data(), se.size(), d->stream);
+        d->recv_ent.alloc(std::max<size_t>(1, re.size()));
+        if (!re.empty()) d->recv_ent.upload(re.data(), re.size(), d->stream);
+        int32_t nmo = 0;
+        for (const DdPart &Q : d->plan.parts) nmo = std::max(nmo, Q.n_own);
+        d->nmax_own = nmo;
+        std::vector<int32_t> all((size_t)P * nmo, -1);
+        for (int32_t q = 0; q < P; ++q)
+            for (int32_t i = 0; i < d->plan.parts[q].n_own; ++i) all[(size_t)q * nmo + i] = d->plan.parts[q].l2g[i];
+        d->all_l2g.alloc(all.size());
+        d->all_l2g.upload(all.data(), all.size(), d->stream);
+    }
+    MOF_HIP(hipStreamSynchronize(d->stream));
+    d->ms_setup = dd_now_ms() - t0;
+}
+
+void dd_free(mof_dd *d) {
+    if (!d) return;
+    {
+        DevGuard g(d->device);
+        if (d->stream) (void)hipStreamSynchronize(d->stream);
+        for (mof_mesh *m : d->parts) mof_mesh_destroy(m);
+        d->parts.clear();
+        if (d->comm && d->nccl) (void)d->nccl->comm_destroy(static_cast<ncclComm_t>(d->comm));
+        d->comm = nullptr;
+        if (d->stream) (void)hipStreamDestroy(d->stream);
+        d->stream = nullptr;
+        delete d;
+    }
+}
+
+void check_mesh_args(const double *xyz, const double *nrm, const int32_t *tri, const double *area, int32_t N,
+                     int32_t M, int32_t nparts, const int32_t *part) {
+    MOF_REQUIRE(xyz && nrm && tri && area, "NULL input array");
+    MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
+    MOF_REQUIRE(nparts >= 1 && nparts <= N, "need 1 <= nparts <= N");
+    for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+        MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
+    if (part)
+        for (int32_t i = 0; i < N; ++i) MOF_REQUIRE(part[i] >= 0 && part[i] < nparts, "part id out of range");
+}
+
+}  // namespace
+
+extern "C" {
+
+int mof_partition_rcb(const double *xyz, int32_t N, int32_t nparts, int32_t *part) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(xyz && part, "NULL argument");
+        mof::partition_rcb(xyz, N, nparts, part);
+    });
+}
+
+int mof_dd_plan_info(const int32_t *tri, int32_t N, int32_t M, int32_t nparts, const int32_t *part,
+                     int32_t *n_own, int32_t *n_ghost, int32_t *n_nbr, int32_t *n_tri, int64_t *n_send) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(tri && part && n_own && n_ghost && n_nbr && n_tri && n_send, "NULL argument");
+        MOF_REQUIRE(N > 0 && M > 0 && nparts >= 1, "bad sizes");
+        for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+            MOF_REQUIRE(tri[q] >= 0 && tri[q] < N, "triangle vertex index out of range");
+        mof::DdPlan plan;
+        mof::build_dd_plan(tri, N, M, nparts, part, nullptr, plan);
+        for (int32_t p = 0; p < nparts; ++p) {
+            const mof::DdPart &D = plan.parts[p];
+            n_own[p] = D.n_own;
+            n_ghost[p] = D.n_ghost;
+            n_nbr[p] = (int32_t)D.nbr.size();
+            n_tri[p] = (int32_t)D.tris.size();
+            n_send[p] = (int64_t)D.send_idx.size();
+        }
+    });
+}
+
+int mof_dd_create(const double *xyz, const double *nrm, const int32_t *tri, const double *area, int32_t N,
+                  int32_t M, int32_t nparts, const int32_t *part, int32_t device, uint32_t flags, mof_dd **out) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(out, "out is NULL");
+        *out = nullptr;
+        check_mesh_args(xyz, nrm, tri, area, N, M, nparts, part);
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DevGuard g(device);
+        auto *d = new mof_dd();
+        d->N = N;
+        d->M = M;
+        d->P = nparts;
+        d->device = device;
+        d->flags = flags;
+        try {
+            dd_setup(d, xyz, nrm, tri, area, part);
+        } catch (...) {
+            dd_free(d);
+            throw;
+        }
+        *out = d;
+    });
+}
+
+int mof_dd_unique_id(uint8_t *id) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(id, "NULL argument");
+        mof::RcclApi *a = mof::rccl_open();
+        ncclUniqueId u;
+        mof::nccl_check(a, a->get_unique_id(&u), "ncclGetUniqueId");
+        std::memcpy(id, u.internal, MOF_DD_ID_BYTES);
+    });
+}
+
+int mof_dd_create_rank(const double *xyz, const double *nrm, const int32_t *tri, const double *area, int32_t N,
+                       int32_t M, int32_t nranks, const int32_t *part, int32_t rank, const uint8_t *id,
+                       int32_t device, uint32_t flags, mof_dd **out) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(out && id, "NULL argument");
+        *out = nullptr;
+        check_mesh_args(xyz, nrm, tri, area, N, M, nranks, part);
+        MOF_REQUIRE(rank >= 0 && rank < nranks, "rank out of range");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DevGuard g(device);
+        auto *d = new mof_dd();
+        d->N = N;
+        d->M = M;
+        d->P = nranks;
+        d->device = device;
+        d->flags = flags;
+        d->rank = rank;
+        try {
+            d->nccl = mof::rccl_open();
+            ncclUniqueId u;
+            std::memcpy(u.internal, id, sizeof(u.internal));
+            ncclComm_t comm = nullptr;
+            mof::nccl_check(d->nccl, d->nccl->comm_init_rank(&comm, nranks, u, rank), "ncclCommInitRank");
+            d->comm = comm;
+            dd_setup(d, xyz, nrm, tri, area, part);
+        } catch (...) {
+            dd_free(d);
+            throw;
+        }
+        *out = d;
+    });
+}
+
+int mof_dd_destroy(mof_dd *d) {
+    return mof_io_guard([&] { dd_free(d); });
+}
+
+int mof_dd_get_info(const mof_dd *d, mof_dd_info *info) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(d && info, "NULL argument");
+        std::memset(info, 0, sizeof(*info));
+        info->nparts = d->P;
+        info->local_parts = (int32_t)d->parts.size();
+        info->rank = d->rank;
+        for (const mof::DdPart &D : d->plan.parts) {
+            info->ghost_rows += D.n_ghost;
+            info->send_rows += (int64_t)D.send_idx.size();
+            info->max_neighbours = std::max(info->max_neighbours, (int32_t)D.nbr.size());
+            info->max_owned = std::max(info->max_owned, D.n_own);
+        }
+        info->ms_setup = d->ms_setup;
+    });
+}
+
+int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const double *t_k, int32_t T, int32_t k0,
+                       int32_t k1, double lambda, const mof_opts *opts, double *V_out, mof_stats *stats) {
+    return mof_io_guard([&] {
+        using namespace mof;
+        MOF_REQUIRE(d && I && t_k && V_out, "NULL argument");
+        MOF_REQUIRE(T >= 1 && k0 >= 0 && k0 <= k1 && k1 <= T - 1, "need 0 <= k0 <= k1 <= T-1");
+        mof_opts o{};
+        if (opts) {
+            MOF_REQUIRE(opts->struct_size == 0 || opts->struct_size >= sizeof(mof_opts),
+                        "mof_opts.struct_size too small");
+            o = *opts;
+        }
+        MOF_REQUIRE(o.precision == MOF_PREC_F64 || o.precision == MOF_PREC_MIXED, "unknown precision");
+        MOF_REQUIRE(!(o.flags & MOF_PRECOND_AMG), "the decomposed solve uses block Jacobi (no MOF_PRECOND_AMG)");
+        SolveParams sp;
+        sp.precision = o.precision;
+        sp.amg = false;
+        sp.block_jacobi = !(o.flags & MOF_NO_BLOCK_JACOBI);
+        sp.time_spmv = false;
+        sp.max_iter = o.max_iter > 0 ? o.max_iter : 10000;
+        sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
+        sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
+        sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
+        const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
+        if (!I2) I2 = I;
+        DevGuard g(d->device);
+        hipStream_t s = o.stream ? (hipStream_t)o.stream : d->stream;
+        const int32_t K = k1 - k0;
+        const int64_t N = d->N;
+        mof_stats st{};
+        if (K > 0) {
+            int32_t Bmax = o.batch;
+            if (Bmax <= 0) {
+                size_t free_b = 0, total_b = 0;
+                MOF_HIP(hipMemGetInfo(&free_b, &total_b));
+                const double per_sys = 600.0 * (double)N * (d->rank < 0 ? 1.0 : 1.0 / d->P) + 1.0;
+                Bmax = (int32_t)std::max(1.0, std::min(64.0, 0.25 * (double)free_b / per_sys));
+            }
+            const int32_t B = std::min(K, Bmax);
+            dd_ensure(d, B, sp.precision);
+            DevArray<double> Ibuf, Vbuf;
+            if (!dev_io) {
+                Ibuf.alloc(2 * (size_t)N * B);
+                Vbuf.alloc(2 * (size_t)N * B);
+            }
+            for (mof_mesh *m : d->parts) prepare_operator(m, lambda, s);
+            hipEvent_t ev[3];
+            for (auto &e : ev) MOF_HIP(hipEventCreate(&e));
+            std::vector<double> dts(B);
+            try {
+                for (int32_t k = k0; k < k1; k += B) {
+                    const int32_t nb = std::min(B, k1 - k);
+                    for (int32_t b = 0; b < nb; ++b) dts[b] = t_k[k + b + 1] - t_k[k + b];
+                    for (mof_mesh *m : d->parts)
+                        MOF_HIP(hipMemcpyAsync(m->ws.dt.p, dts.data(), sizeof(double) * nb, hipMemcpyHostToDevice, s));
+                    const double *I0p, *I1p;
+                    if (dev_io) {
+                        I0p = I + (int64_t)k * N;
+                        I1p = I2 + (int64_t)(k + 1) * N;
+                    } else {
+                        MOF_HIP(hipMemcpyAsync(Ibuf.p, I + (int64_t)k * N, sizeof(double) * N * nb,
+                                               hipMemcpyHostToDevice, s));
+                        MOF_HIP(hipMemcpyAsync(Ibuf.p + N * B, I2 + (int64_t)(k + 1) * N, sizeof(double) * N * nb,
+                                               hipMemcpyHostToDevice, s));
+                        I0p = Ibuf.p;
+                        I1p = Ibuf.p + N * B;
+                    }
+                    MOF_HIP(hipEventRecord(ev[0], s));
+                    for (mof_mesh *m : d->parts)
+                        launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s);
+                    MOF_HIP(hipEventRecord(ev[1], s));
+                    int32_t outer = 0;
+                    st.iterations += solve_batch_dd(d, nb, sp, s, &outer, &st.max_iterations);
+                    st.outer_steps = outer;
+                    double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : Vbuf.p;
+                    dd_gather_v(d, nb, Vdst, s);
+                    MOF_HIP(hipEventRecord(ev[2], s));
+                    if (!dev_io)
+                        MOF_HIP(hipMemcpyAsync(V_out + (int64_t)(k - k0) * 2 * N, Vbuf.p, sizeof(double) * 2 * N * nb,
+                                               hipMemcpyDeviceToHost, s));
+                    MOF_HIP(hipStreamSynchronize(s));
+                    float a = 0.f, b2 = 0.f;
+                    (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+                    (void)hipEventElapsedTime(&b2, ev[1], ev[2]);
+                    st.ms_assembly += a;
+                    st.ms_solve += b2;
+                    const mof_mesh *m0 = d->parts[0];
+                    for (int32_t b = 0; b < nb; ++b) {
+                        if (m0->h_sysi[b * kSysStride + SI_FAILED]) st.failed++;
+                        st.max_rel_residual = std::max(st.max_rel_residual, m0->h_sysd[b * kSysStride + SD_REL]);
+                    }
+                    st.batches++;
+                }
+            } catch (...) {
+                for (auto &e : ev) (void)hipEventDestroy(e);
+                throw;
+            }
+            for (auto &e : ev) (void)hipEventDestroy(e);
+        }
+        st.systems = K;
+        if (stats) *stats = st;
+        if (st.failed)
+            throw Error{MOF_E_NOCONV, std::to_string(st.failed) + " system(s) did not converge; their V is NaN-filled"};
+    });
+}
+
+}  // extern "C"

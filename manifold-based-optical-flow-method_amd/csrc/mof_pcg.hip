@@ -38,6 +38,7 @@
 #include <chrono>
 #include <cmath>
 
+#include "mof_dd.h"
 #include "mof_internal.h"
 #include "mof_rowkern.h"
 
@@ -62,15 +63,41 @@ struct PcgArgs {
     MatArgs<V> mat;
     const V *dinv;   // [B][N][4]
     V *x, *r, *z, *p, *q;  // [B][N][2]
-    double *part_pq;       // [B][nblk]
-    double *part_rzrr;     // [2][B][nblk][2]
+    double *part_pq;       // [P][B][nmax] (single domain: P = 1, nmax = nblk)
+    double *part_rzrr;     // [2][P][B][nmax][2]
     double *sysd;          // [B][8]
     int32_t *sysi;         // [B][8]
     int32_t ext;           // z and r.z come from an external preconditioner (AMG)
     V *x0;                 // ext: pre-smoothed x0 = omega D^-1 r for the V-cycle
     V omega;
     const uint2 *dh;       // ext (multigrid, fp32): the smoother's 2x2 D^-1, 4 bf16 [B][N]
+    RedArgs red;           // partial-record layout; rows >= red.nown (ghosts) are not summed
 };
+
+// Record of (this part, system b, workgroup w) in a partial array.
+__device__ __forceinline__ int64_t red_rec(const RedArgs &rd, int32_t B, int32_t b, int32_t w) {
+    return ((int64_t)rd.part * B + b) * rd.nmax + w;
+}
+
+// Sum over all parts' partial records of system b, in one fixed order (part,
+// then workgroup), so every part of a decomposed solve gets the same bits.
+template <int NV>
+__device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd, int32_t B, int32_t b,
+                                           double (&out)[NV], double *lds) {
+    if (rd.P == 1) {
+        reduce_partials<NV>(slot + (int64_t)NV * b * rd.nmax, rd.nmax, out, lds);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = 0.0;
+    for (int32_t q = 0; q < rd.P; ++q) {
+        const double *p = slot + (int64_t)NV * ((int64_t)q * B + b) * rd.nmax;
+        for (int32_t w = threadIdx.x; w < rd.nmax; w += kWG)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) out[k] += p[(int64_t)w * NV + k];
+    }
+    block_sum<NV>(out, lds);
+}
 
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
@@ -165,18 +192,18 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
             const V *d = a.dinv + 4 * vi;
             const V z0 = d[0] * r0 + d[1] * r1, z1 = d[2] * r0 + d[3] * r1;
             *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
-            rz += (double)r0 * z0 + (double)r1 * z1;
+            if (i < a.red.nown) rz += (double)r0 * z0 + (double)r1 * z1;  // ghost rows: never summed
         } else if constexpr (sizeof(V) == 4) {
             // the smoother's D^-1 (bf16), as in every later sweep
             const float2 d = bf16_mat2(a.dh[vi], r0, r1);
             *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * d.x, a.omega * d.y};
         }
-        rr += (double)r0 * r0 + (double)r1 * r1;
+        if (i < a.red.nown) rr += (double)r0 * r0 + (double)r1 * r1;
     }
     double v[2] = {rz, rr};
     block_sum<2>(v, lds);
     if (threadIdx.x == 0) {
-        double *o = a.part_rzrr + 2 * ((int64_t)b * a.nblk + blockIdx.x);  // slot 0
+        double *o = a.part_rzrr + 2 * red_rec(a.red, a.B, b, blockIdx.x);  // slot 0
         o[0] = v[0];
         o[1] = v[1];
     }
@@ -193,7 +220,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol) {
         return;
     }
     double v[2];
-    reduce_partials<2>(a.part_rzrr + 2 * (int64_t)b * a.nblk, a.nblk, v, lds);
+    reduce_sys<2>(a.part_rzrr, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) {
         a.sysd[b * kSysStride + SD_TOL2] = rtol * rtol * v[1];
         si[SI_CONV] = -1;
@@ -210,9 +237,9 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
     // word is sticky, so no later launch re-reads a stale partial slot)
     if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || a.sysi[b * kSysStride + SI_CONV] >= 0))
         return;
-    const int64_t ps = (int64_t)a.B * a.nblk * 2;  // slot stride
+    const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;  // slot stride
     double cur[2];
-    reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
+    reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
     if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
         if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
             a.sysi[b * kSysStride + SI_CONV] = it;
@@ -221,8 +248,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
     V beta = 0;
     if (!FIRST) {
         double old[2];
-        reduce_partials<2>(a.part_rzrr + ((it + 1) & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, old,
-                           lds);
+        reduce_sys<2>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
         beta = (V)(cur[0] / old[0]);
     }
     using V2 = typename VT<V>::V2;
@@ -248,11 +274,11 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
         }
         *reinterpret_cast<V2 *>(a.q + 2 * vi) = qi;
         *reinterpret_cast<V2 *>(a.p + 2 * vi) = pi;
-        pq += (double)pi.x * qi.x + (double)pi.y * qi.y;
+        if (i < a.red.nown) pq += (double)pi.x * qi.x + (double)pi.y * qi.y;
     }
     double v[1] = {pq};
     block_sum<1>(v, lds);
-    if (threadIdx.x == 0) a.part_pq[(int64_t)b * a.nblk + rb] = v[0];
+    if (threadIdx.x == 0) a.part_pq[red_rec(a.red, a.B, b, rb)] = v[0];
 }
 
 template <typename V>
@@ -261,12 +287,12 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     const int32_t b = blockIdx.y;
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
-    const int64_t ps = (int64_t)a.B * a.nblk * 2;
+    const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
     double cur[2];
-    reduce_partials<2>(a.part_rzrr + (it & 1) * ps + 2 * (int64_t)b * a.nblk, a.nblk, cur, lds);
+    reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
     if (cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) return;
     double pqv[1];
-    reduce_partials<1>(a.part_pq + (int64_t)b * a.nblk, a.nblk, pqv, lds);
+    reduce_sys<1>(a.part_pq, a.red, a.B, b, pqv, lds);
     if (!(pqv[0] > 0.0) || !isfinite(pqv[0]) || !isfinite(cur[0])) {
         // breakdown: A (or the preconditioner) is not SPD / singular
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -298,18 +324,18 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
             ld_blk(a.dinv, vi, d);
             const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
             *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
-            rz += (double)ri.x * z0 + (double)ri.y * z1;
+            if (i < a.red.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
         } else if constexpr (sizeof(V) == 4) {
             // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
             const float2 d = bf16_mat2(a.dh[vi], ri.x, ri.y);
             *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * d.x, a.omega * d.y};
         }
-        rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
+        if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
     }
     double v[2] = {rz, rr};
     block_sum<2>(v, lds);
     if (threadIdx.x == 0) {
-        double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * ((int64_t)b * a.nblk + blockIdx.x);
+        double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * red_rec(a.red, a.B, blockIdx.y, blockIdx.x);
         o[0] = v[0];
         o[1] = v[1];
     }
@@ -336,7 +362,7 @@ __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
 // partial |r|^2 and |f|^2.
-__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B,
+__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                   const double *__restrict__ rhs,
                                                   const double *__restrict__ x64,
                                                   const int32_t *__restrict__ sysi,
@@ -357,20 +383,22 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
         const double r0 = f.x - y0, r1 = f.y - y1;
         *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
-        rr += r0 * r0 + r1 * r1;
-        ff += f.x * f.x + f.y * f.y;
+        if (i < rd.nown) {
+            rr += r0 * r0 + r1 * r1;
+            ff += f.x * f.x + f.y * f.y;
+        }
     }
     double v[2] = {rr, ff};
     block_sum<2>(v, lds);
     if (threadIdx.x == 0) {
-        double *o = part + 2 * ((int64_t)b * nblk + rb);
+        double *o = part + 2 * red_rec(rd, B, b, rb);
         o[0] = v[0];
         o[1] = v[1];
     }
 }
 
 // One workgroup per system: relative true residual; retire converged systems.
-__global__ __launch_bounds__(kWG) void k_outer_check(int32_t nblk, const double *__restrict__ part,
+__global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, const double *__restrict__ part,
                                                      double rtol, double *__restrict__ sysd,
                                                      int32_t *__restrict__ sysi) {
     __shared__ double lds[8];
@@ -378,7 +406,7 @@ __global__ __launch_bounds__(kWG) void k_outer_check(int32_t nblk, const double 
     int32_t *si = sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) return;
     double v[2];
-    reduce_partials<2>(part + 2 * (int64_t)b * nblk, nblk, v, lds);
+    reduce_sys<2>(part, rd, B, b, v, lds);
     if (threadIdx.x == 0) {
         const double rel = v[1] > 0.0 ? sqrt(v[0] / v[1]) : (v[0] > 0.0 ? INFINITY : 0.0);
         sysd[b * kSysStride + SD_REL] = rel;
@@ -458,6 +486,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.part_rzrr = w.part_rzrr.p;
     a.sysd = w.sysd.p;
     a.sysi = w.sysi.p;
+    a.red = RedArgs{1, 0, w.nblk, m->N};
     a.ext = 0;
     a.x0 = nullptr;
     a.omega = (V)0;
@@ -683,9 +712,10 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
                                  sp.precision, tm, &m->iter_hint[std::min(o, 15)], false);
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
-        k_residual<<<dim3(xcd_grid(w.nblk, B)), kWG, 0, s>>>(o64, w.nblk, B, w.rhs.p, w.x64.p, w.sysi.p,
+        const RedArgs rd{1, 0, w.nblk, m->N};
+        k_residual<<<dim3(xcd_grid(w.nblk, B)), kWG, 0, s>>>(o64, w.nblk, B, rd, w.rhs.p, w.x64.p, w.sysi.p,
                                                               w.r64.p, w.part_rr0.p);
-        k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(w.nblk, w.part_rr0.p, sp.rtol, w.sysd.p,
+        k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -699,6 +729,172 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p);
     MOF_HIP(hipGetLastError());
     fetch_flags(m, B, s);
+    *outer = o;
+    return iters;
+}
+
+// ---- domain-decomposed solve (mof_dd.h): the same kernels on every local
+// part, in lockstep on one stream; ghost rows are computed but never summed,
+// the SpMV operand's ghosts are refreshed by the halo exchange, and every
+// reduction runs over the [P][B][nmax] records of all parts.
+namespace {
+
+template <typename V>
+std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, uint32_t precision) {
+    std::vector<PcgArgs<V>> args;
+    for (size_t l = 0; l < d->parts.size(); ++l) {
+        mof_mesh *m = d->parts[l];
+        Workspace &w = m->ws;
+        PcgArgs<V> a;
+        if constexpr (sizeof(V) == 4)
+            a = make_args<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p);
+        else
+            a = make_args<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p);
+        a.part_pq = d->part_pq.p;
+        a.part_rzrr = d->part_rzrr.p;
+        a.red = RedArgs{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
+        args.push_back(a);
+    }
+    (void)precision;
+    return args;
+}
+
+template <typename V>
+int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_iter, hipStream_t s,
+               int32_t *max_iters, int32_t *hint, uint32_t precision) {
+    std::vector<PcgArgs<V>> args = dd_args<V>(d, B, precision);
+    const size_t L = args.size();
+    mof_mesh *m0 = d->parts[0];
+    const int64_t rec = (int64_t)B * d->nmax;  // records of one part
+    const int64_t ps = (int64_t)d->P * rec * 2;
+    for (size_t l = 0; l < L; ++l) {
+        Workspace &w = d->parts[l]->ws;
+        const double *rhs = first_outer ? w.rhs.p : w.r64.p;
+        k_pcg_init<V><<<dim3((unsigned)w.nblk, (unsigned)B), kWG, 0, s>>>(args[l], rhs);
+    }
+    dd_sync_partials(d, d->part_rzrr.p, 2 * rec, s);
+    for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol);
+    MOF_HIP(hipGetLastError());
+    std::vector<int32_t> was_active(B);
+    for (int32_t b = 0; b < B; ++b) was_active[b] = m0->h_sysi[b * kSysStride + SI_ACTIVE];
+    int32_t it = 0;
+    int32_t chunk = *hint > 0 ? *hint : 8;
+    bool done = false;
+    auto spmv = [&](bool first, int32_t it_) {
+        dd_halo(d, B, sizeof(V) == 4, 0, s);
+        for (size_t l = 0; l < L; ++l) {
+            const dim3 gx(xcd_grid(d->parts[l]->ws.nblk, B));
+            if (first)
+                k_pcg_spmv<V, true><<<gx, kWG, 0, s>>>(args[l], it_, 0);
+            else
+                k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(args[l], it_, 0);
+        }
+        dd_sync_partials(d, d->part_pq.p, rec, s);
+    };
+    while (!done && it < max_iter) {
+        const int32_t n = std::min(chunk, max_iter - it);
+        for (int32_t c = 0; c < n; ++c, ++it) {
+            spmv(it == 0, it);
+            for (size_t l = 0; l < L; ++l)
+                k_pcg_update<V><<<dim3((unsigned)d->parts[l]->ws.nblk, (unsigned)B), kWG, 0, s>>>(args[l], it);
+            dd_sync_partials(d, d->part_rzrr.p + ((it + 1) & 1) * ps, 2 * rec, s);
+        }
+        MOF_HIP(hipGetLastError());
+        fetch_flags(m0, B, s);
+        done = true;
+        for (int32_t b = 0; b < B; ++b) {
+            const int32_t *si = m0->h_sysi + b * kSysStride;
+            if (si[SI_ACTIVE] && !si[SI_FAILED] && si[SI_CONV] < 0) done = false;
+        }
+        chunk = 8;
+    }
+    if (!done) {
+        spmv(false, it);
+        fetch_flags(m0, B, s);
+    }
+    int64_t total = 0;
+    int32_t slowest = 0;
+    for (int32_t b = 0; b < B; ++b) {
+        if (!was_active[b]) continue;
+        const int32_t c = m0->h_sysi[b * kSysStride + SI_CONV];
+        const int32_t its = c >= 0 ? c : it;
+        total += its;
+        slowest = std::max(slowest, its);
+    }
+    *max_iters = std::max(*max_iters, slowest);
+    if (slowest > 0) *hint = slowest + 1;
+    return total;
+}
+
+}  // namespace
+
+int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
+                       int32_t *max_iters) {
+    const size_t L = d->parts.size();
+    mof_mesh *m0 = d->parts[0];
+    // records of workgroups past a part's own count must read as zero, and
+    // their positions move with B: clear the partial arrays per batch
+    MOF_HIP(hipMemsetAsync(d->part_pq.p, 0, d->part_pq.bytes(), s));
+    MOF_HIP(hipMemsetAsync(d->part_rzrr.p, 0, d->part_rzrr.bytes(), s));
+    MOF_HIP(hipMemsetAsync(d->part_rr0.p, 0, d->part_rr0.bytes(), s));
+    for (size_t l = 0; l < L; ++l) {
+        Workspace &w = d->parts[l]->ws;
+        k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
+    }
+    MOF_HIP(hipGetLastError());
+    for (int32_t b = 0; b < B; ++b) {
+        int32_t *si = m0->h_sysi + b * kSysStride;
+        for (int k = 0; k < kSysStride; ++k) si[k] = 0;
+        si[SI_ACTIVE] = 1;
+        si[SI_CONV] = -1;
+    }
+    if (m0->iter_hint.size() < 2 * 16) m0->iter_hint.assign(2 * 16, 0);
+    int64_t iters = 0;
+    int32_t o = 0;
+    for (; o < sp.max_outer; ++o) {
+        if (sp.precision == MOF_PREC_MIXED)
+            iters += pcg_dd<float>(d, B, o == 0, sp.inner_rtol, sp.max_iter, s, max_iters,
+                                   &m0->iter_hint[16 + std::min(o, 15)], sp.precision);
+        else
+            iters += pcg_dd<double>(d, B, o == 0, o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s,
+                                    max_iters, &m0->iter_hint[std::min(o, 15)], sp.precision);
+        for (size_t l = 0; l < L; ++l) {
+            mof_mesh *m = d->parts[l];
+            Workspace &w = m->ws;
+            dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
+            if (sp.precision == MOF_PREC_MIXED)
+                k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
+                                                        w.sysi.p, w.x64.p);
+            else
+                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+        }
+        dd_halo(d, B, false, 1, s);  // the residual reads x64 at the ghosts
+        for (size_t l = 0; l < L; ++l) {
+            mof_mesh *m = d->parts[l];
+            Workspace &w = m->ws;
+            const RedArgs rd{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
+            k_residual<<<dim3(xcd_grid(w.nblk, B)), kWG, 0, s>>>(op64(m), w.nblk, B, rd, w.rhs.p, w.x64.p,
+                                                                  w.sysi.p, w.r64.p, d->part_rr0.p);
+        }
+        dd_sync_partials(d, d->part_rr0.p, 2 * (int64_t)B * d->nmax, s);
+        for (size_t l = 0; l < L; ++l) {
+            Workspace &w = d->parts[l]->ws;
+            const RedArgs rd{d->P, d->part_ids[l], d->nmax, 0};
+            k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, d->part_rr0.p, sp.rtol, w.sysd.p, w.sysi.p);
+        }
+        MOF_HIP(hipGetLastError());
+        fetch_flags(m0, B, s);
+        bool any = false;
+        for (int32_t b = 0; b < B; ++b) any |= m0->h_sysi[b * kSysStride + SI_ACTIVE] != 0;
+        if (!any) {
+            ++o;
+            break;
+        }
+    }
+    for (size_t l = 0; l < L; ++l)
+        k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, d->parts[l]->ws.sysi.p);
+    MOF_HIP(hipGetLastError());
+    fetch_flags(m0, B, s);
     *outer = o;
     return iters;
 }

@@ -9,4 +9,5 @@ next to this package.
 from ._lib import (MofError, NotConverged, build_native, device_count, lib,  # noqa: F401
                    version, EXPORTS, LIB_PATH)
 from .mesh import DeviceMesh  # noqa: F401
+from .decomp import DecomposedMesh, partition_rcb, plan_info  # noqa: F401
 from .solve import velocity_field_sharded, shard_ranges  # noqa: F401

@@ -45,6 +45,8 @@ EXPORTS = (
     "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
     "mof_csv_write", "mof_csv_shape", "mof_csv_read", "mof_ply_info", "mof_ply_read",
     "mof_point_normals", "mof_cell_areas", "mof_singularities", "mof_amg_probe",
+    "mof_partition_rcb", "mof_dd_plan_info", "mof_dd_create", "mof_dd_unique_id",
+    "mof_dd_create_rank", "mof_dd_destroy", "mof_dd_get_info", "mof_dd_solve_range",
 )
 
 
@@ -91,6 +93,17 @@ class MofMeshInfo(ctypes.Structure):
         ("ms_pattern", ctypes.c_double),
     ]
 
+
+class MofDdInfo(ctypes.Structure):
+    _fields_ = [
+        ("nparts", ctypes.c_int32), ("local_parts", ctypes.c_int32), ("rank", ctypes.c_int32),
+        ("max_neighbours", ctypes.c_int32), ("max_owned", ctypes.c_int32),
+        ("pad_", ctypes.c_int32), ("ghost_rows", ctypes.c_int64), ("send_rows", ctypes.c_int64),
+        ("ms_setup", ctypes.c_double),
+    ]
+
+
+MOF_DD_ID_BYTES = 128
 
 _lib = None
 _lock = threading.Lock()
@@ -143,6 +156,15 @@ def lib():
             "mof_singularities": ([i32, P, P, i32, i32, P, i32, f64, u32, P, P, P, P, P],
                                   ctypes.c_int),
             "mof_amg_probe": ([P, P, i32, i32, P, P, P], ctypes.c_int),
+            "mof_partition_rcb": ([P, i32, i32, P], ctypes.c_int),
+            "mof_dd_plan_info": ([P, i32, i32, i32, P, P, P, P, P, P], ctypes.c_int),
+            "mof_dd_create": ([P, P, P, P, i32, i32, i32, P, i32, u32, P], ctypes.c_int),
+            "mof_dd_unique_id": ([P], ctypes.c_int),
+            "mof_dd_create_rank": ([P, P, P, P, i32, i32, i32, P, i32, P, i32, u32, P],
+                                   ctypes.c_int),
+            "mof_dd_destroy": ([P], ctypes.c_int),
+            "mof_dd_get_info": ([P, P], ctypes.c_int),
+            "mof_dd_solve_range": ([P, P, P, P, i32, i32, i32, f64, P, P, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

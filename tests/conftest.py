@@ -42,3 +42,18 @@ def golden_csr(g, prefix):
     n = len(g[prefix + "_indptr"]) - 1
     return sp.csr_matrix((g[prefix + "_data"], g[prefix + "_indices"], g[prefix + "_indptr"]),
                          shape=(n, n))
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _torch_hip_first(request):
+    """torch ships its own copy of the HIP runtime; it must initialise before
+    libmofhip's (as in bench.py) for torch device tensors to coexist with the
+    library in one process. Only when GPU tests were collected."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+    yield
