@@ -167,6 +167,8 @@ def lib():
             "mof_dd_solve_range": ([P, P, P, P, i32, i32, i32, f64, P, P, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
+            if os.environ.get("MOFHIP_LIB") and not hasattr(L, name):
+                continue  # an older build under A/B measurement
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
