@@ -267,7 +267,12 @@ int mof_dd_plan_info(const int32_t *tri, int32_t N, int32_t M, int32_t nparts, c
 
 /* All nparts parts in this process on one device (in-process transport: halo
  * by one gather kernel, shared partial sums). part (N) NULL: RCB. Arguments as
- * mof_mesh_create (flags: MOF_GEOM_F32_POINTS). */
+ * mof_mesh_create (flags: MOF_GEOM_F32_POINTS, MOF_DD_STAGED). */
+#define MOF_DD_STAGED 64u     /* mof_dd_create: exchange halos and gather V
+                                  through the pack / copy / unpack kernels and
+                                  segment layout of the RCCL transport (device
+                                  copies instead of ncclSend/Recv): exercises
+                                  that path on one GPU */
 int mof_dd_create(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
                   int32_t N, int32_t M, int32_t nparts, const int32_t *part, int32_t device,
                   uint32_t flags, mof_dd **out);

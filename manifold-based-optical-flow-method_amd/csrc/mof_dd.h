@@ -85,10 +85,15 @@ struct mof_dd {
     mof::DevArray<int32_t> nloc;     // (P) local rows per part
     mof::DevArray<int32_t> own_l2g;  // owned caller vertices of the local parts, concatenated
     std::vector<int64_t> own_off;    // offset of each local part in own_l2g
-    // RCCL transport
+    // RCCL transport (rank >= 0)
     mof::RcclApi *nccl = nullptr;
     void *comm = nullptr;
-    mof::DevArray<int4> send_ent, recv_ent;  // {row, segment offset, segment rows, -}
+    // pack -> exchange -> unpack (RCCL, or in-process with MOF_DD_STAGED):
+    // entries {row, segment offset, segment rows, -} of the local parts,
+    // concatenated; part l's entries start at send_base[l] / recv_base[l] and
+    // its buffer region at 2 * cap * send_base[l] elements
+    mof::DevArray<int4> send_ent, recv_ent;
+    std::vector<int64_t> send_base, recv_base;
     mof::DevArray<double> sendbuf, recvbuf;  // [B][rows][2] per neighbour segment (fp64 sized)
     mof::DevArray<double> vgather;      // [P][B][nmax_own][2] owned V of every part
     int32_t nmax_own = 0;

@@ -195,9 +195,14 @@ void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s) {
                "ncclAllGather(partials)");
 }
 
+// The pack -> exchange -> unpack path: the RCCL transport, or in-process
+// parts with MOF_DD_STAGED (the same kernels and segment offsets, the
+// exchange done by device copies).
+static bool staged(const mof_dd *d) { return d->rank >= 0 || (d->flags & MOF_DD_STAGED); }
+
 void dd_halo(mof_dd *d, int32_t B, bool f32, int which, hipStream_t s) {
     if (d->P == 1) return;
-    if (d->rank < 0) {
+    if (!staged(d)) {
         const int64_t n = d->n_halo;
         if (n == 0) return;
         void *const *tab = d->vbase.p + (which ? d->P : 0);
@@ -208,46 +213,77 @@ void dd_halo(mof_dd *d, int32_t B, bool f32, int which, hipStream_t s) {
         MOF_HIP(hipGetLastError());
         return;
     }
-    const DdPart &D = d->plan.parts[d->rank];
-    const int32_t nloc = D.n_loc();
-    const int64_t ns = (int64_t)D.send_idx.size(), ng = D.n_ghost;
     const size_t esz = f32 ? 4 : 8;
-    void *vec = which ? (void *)d->parts[0]->ws.x64.p : (void *)d->parts[0]->ws.vz.p;
-    const ncclDataType_t dt = f32 ? ncclFloat32 : ncclFloat64;
-    if (ns > 0) {
+    const size_t L = d->parts.size();
+    char *sbuf = reinterpret_cast<char *>(d->sendbuf.p), *rbuf = reinterpret_cast<char *>(d->recvbuf.p);
+    // byte address of element e of local part l's send / receive region
+    auto sptr = [&](size_t l, int64_t e) { return sbuf + (2 * (size_t)d->cap * d->send_base[l] + e) * esz; };
+    auto rptr = [&](size_t l, int64_t e) { return rbuf + (2 * (size_t)d->cap * d->recv_base[l] + e) * esz; };
+    auto vec = [&](size_t l) {
+        return which ? (void *)d->parts[l]->ws.x64.p : (void *)d->parts[l]->ws.vz.p;
+    };
+    for (size_t l = 0; l < L; ++l) {
+        const DdPart &D = d->plan.parts[d->part_ids[l]];
+        const int64_t ns = (int64_t)D.send_idx.size();
+        if (ns == 0) continue;
+        const int4 *ent = d->send_ent.p + d->send_base[l];
         if (f32)
-            k_halo_pack<float><<<blocks(ns), kWG, 0, s>>>(ns, B, nloc, d->send_ent.p,
-                                                          static_cast<const float *>(vec),
-                                                          reinterpret_cast<float *>(d->sendbuf.p));
+            k_halo_pack<float><<<blocks(ns), kWG, 0, s>>>(ns, B, D.n_loc(), ent, static_cast<const float *>(vec(l)),
+                                                          reinterpret_cast<float *>(sptr(l, 0)));
         else
-            k_halo_pack<double><<<blocks(ns), kWG, 0, s>>>(ns, B, nloc, d->send_ent.p,
-                                                           static_cast<const double *>(vec), d->sendbuf.p);
-        MOF_HIP(hipGetLastError());
+            k_halo_pack<double><<<blocks(ns), kWG, 0, s>>>(ns, B, D.n_loc(), ent,
+                                                           static_cast<const double *>(vec(l)),
+                                                           reinterpret_cast<double *>(sptr(l, 0)));
     }
-    RcclApi *a = d->nccl;
-    nccl_check(a, a->group_start(), "ncclGroupStart");
-    for (size_t k = 0; k < D.nbr.size(); ++k) {
-        const size_t so = 2 * (size_t)B * D.send_off[k], sc = 2 * (size_t)B * (D.send_off[k + 1] - D.send_off[k]);
-        const size_t ro = 2 * (size_t)B * D.recv_off[k], rc = 2 * (size_t)B * (D.recv_off[k + 1] - D.recv_off[k]);
-        char *sb = reinterpret_cast<char *>(d->sendbuf.p), *rb = reinterpret_cast<char *>(d->recvbuf.p);
-        if (sc) nccl_check(a, a->send(sb + so * esz, sc, dt, D.nbr[k], static_cast<ncclComm_t>(d->comm), s), "ncclSend");
-        if (rc) nccl_check(a, a->recv(rb + ro * esz, rc, dt, D.nbr[k], static_cast<ncclComm_t>(d->comm), s), "ncclRecv");
+    MOF_HIP(hipGetLastError());
+    if (d->rank >= 0) {
+        const DdPart &D = d->plan.parts[d->rank];
+        const ncclDataType_t dt = f32 ? ncclFloat32 : ncclFloat64;
+        RcclApi *a = d->nccl;
+        ncclComm_t comm = static_cast<ncclComm_t>(d->comm);
+        nccl_check(a, a->group_start(), "ncclGroupStart");
+        for (size_t k = 0; k < D.nbr.size(); ++k) {
+            const size_t sc = 2 * (size_t)B * (D.send_off[k + 1] - D.send_off[k]);
+            const size_t rc = 2 * (size_t)B * (D.recv_off[k + 1] - D.recv_off[k]);
+            if (sc) nccl_check(a, a->send(sptr(0, 2 * (int64_t)B * D.send_off[k]), sc, dt, D.nbr[k], comm, s), "ncclSend");
+            if (rc) nccl_check(a, a->recv(rptr(0, 2 * (int64_t)B * D.recv_off[k]), rc, dt, D.nbr[k], comm, s), "ncclRecv");
+        }
+        nccl_check(a, a->group_end(), "ncclGroupEnd");
+    } else {
+        // in-process: part q's segment for p -> p's receive segment for q
+        for (size_t p = 0; p < L; ++p) {
+            const DdPart &D = d->plan.parts[p];
+            for (size_t k = 0; k < D.nbr.size(); ++k) {
+                const int32_t q = D.nbr[k];
+                const DdPart &Q = d->plan.parts[q];
+                const size_t kk = (size_t)(std::lower_bound(Q.nbr.begin(), Q.nbr.end(), (int32_t)p) - Q.nbr.begin());
+                const size_t cnt = (size_t)(D.recv_off[k + 1] - D.recv_off[k]);
+                MOF_REQUIRE(kk < Q.nbr.size() && (size_t)(Q.send_off[kk + 1] - Q.send_off[kk]) == cnt,
+                            "halo segments disagree (internal error)");
+                MOF_HIP(hipMemcpyAsync(rptr(p, 2 * (int64_t)B * D.recv_off[k]), sptr(q, 2 * (int64_t)B * Q.send_off[kk]),
+                                       2 * (size_t)B * cnt * esz, hipMemcpyDeviceToDevice, s));
+            }
+        }
     }
-    nccl_check(a, a->group_end(), "ncclGroupEnd");
-    if (ng > 0) {
+    for (size_t l = 0; l < L; ++l) {
+        const DdPart &D = d->plan.parts[d->part_ids[l]];
+        const int64_t ng = D.n_ghost;
+        if (ng == 0) continue;
+        const int4 *ent = d->recv_ent.p + d->recv_base[l];
         if (f32)
-            k_halo_unpack<float><<<blocks(ng), kWG, 0, s>>>(ng, B, nloc, d->recv_ent.p,
-                                                            reinterpret_cast<const float *>(d->recvbuf.p),
-                                                            static_cast<float *>(vec));
+            k_halo_unpack<float><<<blocks(ng), kWG, 0, s>>>(ng, B, D.n_loc(), ent,
+                                                            reinterpret_cast<const float *>(rptr(l, 0)),
+                                                            static_cast<float *>(vec(l)));
         else
-            k_halo_unpack<double><<<blocks(ng), kWG, 0, s>>>(ng, B, nloc, d->recv_ent.p, d->recvbuf.p,
-                                                             static_cast<double *>(vec));
-        MOF_HIP(hipGetLastError());
+            k_halo_unpack<double><<<blocks(ng), kWG, 0, s>>>(ng, B, D.n_loc(), ent,
+                                                             reinterpret_cast<const double *>(rptr(l, 0)),
+                                                             static_cast<double *>(vec(l)));
     }
+    MOF_HIP(hipGetLastError());
 }
 
 void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s) {
-    if (d->rank < 0) {
+    if (!staged(d)) {
         for (size_t l = 0; l < d->parts.size(); ++l) {
             const DdPart &D = d->plan.parts[d->part_ids[l]];
             mof_mesh *m = d->parts[l];
@@ -257,13 +293,18 @@ void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s) {
         MOF_HIP(hipGetLastError());
         return;
     }
-    const DdPart &D = d->plan.parts[d->rank];
-    mof_mesh *m = d->parts[0];
+    // every part's owned rows into its [B][nmax_own][2] record, all-gathered
+    // (RCCL), then one scatter of all records into the planar V
     const size_t per = 2 * (size_t)B * d->nmax_own;
-    k_dd_own_pack<<<dim3(blocks(D.n_own), (unsigned)B), kWG, 0, s>>>(D.n_own, D.n_loc(), d->nmax_own, m->ws.x64.p,
-                                                                     m->ws.sysi.p, d->vgather.p + per * d->rank);
+    for (size_t l = 0; l < d->parts.size(); ++l) {
+        const int32_t p = d->part_ids[l];
+        const DdPart &D = d->plan.parts[p];
+        mof_mesh *m = d->parts[l];
+        k_dd_own_pack<<<dim3(blocks(D.n_own), (unsigned)B), kWG, 0, s>>>(D.n_own, D.n_loc(), d->nmax_own, m->ws.x64.p,
+                                                                         m->ws.sysi.p, d->vgather.p + per * p);
+    }
     MOF_HIP(hipGetLastError());
-    if (d->P > 1)
+    if (d->rank >= 0 && d->P > 1)
         nccl_check(d->nccl, d->nccl->all_gather(d->vgather.p + per * d->rank, d->vgather.p, per, ncclFloat64,
                                                 static_cast<ncclComm_t>(d->comm), s),
                    "ncclAllGather(V)");
@@ -274,7 +315,7 @@ void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s) {
 
 void dd_ensure(mof_dd *d, int32_t B, uint32_t precision) {
     for (mof_mesh *m : d->parts) ensure_workspace(m, B, precision);
-    if (d->rank < 0) {
+    if (!staged(d)) {
         // halo pointer tables (the workspaces may have been reallocated)
         std::vector<void *> tab(2 * (size_t)d->P);
         for (int32_t p = 0; p < d->P; ++p) {
@@ -293,10 +334,9 @@ void dd_ensure(mof_dd *d, int32_t B, uint32_t precision) {
     d->part_pq.alloc(rec);
     d->part_rzrr.alloc(4 * rec);
     d->part_rr0.alloc(2 * rec);
-    if (d->rank >= 0) {
-        const DdPart &D = d->plan.parts[d->rank];
-        d->sendbuf.alloc(2 * (size_t)B * std::max<size_t>(1, D.send_idx.size()));
-        d->recvbuf.alloc(2 * (size_t)B * std::max<int32_t>(1, D.n_ghost));
+    if (staged(d)) {
+        d->sendbuf.alloc(2 * (size_t)B * std::max<int64_t>(1, d->send_base.back()));
+        d->recvbuf.alloc(2 * (size_t)B * std::max<int64_t>(1, d->recv_base.back()));
         d->vgather.alloc(2 * (size_t)d->P * B * d->nmax_own);
     }
 }
@@ -388,14 +428,22 @@ void dd_setup(mof_dd *d, const double *xyz, const double *nrm, const int32_t *tr
         d->nloc.alloc(P);
         d->nloc.upload(nl.data(), P, d->stream);
         d->vbase.alloc(2 * (size_t)P);
-    } else {
-        const DdPart &D = d->plan.parts[d->rank];
+    }
+    if (d->rank >= 0 || (d->flags & MOF_DD_STAGED)) {
+        // pack / unpack entries of every local part, concatenated
         std::vector<int4> se, re;
-        for (size_t k = 0; k < D.nbr.size(); ++k) {
-            for (int32_t e = D.send_off[k]; e < D.send_off[k + 1]; ++e)
-                se.push_back(make_int4(D.send_idx[e], D.send_off[k], D.send_off[k + 1] - D.send_off[k], 0));
-            for (int32_t g = D.recv_off[k]; g < D.recv_off[k + 1]; ++g)
-                re.push_back(make_int4(D.n_own + g, D.recv_off[k], D.recv_off[k + 1] - D.recv_off[k], 0));
+        d->send_base.assign(1, 0);
+        d->recv_base.assign(1, 0);
+        for (int32_t p : d->part_ids) {
+            const DdPart &D = d->plan.parts[p];
+            for (size_t k = 0; k < D.nbr.size(); ++k) {
+                for (int32_t e = D.send_off[k]; e < D.send_off[k + 1]; ++e)
+                    se.push_back(make_int4(D.send_idx[e], D.send_off[k], D.send_off[k + 1] - D.send_off[k], 0));
+                for (int32_t g = D.recv_off[k]; g < D.recv_off[k + 1]; ++g)
+                    re.push_back(make_int4(D.n_own + g, D.recv_off[k], D.recv_off[k + 1] - D.recv_off[k], 0));
+            }
+            d->send_base.push_back((int64_t)se.size());
+            d->recv_base.push_back((int64_t)re.size());
         }
         d->send_ent.alloc(std::max<size_t>(1, se.size()));
         if (!se.empty()) d->send_ent.upload(se.data(), se.size(), d->stream);

@@ -35,6 +35,7 @@ MOF_TIME_SPMV = 4
 MOF_PRECOND_AMG = 8
 MOF_CSV_ROUND_TRIP = 1
 MOF_COORDS_F32 = 32
+MOF_DD_STAGED = 64
 MOF_CSR_A2 = 0
 MOF_CSR_A_LAST = 1
 

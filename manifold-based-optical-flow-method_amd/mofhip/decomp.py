@@ -51,10 +51,12 @@ class DecomposedMesh:
     """One mesh decomposed into ``nparts`` vertex parts (RCB unless ``part``
     is given). Without ``group`` every part lives in this process on
     ``device``; with a torch.distributed ``group`` this rank drives part
-    ``group.rank()`` on ``device`` and ``nparts`` must equal the group size."""
+    ``group.rank()`` on ``device`` and ``nparts`` must equal the group size.
+    ``staged`` (in-process only): exchange through the pack / copy / unpack
+    kernels of the RCCL transport (a one-GPU rehearsal of that path)."""
 
     def __init__(self, coordinates, normals, triangles, areas, nparts: int, device: int = 0,
-                 part=None, group=None, rank=None):
+                 part=None, group=None, rank=None, staged: bool = False):
         coords = np.asarray(coordinates)
         tri = np.asarray(triangles)
         if coords.ndim != 2 or coords.shape[1] != 3 or tri.ndim != 2 or tri.shape[1] != 3:
@@ -73,7 +75,8 @@ class DecomposedMesh:
         if self._part is not None and self._part.shape != (self.N,):
             raise ValueError("part must be (N,)")
         self.device = int(device)
-        flags = L.MOF_GEOM_F32_POINTS if self.f32_points else 0
+        flags = ((L.MOF_GEOM_F32_POINTS if self.f32_points else 0)
+                 | (L.MOF_DD_STAGED if staged else 0))
         h = ctypes.c_void_p()
         pp = L.ptr(self._part) if self._part is not None else None
         if group is None:

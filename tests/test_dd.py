@@ -132,6 +132,25 @@ def test_dd_matches_single_domain(P, random):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,precision", [(3, "mixed"), (8, "f64")])
+def test_dd_staged_transport(P, precision):
+    """The RCCL transport's pack -> exchange -> unpack kernels and V gather
+    (device copies in place of ncclSend/Recv/AllGather) give the same bits
+    as the in-process gather."""
+    p, t, n, a, I = wave_case(n=16, T=5)
+    tk = np.arange(len(I), dtype=np.float64)
+    part = np.random.default_rng(3).integers(0, P, len(p)).astype(np.int32)
+    d1 = DecomposedMesh(p, n, t, a, P, part=part)
+    d2 = DecomposedMesh(p, n, t, a, P, part=part, staged=True)
+    V1, s1 = d1.solve_range(I, tk, 0, 4, 0.01, precision=precision, batch=3)
+    V2, s2 = d2.solve_range(I, tk, 0, 4, 0.01, precision=precision, batch=3)
+    assert s2["failed"] == 0 and s1["iterations"] == s2["iterations"]
+    assert np.array_equal(V1, V2)
+    d1.close()
+    d2.close()
+
+
+@pytest.mark.gpu
 def test_dd_nonconvergence_nan():
     p, t, n, a, I = wave_case(n=12, T=3)
     tk = np.arange(len(I), dtype=np.float64)
