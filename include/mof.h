@@ -72,7 +72,7 @@ typedef struct mof_opts {
     uint32_t precision;    /* MOF_PREC_* */
     uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI | MOF_TIME_SPMV | MOF_PRECOND_AMG */
     int32_t batch;         /* timesteps solved together per launch (0: auto =
-                              64, fewer if device memory is short) */
+                              256, fewer if device memory is short) */
     int32_t max_iter;      /* PCG iterations per inner solve (0: 10000) */
     int32_t max_outer;     /* refinement steps, MOF_PREC_MIXED (0: 10) */
     double rtol;           /* stop at ||f - A V||_2 <= rtol ||f||_2 (0: 1e-8) */

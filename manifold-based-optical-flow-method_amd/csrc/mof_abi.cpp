@@ -393,13 +393,13 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         if (K > 0) {
             int32_t Bmax = o.batch;
             if (Bmax <= 0) {
-                // auto: 64 timesteps per launch sequence, fewer when a quarter
+                // auto: 256 timesteps per launch sequence, fewer when a quarter
                 // of the free device memory cannot hold their workspace
                 // (~700 B per vertex and system with the multigrid levels)
                 size_t free_b = 0, total_b = 0;
                 MOF_HIP(hipMemGetInfo(&free_b, &total_b));
                 const double per_sys = 700.0 * (double)m->N + 1.0;
-                Bmax = (int32_t)std::max(1.0, std::min(64.0, 0.25 * (double)free_b / per_sys));
+                Bmax = (int32_t)std::max(1.0, std::min(256.0, 0.25 * (double)free_b / per_sys));
             }
             const int32_t B = std::min(K, Bmax);
             mof::ensure_workspace(m, B, sp.precision);
@@ -407,6 +407,10 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
             const int64_t N = m->N;
             Events ev;
             mof::prepare_operator(m, lambda, s);
+            // multigrid hierarchy before the first assembly (which writes the
+            // level-0 smoother's bf16 copies)
+            const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && mof::amg_build(m);
+            if (amg) mof::amg_ensure(m, B);
             std::vector<double> dts(B);
             for (int32_t k = k0; k < k1; k += B) {
                 const int32_t nb = std::min(B, k1 - k);
@@ -425,7 +429,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                     I1p = w.Ibuf.p + N * B;
                 }
                 MOF_HIP(hipEventRecord(ev.e[0], s));
-                mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s);
+                mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s, amg);
                 MOF_HIP(hipEventRecord(ev.e[1], s));
                 int32_t outer = 0;
                 st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);

@@ -144,17 +144,12 @@ __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__rest
 // b, summed over its gather list in list order; the diagonal block also gets
 // 1 on dead dofs and stores its 3x3 inverse for the smoother.
 template <int BSF>
-__global__ __launch_bounds__(kWG) void k_galerkin(
-    int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+__device__ __forceinline__ void galerkin_block(
+    int64_t pos, int32_t b, int64_t c_sell_nb, int32_t nC, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
-    // XCD-aware tiles: the B systems of a tile share its gather lists and Q
-    int32_t tile, b;
-    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b)) return;
-    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
-    if (pos >= c_sell_nb) return;
     const int32_t I = c_sell_row[pos];
     if (I >= nC) return;  // rows past n in the last slice
     const float *A = Af + (int64_t)b * f_sell_nb * bstride<BSF>();
@@ -218,6 +213,24 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     }
     st3(Ac, (int64_t)b * c_sell_nb + pos, C);
     if (Ah) st_h9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, C);  // bf16 sweep copy
+}
+
+// XCD-aware tiles: the B systems of a 256-position tile run back to back and
+// share its gather lists and Q in L2. (One coarse slice per workgroup, for L1
+// re-use of the fine blocks, measured equal.)
+template <int BSF>
+__global__ __launch_bounds__(kWG) void k_galerkin(
+    int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
+    const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
+    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
+    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
+    int32_t tile, b;
+    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
+    if (pos >= c_sell_nb) return;
+    galerkin_block<BSF>(pos, b, c_sell_nb, nC, c_sell_row, c_diag, c_dead, gptr, gent, Q, Af, f_sell_nb, Ac, Dh,
+                        Dh22, Ah, Ah22);
 }
 
 constexpr int kMaxCoarse = 128;
@@ -740,6 +753,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.x.alloc(2 * n * B);
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
             G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
+            G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
             G.D0h.alloc(2 * n * B);
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
@@ -763,6 +777,13 @@ void amg_ensure(mof_mesh *m, int32_t B) {
     MOF_HIP(hipStreamSynchronize(s));
 }
 
+AmgBf16 amg_bf16_targets(mof_mesh *m, int32_t B) {
+    AmgDevice &G = *m->amg;
+    MOF_REQUIRE(G.cap >= B, "multigrid storage not sized for the batch");
+    G.bf16_fresh = true;
+    return AmgBf16{reinterpret_cast<uint2 *>(G.A0h.p), reinterpret_cast<uint2 *>(G.D0h.p)};
+}
+
 AmgFine amg_fine(mof_mesh *m) {
     AmgDevice &G = *m->amg;
     AmgFine f;
@@ -780,12 +801,15 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     AmgDevice &G = *m->amg;
     Workspace &w = m->ws;
     const size_t L = G.lv.size();
-    const int64_t nb0 = m->pat.sell_nb() * B;
-    k_to_bf16<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
-        nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
-    const int64_t nd0 = (int64_t)m->N * B;
-    k_to_bf16<<<dim3((unsigned)((nd0 + kWG - 1) / kWG)), kWG, 0, s>>>(
-        nd0, reinterpret_cast<const float4 *>(w.dinv32.p), reinterpret_cast<uint2 *>(G.D0h.p));
+    if (!G.bf16_fresh) {
+        const int64_t nb0 = m->pat.sell_nb() * B;
+        k_to_bf16<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
+            nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
+        const int64_t nd0 = (int64_t)m->N * B;
+        k_to_bf16<<<dim3((unsigned)((nd0 + kWG - 1) / kWG)), kWG, 0, s>>>(
+            nd0, reinterpret_cast<const float4 *>(w.dinv32.p), reinterpret_cast<uint2 *>(G.D0h.p));
+    }
+    G.bf16_fresh = false;
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
         if (l == 0)

@@ -9,6 +9,7 @@
 //
 // All per-timestep accumulation is a gather in triangle order over the
 // pre-built contribution lists (mof_pattern.cpp): deterministic, no atomics.
+#include "mof_amg.h"
 #include "mof_internal.h"
 #include "mof_rowkern.h"
 
@@ -330,15 +331,20 @@ __global__ __launch_bounds__(kWG) void k_assemble_blocks(
 // Mixed-precision solve path: A32 = a1 + lambda a2 folded in fp32 from the
 // fp32 copy of u (half the gathered bytes of the fp64 fold; the inner PCG
 // runs on fp32 A anyway and the fp64 refinement uses the exact operator).
-// The diagonal slot still folds f in fp64 from the f terms (bit-identical
-// to the reference's f) and writes the fp32 2x2 block-Jacobi inverse.
+// The diagonal slot also folds f in fp64 from the f terms (bit-identical to
+// the reference's f: its own-corner terms in triangle order; folding them in
+// the main loop measured 0.5 % slower) and writes the 2x2 block-Jacobi
+// inverse. With the multigrid preconditioner (Ah != null)
+// the bf16 copies of A and D^-1 the level-0 smoother sweeps read are written
+// here too (D^-1 then only in bf16: the PCG applies the V-cycle, not D^-1).
 __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     int64_t sell_nb, int32_t N, int32_t M, int32_t B, const int32_t *__restrict__ sell_blk,
     const int32_t *__restrict__ blk_row, const int32_t *__restrict__ vcol,
     const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
     const float *__restrict__ w12, const float *__restrict__ a2s, const float *__restrict__ u,
     const double *__restrict__ fc, int block_jacobi, float *__restrict__ A,
-    float *__restrict__ dinv32, double *__restrict__ rhs) {
+    float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
+    uint2 *__restrict__ Dh) {
     int32_t tile, b;
     if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
@@ -370,7 +376,8 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
         }
 #pragma unroll
         for (int q = 0; q < U; ++q) {
-            const float integ = (c + q < c1) ? (diag ? 2.f * wq[q] : wq[q]) : 0.f;
+            const bool on = c + q < c1;
+            const float integ = on ? (diag ? 2.f * wq[q] : wq[q]) : 0.f;
             acc[0] += ua[q].x * uv[q].x * integ;
             acc[1] += ua[q].x * uv[q].y * integ;
             acc[2] += ua[q].y * uv[q].x * integ;
@@ -379,7 +386,9 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     }
     const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
     const float Av[4] = {acc[0] + s4.x, acc[1] + s4.y, acc[2] + s4.z, acc[3] + s4.w};
-    reinterpret_cast<float4 *>(A)[(int64_t)b * sell_nb + pos] = make_float4(Av[0], Av[1], Av[2], Av[3]);
+    const int64_t q = (int64_t)b * sell_nb + pos;
+    reinterpret_cast<float4 *>(A)[q] = make_float4(Av[0], Av[1], Av[2], Av[3]);
+    if (Ah) Ah[q] = bf16x4(Av[0], Av[1], Av[2], Av[3]);
     if (!diag) return;
     // f_i in fp64, in the reference's triangle order
     const double *fb = fc + 6 * (int64_t)b * (M + 1);
@@ -401,8 +410,11 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
         inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
     }
     const int64_t vi = (int64_t)b * N + i;
-    reinterpret_cast<float4 *>(dinv32)[vi] =
-        make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+    if (Dh)
+        Dh[vi] = bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+    else
+        reinterpret_cast<float4 *>(dinv32)[vi] =
+            make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
     *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
 }
 
@@ -589,7 +601,7 @@ void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
 }
 
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
-                     bool block_jacobi, uint32_t precision, hipStream_t s) {
+                     bool block_jacobi, uint32_t precision, hipStream_t s, bool amg) {
     Workspace &w = m->ws;
     check_mesh_arrays(m);
     const size_t nbs = (size_t)m->pat.sell_nb(), mu = 6 * ((size_t)m->M + 1) * B;
@@ -604,10 +616,13 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B));
     const int bj = block_jacobi ? 1 : 0;
+    // multigrid: the level-0 smoother's bf16 operator and D^-1 come from here
+    AmgBf16 bf{nullptr, nullptr};
+    if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
     if (precision == MOF_PREC_MIXED)
         k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                             m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,
-                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p);
+                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h);
     else
         k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,

@@ -179,8 +179,10 @@ void launch_a2(mof_mesh *m);
 void prepare_operator(mof_mesh *m, double lambda, hipStream_t s);
 // per-timestep terms of B systems: u, f, D^-1. I0 / I1 rows are device
 // pointers (row b at +b*ldI).
+// amg: the multigrid preconditioner's hierarchy is built and sized for B
+// (amg_build + amg_ensure): also write the level-0 bf16 smoother copies.
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
-                     bool block_jacobi, uint32_t precision, hipStream_t s);
+                     bool block_jacobi, uint32_t precision, hipStream_t s, bool amg = false);
 // bit-exact A (SELL, fp64) and f of one timestep into m->Aexp / m->fexp
 void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
                             hipStream_t s);
@@ -229,6 +231,12 @@ struct AmgFine {
     float omega;
 };
 AmgFine amg_fine(mof_mesh *m);
+// bf16 level-0 A / D^-1 of the next batch, written by the assembly (marks
+// them fresh, so amg_setup_batch does not convert A32 again)
+struct AmgBf16 {
+    uint2 *A0h, *D0h;
+};
+AmgBf16 amg_bf16_targets(mof_mesh *m, int32_t B);
 void amg_destroy(AmgDevice *g);
 
 int32_t amg_levels(const mof_mesh *m);
