@@ -151,6 +151,27 @@ def test_dd_staged_transport(P, precision):
 
 
 @pytest.mark.gpu
+@pytest.mark.slow
+def test_dd_full_size_c3():
+    """C3 (163,842 vertices) over 8 RCB parts: every system meets the fp64
+    residual bar, V agrees with the single-domain solve to the solver
+    tolerance, and the iteration counts are the single-domain ones (block
+    Jacobi is pointwise)."""
+    p, t, n, a = synth.mesh_for_config("C3")
+    I = synth.travelling_wave(p, 5)
+    tk = np.arange(len(I), dtype=np.float64)
+    d = DecomposedMesh(p, n, t, a, 8)
+    V2, s2 = d.solve_range(I, tk, 0, 4, 0.01, precision="mixed")
+    d.close()
+    ref = DeviceMesh(p, n, t, a)
+    V1, s1 = ref.solve_range(I, tk, 0, 4, 0.01, precision="mixed")
+    ref.close()
+    assert s2["failed"] == 0 and s2["max_rel_residual"] <= 1e-8
+    assert abs(s2["iterations"] - s1["iterations"]) <= 8
+    assert np.abs(V2 - V1).max() <= 1e-6
+
+
+@pytest.mark.gpu
 def test_dd_nonconvergence_nan():
     p, t, n, a, I = wave_case(n=12, T=3)
     tk = np.arange(len(I), dtype=np.float64)
