@@ -8,9 +8,10 @@ parts (RCB), PCG in lockstep with a halo exchange per iteration.
 
 Without torchrun all P parts run in this process on GPU 0 (in-process
 transport); the line then also times the single-domain solve of the same
-systems with the same solver (mixed precision, 2x2 block-Jacobi PCG) on the
+systems with the same solver (mixed precision; multigrid or 2x2 block-Jacobi PCG) on the
 same GPU, so ``dd_overhead`` is the cost of the decomposition itself (more,
-smaller launches + the halo gathers). Under torchrun each rank drives its own
+smaller launches + the halo gathers; with ``--precond amg`` also the weaker
+block-Jacobi-over-parts multigrid against the single-domain one). Under torchrun each rank drives its own
 part on its own GPU and the halo / CG scalars travel over RCCL.
 
 One step = B timesteps (assembly, PCG to 1e-8, V in HBM), inputs resident in
@@ -38,6 +39,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--precision", default="mixed", choices=["mixed", "f64"])
+    ap.add_argument("--precond", default="jacobi", choices=["jacobi", "amg"],
+                    help="amg: a V-cycle per part (mixed precision only; fewer iterations, "
+                         "more launches per iteration)")
     ap.add_argument("--no-single", action="store_true", help="skip the single-domain reference")
     args = ap.parse_args()
     from mofhip.dist import rank_env
@@ -66,7 +70,7 @@ def main():
     I_dev = torch.from_numpy(I_host).to(dev)
     V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(total * B + 1, dtype=np.float64)
-    opts = dict(precision=args.precision, batch=B, precond="jacobi")
+    opts = dict(precision=args.precision, batch=B, precond=args.precond)
 
     def run(solver, s):
         return solver.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), total * B + 1, tk, s * B,
@@ -114,7 +118,8 @@ def main():
             "data": "synthetic travelling wave sin(3 phi - 0.3 k), dt = 1, lambda = 0.01",
             "config": {"workload": "%s, %d vertices, %d parts (RCB), %s" % (
                 args.config, N, P, "RCCL, one part per GPU" if world > 1 else "in-process on 1 GPU"),
-                "timesteps_per_step": B, "precision": args.precision, "precond": "block jacobi"},
+                "timesteps_per_step": B, "precision": args.precision,
+                "precond": "multigrid per part" if args.precond == "amg" else "block jacobi"},
             "decomposition": {"max_owned": info["max_owned"], "ghost_rows": info["ghost_rows"],
                               "halo_fraction": round(info["ghost_rows"] / N, 4),
                               "max_neighbours": info["max_neighbours"], "setup_s": round(setup_s, 2)},

@@ -237,7 +237,9 @@ int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int
  * exchanged before every product, the CG scalars are reduced over all parts
  * in one fixed order (every part takes the same decisions; V is deterministic
  * for a given partition and within the solve tolerance of mof_solve_range).
- * Preconditioner: 2x2 block Jacobi (MOF_PRECOND_AMG is rejected). */
+ * Preconditioner: 2x2 block Jacobi, or with MOF_PRECOND_AMG (mixed precision)
+ * block Jacobi over the parts with each part's multigrid V-cycle on its owned
+ * rows (ghost rows decoupled: the owned rows' Dirichlet problem). */
 typedef struct mof_dd mof_dd;
 
 typedef struct mof_dd_info {

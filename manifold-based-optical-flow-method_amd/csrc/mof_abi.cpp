@@ -108,6 +108,7 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
                 const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
                 const int32_t *perm_in, const int32_t *tri_ids) {
     m->N = N;
+    m->n_own = N;
     m->M = M;
     m->device = device;
     m->flags = flags;

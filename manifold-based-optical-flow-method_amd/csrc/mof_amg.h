@@ -11,6 +11,10 @@ struct AmgParams {
     int32_t max_levels = 10;
     int32_t max_coarse_dofs = 128;  // coarsest level: dense inverse in LDS (fp64), one workgroup per system
     float omega = 0.85f;            // damped block-Jacobi smoother (1.0 diverges on irregular meshes)
+    // level-0 rows >= nown are a decomposed part's ghosts: the Galerkin lists
+    // use an identity block on their diagonal and zero for every coupling
+    // that touches them (the Dirichlet problem of the owned rows); -1: none
+    int32_t nown = -1;
 };
 
 // One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser

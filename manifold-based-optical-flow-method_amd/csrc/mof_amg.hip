@@ -170,7 +170,14 @@ __device__ __forceinline__ void galerkin_block(
         float a[U][BSF][BSF], qi[U][BSF][3], qj[U][BSF][3];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            ldm<BSF>(A, fp[u], a[u]);
+            // fp -1 / -2: a decomposed part's ghost block, identity / zero
+            ldm<BSF>(A, max(fp[u], 0), a[u]);
+            if (fp[u] < 0) {
+#pragma unroll
+                for (int r = 0; r < BSF; ++r)
+#pragma unroll
+                    for (int k = 0; k < BSF; ++k) a[u][r][k] = (fp[u] == -1 && r == k) ? 1.f : 0.f;
+            }
 #pragma unroll
             for (int k = 0; k < BSF; ++k)
 #pragma unroll
@@ -628,7 +635,8 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
                                                const float *__restrict__ rv,
                                                const float *__restrict__ xv, float omega,
                                                const int32_t *__restrict__ sysi,
-                                               float *__restrict__ zv, double *__restrict__ part) {
+                                               float *__restrict__ zv, double *__restrict__ part,
+                                               RedArgs rd) {
     __shared__ double lds[8];
     int32_t rb, b;
     if (!xcd_map(nblk, B, rb, b) || retired(sysi, b)) return;
@@ -646,11 +654,11 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
         const float z0 = xi.x + omega * ds.x;
         const float z1 = xi.y + omega * ds.y;
         reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
-        rz += (double)ri.x * z0 + (double)ri.y * z1;
+        if (i < rd.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
     }
     double v[1] = {rz};
     block_sum<1>(v, lds);
-    if (threadIdx.x == 0) part[2 * ((int64_t)b * nblk + rb)] = v[0];
+    if (threadIdx.x == 0) part[2 * (((int64_t)rd.part * B + b) * rd.nmax + rb)] = v[0];
 }
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
@@ -672,6 +680,7 @@ MatH level0_mat(mof_mesh *m) {
 bool amg_build(mof_mesh *m) {
     AmgParams prm;
     if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knob
+    if (m->n_own < m->N) prm.nown = m->n_own;
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
     AmgDevice &G = *m->amg;
@@ -852,7 +861,7 @@ Lvl level_view(const AmgDevLevel &D) {
 }
 
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part_slot, int32_t nblk,
-                hipStream_t s) {
+                const RedArgs &rd, hipStream_t s) {
     AmgDevice &G = *m->amg;
     Workspace &w = m->ws;
     const int32_t L = (int32_t)G.lv.size();
@@ -891,7 +900,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         if (l == 0) {
             k_prolong<2><<<grid2(v[0].n, B), kWG, 0, s>>>(v[0], v[1], sysi);
             k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, reinterpret_cast<const uint2 *>(G.D0h.p), r0,
-                                       v[0].x, om, sysi, z0, part_slot);
+                                       v[0].x, om, sysi, z0, part_slot, rd);
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
             k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om, sysi);

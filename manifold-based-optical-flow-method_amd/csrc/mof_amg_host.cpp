@@ -246,7 +246,9 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
                 for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) {
                     const int32_t p = cblk_of_fine[q];
                     const int32_t k = fill[p]++;
-                    by_block[3 * k + 0] = fine_pos[q];
+                    const bool ghost = H.levels.size() == 1 && prm.nown >= 0 &&
+                                       (i >= prm.nown || F.vcol[q] >= prm.nown);
+                    by_block[3 * k + 0] = ghost ? (F.vcol[q] == i ? -1 : -2) : fine_pos[q];
                     by_block[3 * k + 1] = i;
                     by_block[3 * k + 2] = F.vcol[q];
                 }

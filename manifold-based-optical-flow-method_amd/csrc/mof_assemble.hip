@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     const float *__restrict__ w12, const float *__restrict__ a2s, const float *__restrict__ u,
     const double *__restrict__ fc, int block_jacobi, float *__restrict__ A,
     float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
-    uint2 *__restrict__ Dh) {
+    uint2 *__restrict__ Dh, int32_t nown) {
     int32_t tile, b;
     if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
@@ -388,7 +388,12 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     const float Av[4] = {acc[0] + s4.x, acc[1] + s4.y, acc[2] + s4.z, acc[3] + s4.w};
     const int64_t q = (int64_t)b * sell_nb + pos;
     reinterpret_cast<float4 *>(A)[q] = make_float4(Av[0], Av[1], Av[2], Av[3]);
-    if (Ah) Ah[q] = bf16x4(Av[0], Av[1], Av[2], Av[3]);
+    if (Ah) {
+        // a decomposed part's ghost rows: identity rows, no coupling (the
+        // smoother and coarse levels see the owned rows' Dirichlet problem)
+        const bool g = i >= nown || vcol[p] >= nown;
+        Ah[q] = g ? bf16x4(diag ? 1.f : 0.f, 0.f, 0.f, diag ? 1.f : 0.f) : bf16x4(Av[0], Av[1], Av[2], Av[3]);
+    }
     if (!diag) return;
     // f_i in fp64, in the reference's triangle order
     const double *fb = fc + 6 * (int64_t)b * (M + 1);
@@ -411,7 +416,8 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     }
     const int64_t vi = (int64_t)b * N + i;
     if (Dh)
-        Dh[vi] = bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+        Dh[vi] = i >= nown ? bf16x4(1.f, 0.f, 0.f, 1.f)
+                           : bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
     else
         reinterpret_cast<float4 *>(dinv32)[vi] =
             make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
@@ -622,7 +628,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (precision == MOF_PREC_MIXED)
         k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                             m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,
-                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h);
+                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own);
     else
         k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,

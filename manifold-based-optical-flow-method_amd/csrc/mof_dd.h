@@ -56,12 +56,6 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
                 const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
                 const int32_t *perm, const int32_t *tri_ids);
 
-// Cross-part reduction layout of the PCG kernels: partial record of
-// (part, system b, workgroup w) at ((part * B + b) * nmax + w) * NV.
-struct RedArgs {
-    int32_t P = 1, part = 0, nmax = 0, nown = 0;
-};
-
 struct RcclApi;  // mof_dd.hip
 
 }  // namespace mof

@@ -408,6 +408,7 @@ void dd_setup(mof_dd *d, const double *xyz, const double *nrm, const int32_t *tr
         // the folds; I is gathered by the caller's (global) vertex ids
         mesh_build(m, lx.data(), ln.data(), lt.data(), la.data(), nl, ml, d->device, d->flags, ident.data(),
                    gt.data());
+        m->n_own = D.n_own;  // ghost rows: decoupled in the part's multigrid cycle
         d->own_off.push_back((int64_t)own.size());
         own.insert(own.end(), D.l2g.begin(), D.l2g.begin() + D.n_own);
     }
@@ -624,11 +625,11 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
             o = *opts;
         }
         MOF_REQUIRE(o.precision == MOF_PREC_F64 || o.precision == MOF_PREC_MIXED, "unknown precision");
-        MOF_REQUIRE(!(o.flags & MOF_PRECOND_AMG), "the decomposed solve uses block Jacobi (no MOF_PRECOND_AMG)");
         SolveParams sp;
         sp.precision = o.precision;
-        sp.amg = false;
-        sp.block_jacobi = !(o.flags & MOF_NO_BLOCK_JACOBI);
+        sp.amg = (o.flags & MOF_PRECOND_AMG) != 0;
+        MOF_REQUIRE(!sp.amg || o.precision == MOF_PREC_MIXED, "MOF_PRECOND_AMG needs MOF_PREC_MIXED");
+        sp.block_jacobi = sp.amg || !(o.flags & MOF_NO_BLOCK_JACOBI);
         sp.time_spmv = false;
         sp.max_iter = o.max_iter > 0 ? o.max_iter : 10000;
         sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
@@ -657,6 +658,12 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                 Vbuf.alloc(2 * (size_t)N * B);
             }
             for (mof_mesh *m : d->parts) prepare_operator(m, lambda, s);
+            // subdomain multigrid (every part, or none): built before the first
+            // assembly, which writes the level-0 smoother copies
+            bool amg = sp.amg;
+            for (mof_mesh *m : d->parts) amg = amg && amg_build(m);
+            if (amg)
+                for (mof_mesh *m : d->parts) amg_ensure(m, B);
             hipEvent_t ev[3];
             for (auto &e : ev) MOF_HIP(hipEventCreate(&e));
             std::vector<double> dts(B);
@@ -680,7 +687,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                     }
                     MOF_HIP(hipEventRecord(ev[0], s));
                     for (mof_mesh *m : d->parts)
-                        launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s);
+                        launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s, amg);
                     MOF_HIP(hipEventRecord(ev[1], s));
                     int32_t outer = 0;
                     st.iterations += solve_batch_dd(d, nb, sp, s, &outer, &st.max_iterations);

@@ -129,11 +129,21 @@ constexpr int kSysStride = 8;
 
 struct AmgDevice;  // mof_amg.h
 
+// Cross-part reduction layout of the PCG kernels: partial record of
+// (part, system b, workgroup w) at ((part * B + b) * nmax + w) * NV; rows
+// >= nown (a decomposed part's ghosts) are computed but never summed.
+struct RedArgs {
+    int32_t P = 1, part = 0, nmax = 0, nown = 0;
+};
+
 }  // namespace mof
 
 // The opaque handle of the C ABI.
 struct mof_mesh {
     int32_t N = 0, M = 0, device = 0;
+    // rows [n_own, N) are a decomposed part's ghosts (mof_dd.h): the
+    // multigrid preconditioner decouples them (identity rows); N otherwise
+    int32_t n_own = 0;
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
     mof::Pattern pat;
@@ -223,7 +233,7 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s);  // Galerkin + coar
 // z = V-cycle(r) on the fp32 inner vectors; writes partial r.z (component 0)
 // into the part_rzrr slot `part_slot`
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_slot, int32_t nblk,
-                hipStream_t s);
+                const RedArgs &rd, hipStream_t s);
 // level-0 smoother data the PCG update / init write the pre-smoothing with
 struct AmgFine {
     const void *D0h;  // bf16 2x2 D^-1 [B][N] (uint2 each)

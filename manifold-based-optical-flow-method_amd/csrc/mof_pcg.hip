@@ -185,7 +185,10 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
         if (i >= a.N) break;
         const int64_t vi = (int64_t)b * a.N + i;
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
-        const V r0 = (V)f.x, r1 = (V)f.y;
+        // a decomposed part's ghost rows carry r = 0 (the multigrid cycle
+        // reads every local row; the CG sums skip them anyway)
+        const bool own = i < a.red.nown;
+        const V r0 = own ? (V)f.x : (V)0, r1 = own ? (V)f.y : (V)0;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = V2{r0, r1};
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = V2{(V)0, (V)0};
         if (!a.ext) {
@@ -315,8 +318,8 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
         V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
         xi.x += alpha * pi.x;
         xi.y += alpha * pi.y;
-        ri.x -= alpha * qi.x;
-        ri.y -= alpha * qi.y;
+        ri.x = i < a.red.nown ? ri.x - alpha * qi.x : (V)0;
+        ri.y = i < a.red.nown ? ri.y - alpha * qi.y : (V)0;
         *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
         if (!a.ext) {
@@ -520,7 +523,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
     // z = M^-1 r for the external preconditioner, r.z into slot `slot`
     auto precond = [&](int32_t slot) {
-        if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, s);
+        if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s);
     };
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B));
@@ -740,7 +743,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
 namespace {
 
 template <typename V>
-std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, uint32_t precision) {
+std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, bool amg) {
     std::vector<PcgArgs<V>> args;
     for (size_t l = 0; l < d->parts.size(); ++l) {
         mof_mesh *m = d->parts[l];
@@ -753,27 +756,49 @@ std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, uint32_t precision) {
         a.part_pq = d->part_pq.p;
         a.part_rzrr = d->part_rzrr.p;
         a.red = RedArgs{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
+        if constexpr (sizeof(V) == 4) {
+            if (amg) {  // subdomain multigrid: each part's cycle on its owned rows
+                const AmgFine f = amg_fine(m);
+                a.ext = 1;
+                a.x0 = f.x0;
+                a.omega = f.omega;
+                a.dh = static_cast<const uint2 *>(f.D0h);
+            }
+        }
         args.push_back(a);
     }
-    (void)precision;
     return args;
 }
 
 template <typename V>
 int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_iter, hipStream_t s,
-               int32_t *max_iters, int32_t *hint, uint32_t precision) {
-    std::vector<PcgArgs<V>> args = dd_args<V>(d, B, precision);
+               int32_t *max_iters, int32_t *hint, bool amg) {
+    std::vector<PcgArgs<V>> args = dd_args<V>(d, B, amg);
     const size_t L = args.size();
     mof_mesh *m0 = d->parts[0];
     const int64_t rec = (int64_t)B * d->nmax;  // records of one part
     const int64_t ps = (int64_t)d->P * rec * 2;
+    // z = M^-1 r per part (block Jacobi over the parts, a V-cycle inside
+    // each), r.z into slot `slot`; then the slot's records are complete
+    auto precond = [&](int32_t slot) {
+        if constexpr (sizeof(V) == 4) {
+            if (amg)
+                for (size_t l = 0; l < L; ++l)
+                    amg_vcycle(d->parts[l], B, args[l].r, args[l].z, d->part_rzrr.p + slot * ps,
+                               d->parts[l]->ws.nblk, args[l].red, s);
+        }
+        dd_sync_partials(d, d->part_rzrr.p + slot * ps, 2 * rec, s);
+    };
     for (size_t l = 0; l < L; ++l) {
         Workspace &w = d->parts[l]->ws;
         const double *rhs = first_outer ? w.rhs.p : w.r64.p;
         k_pcg_init<V><<<dim3((unsigned)w.nblk, (unsigned)B), kWG, 0, s>>>(args[l], rhs);
     }
     dd_sync_partials(d, d->part_rzrr.p, 2 * rec, s);
+    // the tolerance step resets the convergence word the cycle's kernels
+    // check, so it runs before the first cycle
     for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol);
+    if (amg) precond(0);
     MOF_HIP(hipGetLastError());
     std::vector<int32_t> was_active(B);
     for (int32_t b = 0; b < B; ++b) was_active[b] = m0->h_sysi[b * kSysStride + SI_ACTIVE];
@@ -797,7 +822,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
             spmv(it == 0, it);
             for (size_t l = 0; l < L; ++l)
                 k_pcg_update<V><<<dim3((unsigned)d->parts[l]->ws.nblk, (unsigned)B), kWG, 0, s>>>(args[l], it);
-            dd_sync_partials(d, d->part_rzrr.p + ((it + 1) & 1) * ps, 2 * rec, s);
+            precond((it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m0, B, s);
@@ -849,15 +874,22 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
         si[SI_CONV] = -1;
     }
     if (m0->iter_hint.size() < 2 * 16) m0->iter_hint.assign(2 * 16, 0);
+    bool amg = sp.amg && sp.precision == MOF_PREC_MIXED;
+    for (size_t l = 0; l < L && amg; ++l) amg = amg_build(d->parts[l]);
+    if (amg)
+        for (size_t l = 0; l < L; ++l) {
+            amg_ensure(d->parts[l], B);
+            amg_setup_batch(d->parts[l], B, s);
+        }
     int64_t iters = 0;
     int32_t o = 0;
     for (; o < sp.max_outer; ++o) {
         if (sp.precision == MOF_PREC_MIXED)
             iters += pcg_dd<float>(d, B, o == 0, sp.inner_rtol, sp.max_iter, s, max_iters,
-                                   &m0->iter_hint[16 + std::min(o, 15)], sp.precision);
+                                   &m0->iter_hint[16 + std::min(o, 15)], amg);
         else
             iters += pcg_dd<double>(d, B, o == 0, o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s,
-                                    max_iters, &m0->iter_hint[std::min(o, 15)], sp.precision);
+                                    max_iters, &m0->iter_hint[std::min(o, 15)], false);
         for (size_t l = 0; l < L; ++l) {
             mof_mesh *m = d->parts[l];
             Workspace &w = m->ws;

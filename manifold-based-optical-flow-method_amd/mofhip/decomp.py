@@ -119,7 +119,8 @@ class DecomposedMesh:
 
     def solve_range(self, I, t_k, k0, k1, lambda_, I2=None, raise_on_noconv=False, **opts):
         """V for k in [k0, k1): (k1-k0, 2N) float64 host array, plus stats
-        (options as :meth:`DeviceMesh.make_opts`, precond "jacobi" only)."""
+        (options as :meth:`DeviceMesh.make_opts`; precond "amg" = a multigrid
+        V-cycle per part on its owned rows, block Jacobi across the parts)."""
         I = _f64(I)
         I2a = I if I2 is None else _f64(I2)
         tk = _f64(t_k)
