@@ -108,7 +108,7 @@ template <typename V>
 __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
                                          const V *__restrict__ x, V &y0, V &y1) {
     using V2 = typename VT<V>::V2;
-    constexpr int U = sizeof(V) == 4 ? 8 : 4;
+    constexpr int U = 8;  // fp64 too: 525 vs 536 us per C2 launch with 4
     const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
