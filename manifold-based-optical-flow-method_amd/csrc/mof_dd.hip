@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <type_traits>
 
@@ -51,6 +52,8 @@ namespace {
 RcclApi *rccl_open() {
     static RcclApi api;
     static bool tried = false;
+    static std::mutex mu;  // handles may be created from several host threads
+    std::lock_guard<std::mutex> lock(mu);
     if (api.h) return &api;
     MOF_REQUIRE(!tried, "librccl could not be loaded");
     tried = true;
