@@ -184,6 +184,20 @@ int mof_singularities(int32_t device, const void *coords, const int32_t *triangl
                       void *stream, double *vmax, uint8_t *vertex_flag, uint8_t *triangle_flag,
                       double *lam_mu);
 
+/* mof_singularities with the reference's list-shaped result
+ * (find_singularity_point.py:156-189 returns the zero vertices and the
+ * triangles holding a zero, not dense flags): per field k, n_vert[k] zero
+ * vertices and n_tri[k] zero triangles; vert_idx / tri_idx / lam_mu (2 per
+ * triangle) hold them field-major, ascending index within a field (compacted
+ * on the device, so only the lists cross PCIe). cap = capacity of each list
+ * (entries over all fields); totals[0..1] receives the vertex / triangle
+ * counts, and MOF_E_ARG is returned when either exceeds cap. Host outputs;
+ * coords / triangles / V_coord host, or device with MOF_IO_DEVICE. */
+int mof_singularities_compact(int32_t device, const void *coords, const int32_t *triangles, int32_t N,
+                              int32_t M, const double *V_coord, int32_t K, double eps, uint32_t flags,
+                              void *stream, int64_t cap, int64_t *totals, double *vmax, int64_t *n_vert,
+                              int32_t *vert_idx, int64_t *n_tri, int32_t *tri_idx, double *lam_mu);
+
 /* ---- the S3 CSV files (host threads, no device) ------
  * mof_csv_write replaces the write of reshape_and_save_data
  * (compute_optical_flow.py:314-320, pd.DataFrame(data).to_csv(path)):

@@ -549,6 +549,94 @@ int mof_singularities(int32_t device, const void *coords, const int32_t *triangl
     });
 }
 
+int mof_singularities_compact(int32_t device, const void *coords, const int32_t *triangles, int32_t N,
+                              int32_t M, const double *V_coord, int32_t K, double eps, uint32_t flags, void *stream,
+                              int64_t cap, int64_t *totals, double *vmax, int64_t *n_vert, int32_t *vert_idx,
+                              int64_t *n_tri, int32_t *tri_idx, double *lam_mu) {
+    return guarded([&] {
+        MOF_REQUIRE(coords && V_coord && totals && vmax && n_vert && n_tri && N > 0 && M >= 0 && K >= 0 &&
+                        cap >= 0,
+                    "bad arguments");
+        MOF_REQUIRE(M == 0 || triangles, "NULL triangles");
+        MOF_REQUIRE(cap == 0 || (vert_idx && tri_idx && lam_mu), "NULL output list");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DeviceGuard dg(device);
+        totals[0] = totals[1] = 0;
+        for (int32_t k = 0; k < K; ++k) n_vert[k] = n_tri[k] = 0;
+        if (K == 0) return;
+        const bool dev_io = (flags & MOF_IO_DEVICE) != 0;
+        if (!dev_io)
+            for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
+                MOF_REQUIRE(triangles[q] >= 0 && triangles[q] < N, "triangle index out of range");
+        hipStream_t s = (hipStream_t)stream;
+        const bool f32 = (flags & MOF_COORDS_F32) != 0;
+        const size_t cb = 3 * (size_t)N * (f32 ? sizeof(float) : sizeof(double));
+        const size_t nk = (size_t)N * K;
+        mof::DevArray<uint8_t> dc, dvf;
+        mof::DevArray<int32_t> dt;
+        mof::DevArray<double> dV, dmax;
+        mof::DevArray<unsigned long long> dcnt;
+        mof::DevArray<int2> dvr, dtr;
+        mof::DevArray<double2> dlm;
+        const void *pc = coords;
+        const int32_t *pt = triangles;
+        const double *pV = V_coord;
+        if (!dev_io) {
+            dc.alloc(cb);
+            MOF_HIP(hipMemcpyAsync(dc.p, coords, cb, hipMemcpyHostToDevice, s));
+            dt.alloc(3 * (size_t)M);
+            if (M) dt.upload(triangles, 3 * (size_t)M, s);
+            dV.alloc(3 * nk);
+            dV.upload(V_coord, 3 * nk, s);
+            pc = dc.p;
+            pt = dt.p;
+            pV = dV.p;
+        }
+        dmax.alloc(K);
+        dvf.alloc(nk);
+        dcnt.alloc(2);
+        dvr.alloc(std::max<int64_t>(1, cap));
+        dtr.alloc(std::max<int64_t>(1, cap));
+        dlm.alloc(std::max<int64_t>(1, cap));
+        mof::launch_singularities_compact(N, M, K, pc, f32, pt, pV, eps, dmax.p, dvf.p, dcnt.p, cap, dvr.p, dtr.p,
+                                          dlm.p, s);
+        unsigned long long cnt[2] = {0, 0};
+        MOF_HIP(hipMemcpyAsync(cnt, dcnt.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipMemcpyAsync(vmax, dmax.p, K * sizeof(double), hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipStreamSynchronize(s));
+        totals[0] = (int64_t)cnt[0];
+        totals[1] = (int64_t)cnt[1];
+        MOF_REQUIRE(totals[0] <= cap && totals[1] <= cap,
+                    "record capacity too small (totals holds the vertex / triangle record counts needed)");
+        std::vector<int2> vr(cnt[0]), tr(cnt[1]);
+        std::vector<double2> lm(cnt[1]);
+        if (cnt[0]) MOF_HIP(hipMemcpyAsync(vr.data(), dvr.p, cnt[0] * sizeof(int2), hipMemcpyDeviceToHost, s));
+        if (cnt[1]) {
+            MOF_HIP(hipMemcpyAsync(tr.data(), dtr.p, cnt[1] * sizeof(int2), hipMemcpyDeviceToHost, s));
+            MOF_HIP(hipMemcpyAsync(lm.data(), dlm.p, cnt[1] * sizeof(double2), hipMemcpyDeviceToHost, s));
+        }
+        MOF_HIP(hipStreamSynchronize(s));
+        // records arrive in atomic order: field-major, ascending index
+        auto key = [](const int2 &r) { return ((int64_t)r.x << 32) | (uint32_t)r.y; };
+        std::sort(vr.begin(), vr.end(), [&](const int2 &a, const int2 &b) { return key(a) < key(b); });
+        for (size_t q = 0; q < vr.size(); ++q) {
+            vert_idx[q] = vr[q].y;
+            n_vert[vr[q].x]++;
+        }
+        std::vector<size_t> ord(tr.size());
+        for (size_t q = 0; q < ord.size(); ++q) ord[q] = q;
+        std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return key(tr[a]) < key(tr[b]); });
+        for (size_t q = 0; q < ord.size(); ++q) {
+            tri_idx[q] = tr[ord[q]].y;
+            lam_mu[2 * q] = lm[ord[q]].x;
+            lam_mu[2 * q + 1] = lm[ord[q]].y;
+            n_tri[tr[ord[q]].x]++;
+        }
+    });
+}
+
 int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
                   int32_t *level_nodes, double *qtq_err) {
     return guarded([&] {

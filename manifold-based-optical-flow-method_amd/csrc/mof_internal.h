@@ -201,6 +201,11 @@ void launch_to_planar(mof_mesh *m, int32_t B, double *V, hipStream_t s);  // V i
 void launch_singularities(int32_t N, int32_t M, int32_t K, const void *coords, bool f32, const int32_t *tri,
                           const double *V, double eps, double *vmax, uint8_t *vflag, uint8_t *tflag,
                           double *lam_mu, hipStream_t s);
+// the same with the flagged vertices / triangles appended as records (SingList)
+void launch_singularities_compact(int32_t N, int32_t M, int32_t K, const void *coords, bool f32,
+                                  const int32_t *tri, const double *V, double eps, double *vmax, uint8_t *vflag,
+                                  unsigned long long *cnt, int64_t cap, int2 *vrec, int2 *trec, double2 *tlm,
+                                  hipStream_t s);
 void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double *V, double *Vc,
                              double *speed, hipStream_t s);
 

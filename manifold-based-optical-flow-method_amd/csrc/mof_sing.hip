@@ -119,20 +119,41 @@ __device__ void lstsq32(const double c0[3], const double c1[3], const double b[3
     }
 }
 
-template <bool F32>
+// Compact output (CMP): flagged vertices / triangles are appended as
+// (field, index[, lam, mu]) records at an atomic cursor (order fixed later on
+// the host by sorting); the dense flags are then not written for triangles.
+struct SingList {
+    unsigned long long *cnt;  // [0] vertex records, [1] triangle records
+    int64_t cap;
+    int2 *vrec;               // (field, vertex)
+    int2 *trec;               // (field, triangle)
+    double2 *tlm;             // (lam, mu) of each triangle record
+};
+
+__global__ void k_sing_vlist(int32_t N, const uint8_t *__restrict__ vflag, SingList L) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t k = blockIdx.y;
+    if (i >= N || !vflag[(int64_t)k * N + i]) return;
+    const unsigned long long q = atomicAdd(L.cnt, 1ull);
+    if ((int64_t)q < L.cap) L.vrec[q] = make_int2(k, i);
+}
+
+template <bool F32, bool CMP>
 __global__ void k_sing_tri(int32_t N, int32_t M, const void *__restrict__ coords, const int32_t *__restrict__ tri,
                            const double *__restrict__ V, const double *__restrict__ vmax,
                            const uint8_t *__restrict__ vflag, uint8_t *__restrict__ tflag,
-                           double *__restrict__ lam_mu) {
+                           double *__restrict__ lam_mu, SingList L) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const int32_t k = blockIdx.y;
     if (t >= M) return;
     const int32_t a = tri[3 * (int64_t)t], b = tri[3 * (int64_t)t + 1], c = tri[3 * (int64_t)t + 2];
     const int64_t vk = (int64_t)k * N;
     const int64_t o = (int64_t)k * M + t;
-    tflag[o] = 0;
-    lam_mu[2 * o] = 0.0;
-    lam_mu[2 * o + 1] = 0.0;
+    if (!CMP) {
+        tflag[o] = 0;
+        lam_mu[2 * o] = 0.0;
+        lam_mu[2 * o + 1] = 0.0;
+    }
     if (vflag[vk + a] | vflag[vk + b] | vflag[vk + c]) return;  // :173-174
     double n[3];
     if constexpr (F32) {
@@ -178,9 +199,17 @@ __global__ void k_sing_tri(int32_t N, int32_t M, const void *__restrict__ coords
     double lam, mu;
     lstsq32(c0, c1, rhs, lam, mu);
     if (lam + mu <= 1 && lam >= 0 && mu >= 0) {
-        tflag[o] = 1;
-        lam_mu[2 * o] = lam;
-        lam_mu[2 * o + 1] = mu;
+        if (CMP) {
+            const unsigned long long q = atomicAdd(L.cnt + 1, 1ull);
+            if ((int64_t)q < L.cap) {
+                L.trec[q] = make_int2(k, t);
+                L.tlm[q] = make_double2(lam, mu);
+            }
+        } else {
+            tflag[o] = 1;
+            lam_mu[2 * o] = lam;
+            lam_mu[2 * o + 1] = mu;
+        }
     }
 }
 
@@ -194,10 +223,31 @@ void launch_singularities(int32_t N, int32_t M, int32_t K, const void *coords, b
     k_sing_vmax<<<gv, kWG, 0, s>>>(N, V, reinterpret_cast<unsigned long long *>(vmax));
     k_sing_vertex<<<gv, kWG, 0, s>>>(N, V, vmax, eps, vflag);
     if (M > 0) {
+        const SingList none{nullptr, 0, nullptr, nullptr, nullptr};
         if (f32)
-            k_sing_tri<true><<<gt, kWG, 0, s>>>(N, M, coords, tri, V, vmax, vflag, tflag, lam_mu);
+            k_sing_tri<true, false><<<gt, kWG, 0, s>>>(N, M, coords, tri, V, vmax, vflag, tflag, lam_mu, none);
         else
-            k_sing_tri<false><<<gt, kWG, 0, s>>>(N, M, coords, tri, V, vmax, vflag, tflag, lam_mu);
+            k_sing_tri<false, false><<<gt, kWG, 0, s>>>(N, M, coords, tri, V, vmax, vflag, tflag, lam_mu, none);
+    }
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_singularities_compact(int32_t N, int32_t M, int32_t K, const void *coords, bool f32,
+                                  const int32_t *tri, const double *V, double eps, double *vmax, uint8_t *vflag,
+                                  unsigned long long *cnt, int64_t cap, int2 *vrec, int2 *trec, double2 *tlm,
+                                  hipStream_t s) {
+    MOF_HIP(hipMemsetAsync(vmax, 0, sizeof(double) * K, s));
+    MOF_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 2, s));
+    const dim3 gv((unsigned)((N + kWG - 1) / kWG), (unsigned)K), gt((unsigned)((M + kWG - 1) / kWG), (unsigned)K);
+    const SingList L{cnt, cap, vrec, trec, tlm};
+    k_sing_vmax<<<gv, kWG, 0, s>>>(N, V, reinterpret_cast<unsigned long long *>(vmax));
+    k_sing_vertex<<<gv, kWG, 0, s>>>(N, V, vmax, eps, vflag);
+    k_sing_vlist<<<gv, kWG, 0, s>>>(N, vflag, L);
+    if (M > 0) {
+        if (f32)
+            k_sing_tri<true, true><<<gt, kWG, 0, s>>>(N, M, coords, tri, V, vmax, vflag, nullptr, nullptr, L);
+        else
+            k_sing_tri<false, true><<<gt, kWG, 0, s>>>(N, M, coords, tri, V, vmax, vflag, nullptr, nullptr, L);
     }
     MOF_HIP(hipGetLastError());
 }

@@ -98,3 +98,23 @@ def test_gpu_160k_vs_oracle_sample():
     g_tf, g_lm = tf[0][sel], lm[0][sel]
     diff = g_tf != otf
     assert np.all(ambiguous(np.where(g_tf[:, None], g_lm, olm))[diff]) and diff.sum() <= 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag,ei", CASES)
+def test_gpu_compact_lists_equal_dense_flags(tag, ei):
+    """mof_singularities_compact returns exactly the dense path's flagged
+    vertices and triangles (and their lam, mu), field by field, also when the
+    first capacity is too small (the wrapper re-sizes from the totals)."""
+    from mofhip import singular
+    g = load_golden("G7_singularities")
+    coords, tri, V, eps = g["coords_" + tag], g["triangles"], g["V"], g["eps"][ei]
+    vmax, vf, tf, lm = singular.singularity_flags(coords, tri, V, eps)
+    for cap in (0, 1):
+        vmax2, verts, tris = singular.singularity_lists(coords, tri, V, eps, cap=cap)
+        assert np.array_equal(vmax, vmax2)
+        for k in range(len(V)):
+            assert np.array_equal(verts[k], np.flatnonzero(vf[k]))
+            tids, lms = tris[k]
+            assert np.array_equal(tids, np.flatnonzero(tf[k]))
+            assert np.array_equal(lms, lm[k][tids])
