@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
     const void *__restrict__ Afh, const uint16_t *__restrict__ Afh22) {
     int32_t tile, b;
-    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b, kGrpGal)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= c_sell_nb) return;
     galerkin_block<BSF>(pos, b, c_sell_nb, nC, c_sell_row, c_diag, c_dead, gptr, gent, Q, Af, f_sell_nb, Ac, Dh,
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B
                                               const int32_t *__restrict__ apos,
                                               const int32_t *__restrict__ sysi, float *__restrict__ r1) {
     int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b) || retired(sysi, b)) return;
+    if (!xcd_map(nblk, B, rb, b, kGrpSmooth) || retired(sysi, b)) return;
     const int64_t vb = (int64_t)b * N;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
                                                   const int32_t *__restrict__ sysi) {
     __shared__ float con[3][kRG];
     int32_t g, b;
-    if (!xcd_map(ngrp, B, g, b) || retired(sysi, b)) return;
+    if (!xcd_map(ngrp, B, g, b, kGrpRestr) || retired(sysi, b)) return;
     const int32_t I0 = grp[g], I1 = grp[g + 1];
     const int32_t q0 = F.mptr[I0], q1 = F.mptr[I1];
     if (q1 - q0 > kRG) {  // one oversized aggregate
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__
 __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, int32_t B,
                                                   const int32_t *__restrict__ sysi) {
     int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b) || retired(sysi, b)) return;
+    if (!xcd_map(nblk, B, rb, b, kGrpProl) || retired(sysi, b)) return;
     const int32_t i = rb * kWG + threadIdx.x;
     if (i >= F.n) return;
     prolong_node<2>(F, C, b, i);
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
                                                RedArgs rd) {
     __shared__ double lds[8];
     int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b) || retired(sysi, b)) return;
+    if (!xcd_map(nblk, B, rb, b, kGrpSmooth) || retired(sysi, b)) return;
     const int64_t vb = (int64_t)b * N;
     double rz = 0.0;
 #pragma unroll
@@ -698,7 +698,7 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
 }
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
-inline dim3 gtile(int64_t n, int32_t B) { return dim3(xcd_grid((int32_t)((n + kWG - 1) / kWG), B)); }
+inline dim3 gtile(int64_t n, int32_t B) { return dim3(xcd_grid((int32_t)((n + kWG - 1) / kWG), B, kGrpGal)); }
 
 MatH level0_mat(mof_mesh *m) {
     MatH mt;
@@ -906,7 +906,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     const int32_t *sysi = w.sysi.p;
     const float om = G.omega;
     const MatH mat0 = level0_mat(m);
-    const dim3 gx(xcd_grid(nblk, B));
+    const dim3 gx(xcd_grid(nblk, B, kGrpSmooth));
     Lvl v[kMaxLevels];
     for (int32_t l = 0; l < L; ++l) v[l] = level_view(G.lv[l]);
     // levels S.. run fused in k_subcycle
@@ -917,11 +917,11 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
             k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x, v[0].apos, sysi, v[0].r);
-            k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B)), kWG, 0, s>>>(
+            k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
                 v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om, sysi);
         } else {
             k_res3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], sysi);
-            k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B)), kWG, 0, s>>>(
+            k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
                 v[l], v[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om, sysi);
         }
     }
@@ -937,7 +937,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = S - 1; l >= 0; --l) {
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
-            k_prolong0<<<dim3(xcd_grid(nb0, B)), kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+            k_prolong0<<<dim3(xcd_grid(nb0, B, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
             k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, reinterpret_cast<const uint2 *>(G.D0h.p), r0,
                                        v[0].x, om, sysi, z0, part_slot, rd);
         } else {

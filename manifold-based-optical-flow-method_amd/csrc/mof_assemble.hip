@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_blocks(
     // XCD-aware tiles: the B systems of a 256-slot tile run back to back on
     // one XCD and share the tile's structure, lambda a2 and iw in its L2
     int32_t tile, b;
-    if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b, kGrpAsm)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= sell_nb) return;
     const int32_t p = sell_blk[pos];
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
     uint2 *__restrict__ Dh, int32_t nown) {
     int32_t tile, b;
-    if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b)) return;
+    if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b, kGrpAsm)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= sell_nb) return;
     const int32_t p = sell_blk[pos];
@@ -620,7 +620,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, ldI, w.dt.p,
                                   w.u64.p, w.fc.p, precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
     const int64_t snb = m->pat.sell_nb();
-    const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B));
+    const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
     // multigrid: the level-0 smoother's bf16 operator and D^-1 come from here
     AmgBf16 bf{nullptr, nullptr};

@@ -234,7 +234,7 @@ template <typename V, bool FIRST>
 __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int32_t flags) {
     __shared__ double lds[8];
     int32_t rb, b;
-    if (!xcd_map(a.nblk, a.B, rb, b)) return;
+    if (!xcd_map(a.nblk, a.B, rb, b, kGrpSpmv)) return;
     const bool force = flags & kForce;
     // retired systems: inactive, or converged in an earlier iteration (the
     // word is sticky, so no later launch re-reads a stale partial slot)
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
                                                   double *__restrict__ part) {
     __shared__ double lds[8];
     int32_t rb, b;  // XCD-aware: the systems of a row block share its a2 blocks in L2
-    if (!xcd_map(nblk, B, rb, b) || !sysi[b * kSysStride + SI_ACTIVE]) return;
+    if (!xcd_map(nblk, B, rb, b, kGrpRes) || !sysi[b * kSysStride + SI_ACTIVE]) return;
     const int32_t N = op.N;
     const int64_t vb = (int64_t)b * N;
     double rr = 0.0, ff = 0.0;
@@ -526,7 +526,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s);
     };
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
-    const dim3 gx(xcd_grid(m->ws.nblk, B));
+    const dim3 gx(xcd_grid(m->ws.nblk, B, kGrpSpmv));
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol);
     if (amg) precond(0);
@@ -716,7 +716,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
-        k_residual<<<dim3(xcd_grid(w.nblk, B)), kWG, 0, s>>>(o64, w.nblk, B, rd, w.rhs.p, w.x64.p, w.sysi.p,
+        k_residual<<<dim3(xcd_grid(w.nblk, B, kGrpRes)), kWG, 0, s>>>(o64, w.nblk, B, rd, w.rhs.p, w.x64.p, w.sysi.p,
                                                               w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
@@ -808,7 +808,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
     auto spmv = [&](bool first, int32_t it_) {
         dd_halo(d, B, sizeof(V) == 4, 0, s);
         for (size_t l = 0; l < L; ++l) {
-            const dim3 gx(xcd_grid(d->parts[l]->ws.nblk, B));
+            const dim3 gx(xcd_grid(d->parts[l]->ws.nblk, B, kGrpSpmv));
             if (first)
                 k_pcg_spmv<V, true><<<gx, kWG, 0, s>>>(args[l], it_, 0);
             else
@@ -905,7 +905,7 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
             mof_mesh *m = d->parts[l];
             Workspace &w = m->ws;
             const RedArgs rd{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
-            k_residual<<<dim3(xcd_grid(w.nblk, B)), kWG, 0, s>>>(op64(m), w.nblk, B, rd, w.rhs.p, w.x64.p,
+            k_residual<<<dim3(xcd_grid(w.nblk, B, kGrpRes)), kWG, 0, s>>>(op64(m), w.nblk, B, rd, w.rhs.p, w.x64.p,
                                                                   w.sysi.p, w.r64.p, d->part_rr0.p);
         }
         dd_sync_partials(d, d->part_rr0.p, 2 * (int64_t)B * d->nmax, s);
@@ -939,7 +939,7 @@ double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipS
     MOF_HIP(hipEventCreate(&e0));
     MOF_HIP(hipEventCreate(&e1));
     *bytes = spmv_launch_bytes(m, precision, B);
-    const dim3 gx(xcd_grid(w.nblk, B));
+    const dim3 gx(xcd_grid(w.nblk, B, kGrpSpmv));
     auto launch = [&]() {
         if (precision == MOF_PREC_MIXED) {
             PcgArgs<float> a = make_args<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p);
