@@ -51,6 +51,21 @@ def test_amg_fewer_iterations_and_deterministic():
     assert np.abs(V1 - Vj).max() < VTOL
 
 
+@pytest.mark.parametrize("precision,precond", [("mixed", "amg"), ("mixed", "jacobi"), ("f64", "jacobi")])
+def test_partial_system_groups_bit_identical(precision, precond):
+    """Batches larger than the XCD system groups (8 and 32 systems) with a
+    partial last group: same bits as one system per launch."""
+    g = load_golden("G1_ico642")
+    m = mesh_of(g)
+    T = 42
+    I = synth.travelling_wave(g["coordinates"], T)
+    tk = np.arange(T, dtype=np.float64)
+    V1, s1 = m.solve_range(I, tk, 0, T - 1, 0.01, precision=precision, precond=precond, batch=1)
+    V41, s41 = m.solve_range(I, tk, 0, T - 1, 0.01, precision=precision, precond=precond, batch=41)
+    assert s1["failed"] == 0 and s41["failed"] == 0
+    assert np.array_equal(V1, V41)
+
+
 def test_amg_tiny_mesh_falls_back():
     """A mesh that does not coarsen (12 vertices) keeps block Jacobi."""
     p, t = synth.icosphere(1, 10.0)
