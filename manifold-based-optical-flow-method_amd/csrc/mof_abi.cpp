@@ -168,6 +168,13 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
     m->tri_orig.upload(tri_old.data(), 3 * (size_t)M, s);
     m->perm_d.alloc(N);
     m->perm_d.upload(m->perm.data(), N, s);
+    {
+        // vertices in no triangle are never gathered: column 0
+        std::vector<int32_t> icol(N, 0);
+        for (size_t q = 0; q < 3 * (size_t)M; ++q) icol[tri_new[q]] = tri_old[q];
+        m->icol.alloc(N);
+        m->icol.upload(icol.data(), N, s);
+    }
     m->area.alloc(M);
     m->area.upload(area_new.data(), M, s);
     auto put = [&](mof::DevArray<int32_t> &d, const std::vector<int32_t> &h) {
@@ -396,10 +403,10 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
             if (Bmax <= 0) {
                 // auto: 256 timesteps per launch sequence, fewer when a quarter
                 // of the free device memory cannot hold their workspace
-                // (~700 B per vertex and system with the multigrid levels)
+                // (~720 B per vertex and system with the multigrid levels)
                 size_t free_b = 0, total_b = 0;
                 MOF_HIP(hipMemGetInfo(&free_b, &total_b));
-                const double per_sys = 700.0 * (double)m->N + 1.0;
+                const double per_sys = 720.0 * (double)m->N + 1.0;
                 Bmax = (int32_t)std::max(1.0, std::min(256.0, 0.25 * (double)free_b / per_sys));
             }
             const int32_t B = std::min(K, Bmax);

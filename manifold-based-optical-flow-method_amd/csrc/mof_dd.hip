@@ -650,7 +650,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
             if (Bmax <= 0) {
                 size_t free_b = 0, total_b = 0;
                 MOF_HIP(hipMemGetInfo(&free_b, &total_b));
-                const double per_sys = 600.0 * (double)N * (d->rank < 0 ? 1.0 : 1.0 / d->P) + 1.0;
+                const double per_sys = 620.0 * (double)N * (d->rank < 0 ? 1.0 : 1.0 / d->P) + 1.0;
                 Bmax = (int32_t)std::max(1.0, std::min(64.0, 0.25 * (double)free_b / per_sys));
             }
             const int32_t B = std::min(K, Bmax);

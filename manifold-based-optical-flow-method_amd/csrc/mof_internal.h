@@ -119,6 +119,7 @@ struct Workspace {
     DevArray<int32_t> sysi;            // [B][8] per-system flags
     DevArray<double> dt;               // [B]
     DevArray<double> Ibuf;             // [B][N] I0 rows + [B][N] I1 rows (host-staged)
+    DevArray<double> Iint;             // the batch's I rows in internal vertex order ([B+1] or [2B] rows)
     DevArray<double> Vbuf;             // [B][2N] planar output staging
 };
 
@@ -154,6 +155,7 @@ struct mof_mesh {
     std::vector<int32_t> tperm, tinv;
     mof::DevArray<int32_t> perm_d;    // (N) old -> new, for the planar V gather
     mof::DevArray<int32_t> tri_orig;  // (M,3) caller's vertex ids, for gathers of I
+    mof::DevArray<int32_t> icol;      // (N) internal vertex -> its column of the caller's I
     // device mesh data (internal order)
     mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row,
         diag_pos, tsell_off, tinc;

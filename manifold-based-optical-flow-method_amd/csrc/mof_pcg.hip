@@ -665,6 +665,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.sysi.alloc((size_t)kSysStride * B);
     w.dt.alloc(B);
     w.Ibuf.alloc(2 * N * B);
+    w.Iint.alloc(2 * N * B);
     w.Vbuf.alloc(2 * N * B);
     if (m->h_cap < B) {
         if (m->h_sysi) (void)hipHostFree(m->h_sysi);
