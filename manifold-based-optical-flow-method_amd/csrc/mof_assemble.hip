@@ -357,7 +357,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     const float *ub = u + 6 * (int64_t)b * (M + 1);
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int32_t c0 = cptr[p], c1 = cptr[p + 1];
-    constexpr int U = 4;
+    constexpr int U = 4;  // 6 / 8: 7492 / 8475 vs 7065 us per 256-system launch
     for (int32_t c = c0; c < c1; c += U) {
         int32_t T[U], a[U], bb[U];
 #pragma unroll
@@ -399,13 +399,25 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     // f_i in fp64, in the reference's triangle order
     const double *fb = fc + 6 * (int64_t)b * (M + 1);
     double f0 = 0.0, f1 = 0.0;
-    for (int32_t c = c0; c < c1; ++c) {
-        const int32_t code = clist[c];
-        const int32_t a = (code % 9) / 3;
-        if (a != code % 3) continue;
-        const double2 fv = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)(code / 9) + 2 * a);
-        f0 += fv.x;
-        f1 += fv.y;
+    // the codes and f terms of a chunk are all fetched before the in-order
+    // fold (masked slots add nothing: the running sum is never -0.0)
+    constexpr int UF = 8;
+    for (int32_t c = c0; c < c1; c += UF) {
+        int32_t code[UF];
+#pragma unroll
+        for (int q = 0; q < UF; ++q) code[q] = clist[min(c + q, c1 - 1)];
+        double2 fv[UF];
+#pragma unroll
+        for (int q = 0; q < UF; ++q)
+            fv[q] = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)(code[q] / 9) + 2 * ((code[q] % 9) / 3));
+#pragma unroll
+        for (int q = 0; q < UF; ++q) {
+            const bool on = c + q < c1 && (code[q] % 9) / 3 == code[q] % 3;
+            if (on) {
+                f0 += fv[q].x;
+                f1 += fv[q].y;
+            }
+        }
     }
     double inv[4];
     const double d0 = Av[0], d1 = Av[1], d2 = Av[2], d3 = Av[3];
