@@ -160,7 +160,7 @@ __device__ __forceinline__ void galerkin_block(
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
     // U entries at a time, every load of a chunk issued before use (entries
     // past the list re-load the last one and are masked out)
-    constexpr int U = 4;
+    constexpr int U = 4;  // level 0 with 2 / 8: 5269 / 6032 vs 4654 us per 256-system launch
     for (int32_t t0 = g0; t0 < g1; t0 += U) {
         int32_t fp[U], ii[U], jj[U];
 #pragma unroll
