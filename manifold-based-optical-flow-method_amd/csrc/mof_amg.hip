@@ -140,8 +140,6 @@ __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__rest
     H[q] = make_uint2(bf16_bits(v.x) | (bf16_bits(v.y) << 16), bf16_bits(v.z) | (bf16_bits(v.w) << 16));
 }
 
-__device__ __forceinline__ void ld_h9(const uint4 *H, const uint16_t *H22, int64_t q, float (&a)[3][3]);
-
 // Block (I, J) at coarse SELL position pos of A_{l+1} = Q^T A_l Q for system
 // b, summed over its gather list in list order; the diagonal block also gets
 // 1 on dead dofs and stores its 3x3 inverse for the smoother.
@@ -152,7 +150,7 @@ __device__ __forceinline__ void galerkin_block(
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
-    const void *__restrict__ Afh, const uint16_t *__restrict__ Afh22) {
+    const uint2 *__restrict__ Afh) {
     const int32_t I = c_sell_row[pos];
     if (I >= nC) return;  // rows past n in the last slice
     const float *A = Af + (int64_t)b * f_sell_nb * bstride<BSF>();
@@ -181,18 +179,16 @@ __device__ __forceinline__ void galerkin_block(
                     // of the fp32 A: 5.35 vs 6.78 ms per 256 systems, same
                     // iteration counts) -- the coarse operator is then the
                     // Galerkin product of the operator the smoother sweeps
-                    const uint2 t = static_cast<const uint2 *>(Afh)[(int64_t)b * f_sell_nb + max(fp[u], 0)];
+                    const uint2 t = Afh[(int64_t)b * f_sell_nb + max(fp[u], 0)];
                     a[u][0][0] = bf16_lo(t.x); a[u][0][1] = bf16_hi(t.x);
                     a[u][1][0] = bf16_lo(t.y); a[u][1][1] = bf16_hi(t.y);
                 } else {
                     ldm<BSF>(A, max(fp[u], 0), a[u]);
                 }
             } else {
-                if (Afh)  // level >= 1: the level's bf16 sweep copy (18 B per block; 620 vs 731 us)
-                    ld_h9(static_cast<const uint4 *>(Afh) + (int64_t)b * f_sell_nb, Afh22 + (int64_t)b * f_sell_nb,
-                          max(fp[u], 0), a[u]);
-                else
-                    ldm<BSF>(A, max(fp[u], 0), a[u]);
+                // level >= 1: the fp32 operator (its bf16 sweep copy: 620 vs
+                // 731 us per launch, but 116 vs 110 PCG its/timestep on R3)
+                ldm<BSF>(A, max(fp[u], 0), a[u]);
             }
             if (fp[u] < 0) {
 #pragma unroll
@@ -254,13 +250,13 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
-    const void *__restrict__ Afh, const uint16_t *__restrict__ Afh22) {
+    const uint2 *__restrict__ Afh) {
     int32_t tile, b;
     if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b, kGrpGal)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= c_sell_nb) return;
     galerkin_block<BSF>(pos, b, c_sell_nb, nC, c_sell_row, c_diag, c_dead, gptr, gent, Q, Af, f_sell_nb, Ac, Dh,
-                        Dh22, Ah, Ah22, Afh, Afh22);
+                        Dh22, Ah, Ah22, Afh);
 }
 
 constexpr int kMaxCoarse = 128;
@@ -862,12 +858,12 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
                                                               m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p,
                                                               ah(C), ah22(C),
-                                                              G.A0h.p, nullptr);
+                                                              reinterpret_cast<const uint2 *>(G.A0h.p));
         else
             k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
                                                               F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
-                                                              ah(F), ah22(F));
+                                                              nullptr);
     }
     AmgDevLevel &Lc = G.lv[L - 1];
     k_coarse_inverse<<<dim3((unsigned)B), kInvWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
