@@ -711,7 +711,8 @@ MatH level0_mat(mof_mesh *m) {
 
 bool amg_build(mof_mesh *m) {
     AmgParams prm;
-    if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knob
+    if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
+    if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
     if (m->n_own < m->N) prm.nown = m->n_own;
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
@@ -723,6 +724,7 @@ bool amg_build(mof_mesh *m) {
     AmgHierarchy H;
     build_amg(m->pat, e.data(), prm, H);
     G.omega = prm.omega;
+    G.omega1 = prm.omega1;
     G.lv.clear();
     G.built = true;
     // a mesh that does not coarsen (<= 42 vertices) keeps block Jacobi
@@ -901,6 +903,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     const int32_t L = (int32_t)G.lv.size();
     const int32_t *sysi = w.sysi.p;
     const float om = G.omega;
+    const float om1 = G.omega1;  // levels >= 1
     const MatH mat0 = level0_mat(m);
     const dim3 gx(xcd_grid(nblk, B, kGrpSmooth));
     Lvl v[kMaxLevels];
@@ -914,11 +917,11 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         if (l == 0) {
             k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x, v[0].apos, sysi, v[0].r);
             k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
-                v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om, sysi);
+                v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
         } else {
             k_res3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], sysi);
             k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
-                v[l], v[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om, sysi);
+                v[l], v[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
         }
     }
     SubArgs sa;
@@ -926,7 +929,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     sa.last = L - 1;
     for (int32_t l = 0; l < L; ++l) sa.lv[l] = v[l];
     sa.cinv = G.cinv.p;
-    sa.omega = om;
+    sa.omega = om1;
     sa.sysi = sysi;
     k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
     // up: coarse correction, post-smooth
@@ -938,7 +941,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                                        v[0].x, om, sysi, z0, part_slot, rd);
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
-            k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om, sysi);
+            k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om1, sysi);
         }
     }
     MOF_HIP(hipGetLastError());
