@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--precond", default=None, choices=["jacobi", "amg"],
                     help="inner preconditioner (default: amg for mixed, jacobi for f64)")
     ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--inner-rtol", type=float, default=0.0,
+                    help="mixed precision: inner PCG tolerance per refinement step (0: the library's 1e-4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 64,
                     help="fraction of the triangle loop the CPU baseline times")
@@ -148,7 +150,7 @@ def main():
     tk = np.arange(K_rank + 1, dtype=np.float64)
     torch.cuda.synchronize(dev)
     precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
-    opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond)
+    opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol)
 
     def step(s, timed):
         return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), K_rank + 1, tk, s * B,
