@@ -8,21 +8,24 @@
 //   k_coarse_inverse   the coarsest operator (<= 128 dofs) inverted by the
 //                      symmetric sweep operator in registers (fp64, one
 //                      workgroup per system).
-// Each PCG iteration applies one symmetric V(1,1)-cycle to the residual r:
+// Each PCG iteration applies one symmetric V(1,1)-cycle to the residual r
+// (damped block Jacobi: w = 0.85 on level 0, w1 = 1.0 on the coarse levels):
 //   level 0 pre-smooth x0 = w D^-1 r is fused into k_pcg_update / k_pcg_init;
 //   per level l:  k_res0 / k_res3  r_l = b_l - A_l x_l, written in member
 //                                  order of the next level's aggregates
 //                 k_restrict       b_{l+1} = Q^T r_l (contiguous members),
-//                                  x_{l+1} = w D^-1 b_{l+1} (next pre-smooth)
-//   levels with <= 4096 nodes and the coarsest solve y = A_c^-1 b run in
+//                                  x_{l+1} = w1 D^-1 b_{l+1} (next pre-smooth)
+//   levels with <= kSubNodes nodes and the coarsest solve y = A_c^-1 b run in
 //   one launch (k_subcycle, one workgroup per system);
-//   per level l:  k_prolong        x_l += Q y_{l+1}
-//                 k_post3 / k_post0  y_l = x_l + w D^-1 (b_l - A_l x_l); at
+//   per level l:  k_prolong0 / k_prolong  x_l += Q y_{l+1}
+//                 k_post0 / k_post3  y_l = x_l + w D^-1 (b_l - A_l x_l); at
 //                                  level 0 y = z and the partial r.z of the PCG
 // Every launch covers all B systems and skips retired systems. Level 0 sweeps
-// a bf16 copy of the inner solver's SELL A (k_to_bf16, once per batch) with
-// its fp32 2x2 D^-1 and row-kernel layout (XCD-aware, batched loads); coarse levels store 3x3 blocks as 12 floats (rows padded to
-// 4) and vectors as float4. All sums run in a fixed order: the cycle is
+// bf16 copies of the inner solver's SELL A and 2x2 D^-1, written by the
+// assembly (k_assemble_mixed), in the PCG row-kernel layout (XCD-aware,
+// batched loads); coarse levels keep fp32 3x3 blocks (12 floats, rows padded
+// to 4) for the Galerkin products and bf16 copies (18 B per block) for the
+// sweeps, vectors as float4. All sums run in a fixed order: the cycle is
 // deterministic and independent of B.
 #include <algorithm>
 #include <cstdio>

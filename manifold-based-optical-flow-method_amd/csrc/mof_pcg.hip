@@ -7,8 +7,10 @@
 // (16 B per block in fp32, read with one dwordx4 per lane, 1 KiB per
 // wave-instruction). The SpMV grid is XCD-aware: each XCD owns one
 // contiguous eighth of the vertex rows of every system and walks it row
-// block by row block, the B systems of a row block back to back, so the
-// row block's column indices are read once per XCD (mof_rowkern.h).
+// block by row block, a group of 8 systems of a row block back to back, so
+// the row block's column indices are read once per XCD and group and a
+// system's neighbour rows are still in L2 at its next row block
+// (mof_rowkern.h).
 //
 // The fp64 residual of the refinement (k_residual) applies A without the
 // materialised blocks: lambda a2 (shared SELL blocks) plus a1 per incident
