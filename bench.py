@@ -142,10 +142,17 @@ def main():
     steps_total = args.warmup + args.steps
     K_rank = steps_total * B
     k_off, _ = rank_k_range(rank, world, 0, world * K_rank)  # this rank's timesteps
-    I_host = np.sin(3.0 * np.arctan2(p[:, 1], p[:, 0])[None, :]
-                    - 0.3 * (k_off + np.arange(K_rank + 1, dtype=np.float64))[:, None])
+    # generated on the device: (K_rank + 1) x N f64 is 7.4 GB per rank at the
+    # default C3 sizes, which 8 ranks would otherwise hold in host memory
     dev = torch.device("cuda", local)
-    I_dev = torch.from_numpy(np.ascontiguousarray(I_host)).to(dev)
+    pts = torch.from_numpy(np.ascontiguousarray(p[:, :2])).to(dev)
+    phi = torch.atan2(pts[:, 1], pts[:, 0])
+    kk = k_off + torch.arange(K_rank + 1, dtype=torch.float64, device=dev)
+    I_dev = torch.empty((K_rank + 1, N), dtype=torch.float64, device=dev)
+    for r0 in range(0, K_rank + 1, 256):
+        r1 = min(K_rank + 1, r0 + 256)
+        I_dev[r0:r1] = torch.sin(3.0 * phi[None, :] - 0.3 * kk[r0:r1, None])
+    del pts, phi, kk
     V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(K_rank + 1, dtype=np.float64)
     torch.cuda.synchronize(dev)
