@@ -59,7 +59,11 @@ extern "C" {
 #define MOF_PRECOND_AMG 8u     /* MOF_PREC_MIXED: aggregation-multigrid V(1,1)
                                   preconditioner for the inner PCG (built
                                   once per mesh; meshes of <= 64 vertices
-                                  keep block Jacobi) */
+                                  keep block Jacobi). Smoother damping:
+                                  0.85 on the fine level, 1.0 on the coarse
+                                  levels; the environment variables
+                                  MOF_AMG_OMEGA / MOF_AMG_OMEGA1, read when
+                                  the hierarchy is built, override them */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */
