@@ -180,6 +180,7 @@ def main():
                   "ms_solve"):
             agg[k] += st[k]
         agg["max_rel_residual"] = max(agg["max_rel_residual"], st["max_rel_residual"])
+        agg["max_outer_steps"] = max(agg.get("max_outer_steps", 0), st["outer_steps"])
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     cdev = torch.device("cpu") if rehearse else dev
@@ -221,6 +222,7 @@ def main():
             "cpu_baseline": cpu,
             "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / (args.steps * B), 1),
                        "failed": agg["failed"], "max_rel_residual": agg["max_rel_residual"],
+                       "max_refinement_steps": agg.get("max_outer_steps", 0),
                        "ms_assembly_per_timestep": round(agg["ms_assembly"] / (args.steps * B), 4),
                        "ms_solve_per_timestep": round(agg["ms_solve"] / (args.steps * B), 4),
                        "mesh_build_s": round(mesh_s, 3), "mesh_geometry_ms": round(info["ms_geometry"], 3),
