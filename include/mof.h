@@ -246,6 +246,12 @@ int mof_cell_areas(const float *points, const int64_t *triangles, int64_t N, int
 int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
                   int32_t *level_nodes, double *qtq_err);
 
+/* Diagnostic (host only): checks that the XCD-aware workgroup order of the
+ * row kernels -- nblk row blocks x batch systems, walked in groups of
+ * `group` systems (0: all) -- visits every (row block, system) pair exactly
+ * once. MOF_OK, or an error with mof_last_error() set. */
+int mof_xcd_map_check(int32_t nblk, int32_t batch, int32_t group);
+
 /* ---- one timestep's system decomposed over P
  * vertex parts (stretch; timestep shards stay the throughput path) --------
  * A part owns vertices (both unknowns of each); its local mesh is every

@@ -677,6 +677,13 @@ int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int
     });
 }
 
+int mof_xcd_map_check(int32_t nblk, int32_t batch, int32_t group) {
+    return guarded([&] {
+        MOF_REQUIRE(nblk > 0 && batch > 0 && group >= 0, "bad arguments");
+        MOF_REQUIRE(mof::xcd_map_covers(nblk, batch, group), "XCD order does not cover every (row block, system) once");
+    });
+}
+
 int mof_bench_spmv(mof_mesh *m, uint32_t precision, int32_t batch, int32_t reps,
                    double *ms_per_launch, double *bytes_per_launch) {
     return guarded([&] {

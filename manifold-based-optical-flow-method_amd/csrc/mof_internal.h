@@ -258,6 +258,8 @@ void amg_destroy(AmgDevice *g);
 
 int32_t amg_levels(const mof_mesh *m);
 
+// every (row block, system) pair of the XCD order (mof_rowkern.h) visited once
+bool xcd_map_covers(int32_t nblk, int32_t B, int32_t grp);
 double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,
                   double *bytes);
 

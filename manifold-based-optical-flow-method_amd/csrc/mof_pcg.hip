@@ -964,4 +964,21 @@ double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipS
     return ms / reps;
 }
 
+
+// Host check of the XCD order (tests, via mof_xcd_map_check): every
+// (row block, system) pair is visited by exactly one workgroup of the grid.
+bool xcd_map_covers(int32_t nblk, int32_t B, int32_t grp) {
+    if (nblk < 1 || B < 1) return false;
+    std::vector<uint8_t> hit((size_t)nblk * B, 0);
+    const int64_t W = xcd_grid(nblk, B, grp);
+    for (int64_t w = 0; w < W; ++w) {
+        int32_t rb, b;
+        if (!xcd_map_w((int32_t)w, nblk, B, rb, b, grp)) continue;
+        if (rb < 0 || b < 0 || hit[(size_t)b * nblk + rb]++) return false;
+    }
+    for (uint8_t h : hit)
+        if (h != 1) return false;
+    return true;
+}
+
 }  // namespace mof

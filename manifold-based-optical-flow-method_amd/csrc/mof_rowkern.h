@@ -176,8 +176,8 @@ constexpr int32_t kGrpSpmv = MOF_G_SPMV, kGrpSmooth = MOF_G_SMOOTH, kGrpRes = MO
                   kGrpAsm = MOF_G_ASM, kGrpProl = MOF_G_PROL, kGrpRestr = MOF_G_RESTR;
 __host__ __device__ __forceinline__ int32_t sys_group(int32_t B, int32_t G) { return G > 0 && G < B ? G : B; }
 
-__device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, int32_t &sys, int32_t grp_sz) {
-    const int32_t w = blockIdx.x;
+__host__ __device__ __forceinline__ bool xcd_map_w(int32_t w, int32_t nblk, int32_t B, int32_t &rb, int32_t &sys,
+                                                   int32_t grp_sz) {
     const int32_t q = w >> 3;
     const int32_t chunk = (nblk + 7) >> 3;
     const int32_t G = sys_group(B, grp_sz);
@@ -185,6 +185,9 @@ __device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, in
     sys = grp * G + rem % G;
     rb = (w & 7) * chunk + rem / G;
     return rb < nblk && sys < B;
+}
+__device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, int32_t &sys, int32_t grp_sz) {
+    return xcd_map_w((int32_t)blockIdx.x, nblk, B, rb, sys, grp_sz);
 }
 
 inline unsigned xcd_grid(int32_t nblk, int32_t B, int32_t grp_sz) {

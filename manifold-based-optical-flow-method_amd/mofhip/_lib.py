@@ -48,7 +48,7 @@ EXPORTS = (
     "mof_point_normals", "mof_cell_areas", "mof_singularities", "mof_amg_probe",
     "mof_partition_rcb", "mof_dd_plan_info", "mof_dd_create", "mof_dd_unique_id",
     "mof_dd_create_rank", "mof_dd_destroy", "mof_dd_get_info", "mof_dd_solve_range",
-    "mof_singularities_compact",
+    "mof_singularities_compact", "mof_xcd_map_check",
 )
 
 
@@ -158,6 +158,7 @@ def lib():
             "mof_singularities": ([i32, P, P, i32, i32, P, i32, f64, u32, P, P, P, P, P],
                                   ctypes.c_int),
             "mof_amg_probe": ([P, P, i32, i32, P, P, P], ctypes.c_int),
+            "mof_xcd_map_check": ([i32, i32, i32], ctypes.c_int),
             "mof_singularities_compact": ([i32, P, P, i32, i32, P, i32, f64, u32, P, i64, P, P, P, P, P,
                                            P, P], ctypes.c_int),
             "mof_partition_rcb": ([P, i32, i32, P], ctypes.c_int),

@@ -60,3 +60,13 @@ def test_probe_rejects_bad_input():
     rc = L.lib().mof_amg_probe(L.ptr(bad), L.ptr(E), len(p), len(t), ctypes.byref(nl), L.ptr(sizes), None)
     with pytest.raises(L.MofError):
         L.check(rc)
+
+
+@pytest.mark.parametrize("nblk", [1, 7, 8, 9, 160, 641])
+@pytest.mark.parametrize("batch", [1, 3, 8, 15, 41, 256])
+@pytest.mark.parametrize("group", [0, 1, 8, 32])
+def test_xcd_order_visits_every_pair_once(nblk, batch, group):
+    """The XCD-aware workgroup order of the row kernels (system groups of
+    8 / 32 / all) covers every (row block, system) pair exactly once, also
+    with partial groups and row-block counts not divisible by 8."""
+    L.check(L.lib().mof_xcd_map_check(nblk, batch, group))
