@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         float y0, y1;
-        spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
+        spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1);
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
         reinterpret_cast<uint32_t *>(r1)[vb + apos[i]] = bf16_bits(ri.x - y0) | (bf16_bits(ri.y - y1) << 16);
     }
@@ -489,11 +489,22 @@ __device__ __forceinline__ void prolong_node(const Lvl &F, const Lvl &C, int32_t
     float y[3], xi[BSF];
     ldv<3>(C.y + (int64_t)b * C.n * 4, F.agg[i], y);
     float *xb = F.x + (int64_t)b * F.n * vstride<BSF>();
-    ldv<BSF>(xb, i, xi);
+    if constexpr (BSF == 2) {
+        const float2 t = ld_x0(F.x, (int64_t)b * F.n + i);
+        xi[0] = t.x;
+        xi[1] = t.y;
+    } else {
+        ldv<BSF>(xb, i, xi);
+    }
     const float *qi = F.Q + (int64_t)i * BSF * 3;
 #pragma unroll
     for (int k = 0; k < BSF; ++k) xi[k] += qi[3 * k] * y[0] + qi[3 * k + 1] * y[1] + qi[3 * k + 2] * y[2];
-    stv<BSF>(xb, i, xi);
+    if constexpr (BSF == 2 && MOF_X0_BF16 == 2)  // full-precision x for the post-smoothing
+        reinterpret_cast<float2 *>(F.y)[(int64_t)b * F.n + i] = make_float2(xi[0], xi[1]);
+    else if constexpr (BSF == 2)
+        st_x0(F.x, (int64_t)b * F.n + i, xi[0], xi[1]);
+    else
+        stv<BSF>(xb, i, xi);
 }
 
 // coarse level: y = x + w D^-1 (b - A x)
@@ -682,9 +693,15 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
         const int32_t i = rb * kRowsPerWG + g * kWG + threadIdx.x;
         if (i >= N) break;
         float y0, y1;
-        spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
+        float2 xi;
+        if constexpr (MOF_X0_BF16 == 2) {
+            spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
+            xi = reinterpret_cast<const float2 *>(xv)[vb + i];
+        } else {
+            spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1);
+            xi = ld_x0(xv, vb + i);
+        }
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-        const float2 xi = reinterpret_cast<const float2 *>(xv)[vb + i];
         const float2 ds = bf16_mat2(Dh[vb + i], ri.x - y0, ri.y - y1);
         const float z0 = xi.x + omega * ds.x;
         const float z1 = xi.y + omega * ds.y;
@@ -797,6 +814,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
         const size_t n = D.n;
         if (l == 0) {
             D.x.alloc(2 * n * B);
+            if (MOF_X0_BF16 == 2) D.y.alloc(2 * n * B);
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
             G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
             G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
@@ -941,7 +959,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
             k_prolong0<<<dim3(xcd_grid(nb0, B, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
             k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, reinterpret_cast<const uint2 *>(G.D0h.p), r0,
-                                       v[0].x, om, sysi, z0, part_slot, rd);
+                                       MOF_X0_BF16 == 2 ? v[0].y : v[0].x, om, sysi, z0, part_slot, rd);
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
             k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om1, sysi);

@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
         } else if constexpr (sizeof(V) == 4) {
             // the smoother's D^-1 (bf16), as in every later sweep
             const float2 d = bf16_mat2(a.dh[vi], r0, r1);
-            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * d.x, a.omega * d.y};
+            st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
         }
         if (i < a.red.nown) rr += (double)r0 * r0 + (double)r1 * r1;
     }
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
         } else if constexpr (sizeof(V) == 4) {
             // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
             const float2 d = bf16_mat2(a.dh[vi], ri.x, ri.y);
-            *reinterpret_cast<V2 *>(a.x0 + 2 * vi) = V2{a.omega * d.x, a.omega * d.y};
+            st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
         }
         if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
     }

@@ -251,6 +251,32 @@ __device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i,
     spmv_row_hx(mt, b, i, [x](int32_t j) { return reinterpret_cast<const float2 *>(x)[j]; }, y0, y1);
 }
 
+// The V-cycle's level-0 iterate: the pre-smoothed x0 = w D^-1 r (written by
+// the PCG update, gathered by k_res0, read by the prolongation) and the
+// corrected x = x0 + Q y (written by the prolongation, gathered by k_post0).
+// MOF_X0_BF16 = 0: both float2 in one buffer; 1: both bf16 pairs (4 B);
+// 2 (default): x0 as a bf16 pair, x as float2 in level 0's y buffer.
+// PCG its/timestep and timesteps/s, C3 / R3 / C2 mixed: mode 0 18 / 101.9 /
+// 22.8 at 2357 / 374 / 9474; mode 1 18 / 115.8 / 22.8 at 2472 / 345 / 9943;
+// mode 2 18 / 103 / 22.8 at 2428 / 376 / 9676 (same box).
+#ifndef MOF_X0_BF16
+#define MOF_X0_BF16 2
+#endif
+__device__ __forceinline__ float2 ld_x0(const float *x, int64_t vi) {
+    if constexpr (MOF_X0_BF16 >= 1) {
+        const uint32_t h = reinterpret_cast<const uint32_t *>(x)[vi];
+        return make_float2(bf16_lo(h), bf16_hi(h));
+    } else {
+        return reinterpret_cast<const float2 *>(x)[vi];
+    }
+}
+__device__ __forceinline__ void st_x0(float *x, int64_t vi, float a, float b) {
+    if constexpr (MOF_X0_BF16 >= 1)
+        reinterpret_cast<uint32_t *>(x)[vi] = bf16_bits(a) | (bf16_bits(b) << 16);
+    else
+        reinterpret_cast<float2 *>(x)[vi] = make_float2(a, b);
+}
+
 // 2x2 block stored as 4 bf16: y = D v
 __device__ __forceinline__ float2 bf16_mat2(uint2 d, float v0, float v1) {
     return make_float2(bf16_lo(d.x) * v0 + bf16_hi(d.x) * v1, bf16_lo(d.y) * v0 + bf16_hi(d.y) * v1);
