@@ -60,7 +60,7 @@ extern "C" {
                                   preconditioner for the inner PCG (built
                                   once per mesh; meshes of <= 64 vertices
                                   keep block Jacobi). Smoother damping:
-                                  0.85 on the fine level, 1.0 on the coarse
+                                  0.85 on the fine level, 1.05 on the coarse
                                   levels; the environment variables
                                   MOF_AMG_OMEGA / MOF_AMG_OMEGA1, read when
                                   the hierarchy is built, override them */

@@ -13,8 +13,9 @@ struct AmgParams {
     float omega = 0.85f;            // damped block-Jacobi smoother, fine level (1.0 diverges on irregular meshes)
     // coarse levels' 3x3 block-Jacobi smoother: C3 / C2 / C5 / R3 PCG its per
     // timestep 19 / 23.4 / 16.5 / 110 at 0.85, 18 / 22.8 / 16 / 102 at 1.0,
-    // 17 / 21.5 / 15.2 / 103 at 1.1; 1.2 diverges on R3
-    float omega1 = 1.0f;
+    // 17.2 / 21.8 / - / 102.3 at 1.05, 17 / 21.5 / 15.2 / 104.6 at 1.1;
+    // 1.2 diverges on R3
+    float omega1 = 1.05f;
     // level-0 rows >= nown are a decomposed part's ghosts: the Galerkin lists
     // use an identity block on their diagonal and zero for every coupling
     // that touches them (the Dirichlet problem of the owned rows); -1: none
@@ -74,7 +75,7 @@ struct AmgDevice {
     bool built = false;
     int32_t cap = 0;
     int32_t nc = 0;  // coarsest dofs (dense)
-    float omega = 0.85f, omega1 = 1.0f;
+    float omega = 0.85f, omega1 = 1.05f;
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)

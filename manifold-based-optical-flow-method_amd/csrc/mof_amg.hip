@@ -9,7 +9,7 @@
 //                      symmetric sweep operator in registers (fp64, one
 //                      workgroup per system).
 // Each PCG iteration applies one symmetric V(1,1)-cycle to the residual r
-// (damped block Jacobi: w = 0.85 on level 0, w1 = 1.0 on the coarse levels):
+// (damped block Jacobi: w = 0.85 on level 0, w1 = 1.05 on the coarse levels):
 //   level 0 pre-smooth x0 = w D^-1 r is fused into k_pcg_update / k_pcg_init;
 //   per level l:  k_res0 / k_res3  r_l = b_l - A_l x_l, written in member
 //                                  order of the next level's aggregates
