@@ -8,19 +8,34 @@ aggregation-multigrid preconditioner, 1 x MI355X), plus the SpMV's achieved GB/s
 One "step" = one batch of B consecutive timesteps (assembly of a1/f + A for
 every timestep, batched PCG to ||f - A V|| <= 1e-8 ||f||, planar V written
 to HBM), inputs resident in HBM before the timed region. With N GPUs (one
-process per GPU, torchrun) each rank solves its own contiguous timesteps
-(weak scaling, no collective on the data path); value = all timesteps / the
-max-over-ranks wall time.
+process per GPU) each rank solves its own contiguous timesteps (no
+collective on the data path); value = all timesteps / the max-over-ranks
+wall time.
+
+  * weak scaling (default): every rank solves K batches of B timesteps;
+  * --fixed-timesteps T (strong scaling, config C4): one step = the whole
+    T-timestep job (5000 in BASELINE configs[3]) split into contiguous
+    k-ranges over the N ranks, as the reference's Pool splits it
+    (compute_optical_flow.py:157-177);
+  * --io host: the drop-in's path -- I in pageable host memory, V back into
+    host memory, one mof_solve_range call over all timed timesteps (the
+    PCIe-inclusive rate; value is never this line's unless asked for).
+
+--gpus N without a torchrun environment starts N local worker processes
+itself (torch.distributed.run, 127.0.0.1) before anything touches a GPU;
+under torchrun --gpus must equal WORLD_SIZE.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                     [--config C3] [--precision mixed|f64] [--precond amg|jacobi]
-                    [--no-cpu-baseline]
+                    [--fixed-timesteps T] [--io device|host] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -57,7 +72,32 @@ def parse():
     ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 64,
                     help="fraction of the triangle loop the CPU baseline times")
     ap.add_argument("--lambda_", type=float, default=0.01)
+    ap.add_argument("--fixed-timesteps", type=int, default=0,
+                    help="strong scaling: one step = this many timesteps split over the ranks")
+    ap.add_argument("--io", default="device", choices=["device", "host"],
+                    help="device: I/V resident in HBM; host: pageable numpy in and out (drop-in path)")
     return ap.parse_args()
+
+
+def self_launch(args):
+    """--gpus N > 1 outside torchrun: run N local ranks through
+    torch.distributed.run as a child process (this process never initialises
+    the GPU; nothing is re-exec'ed) and exit with its status. Under torchrun,
+    --gpus must match WORLD_SIZE."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, world))
+        return
+    if args.gpus <= 1:
+        return
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def pmc_traffic(key, kernel):
@@ -108,11 +148,16 @@ def cpu_baseline(p, t, n, a, lam, frac):
 
 def main():
     args = parse()
+    self_launch(args)
     from mofhip.dist import max_over_ranks, rank_env, rank_k_range, sum_over_ranks
     rank, world, local = rank_env()
     # MOF_BENCH_REHEARSE=1: every rank on GPU 0 over gloo -- exercises the
     # N-rank path on a 1-GPU box (RCCL refuses two ranks on one GPU)
     rehearse = os.environ.get("MOF_BENCH_REHEARSE") == "1"
+    # MOF_BENCH_DRYRUN=1 (CPU tests of the launcher / partition / reduction
+    # path only): no GPU, no solve -- each call returns empty statistics and
+    # the line says "dry_run"; never a measurement
+    dry = os.environ.get("MOF_BENCH_DRYRUN") == "1"
     if rehearse:
         local = 0
     precision = args.precision or ("f64" if args.config == "C2" else "mixed")
@@ -121,87 +166,154 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if rehearse:
+        if rehearse or dry:
             dist.init_process_group(backend="gloo")
         else:
+            torch.cuda.set_device(local)
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
-    from mofhip import DeviceMesh, synth
+    from mofhip import synth
 
     # --- one-time mesh build (reported separately, outside the metric) -----
     p, t, n, a = synth.mesh_for_config(args.config)
     N = len(p)
     t0 = time.perf_counter()
-    mesh = DeviceMesh(p, n, t, a, device=local)
-    info = mesh.info()
+    if dry:
+        mesh, info = None, {"nblocks": 0, "ms_geometry": 0.0, "ms_pattern": 0.0}
+    else:
+        from mofhip import DeviceMesh
+        mesh = DeviceMesh(p, n, t, a, device=local)
+        info = mesh.info()
     mesh_s = time.perf_counter() - t0
 
-    # --- this rank's synthetic signal, resident in HBM ----------------------
+    def sync():
+        if not dry:
+            torch.cuda.synchronize(dev)
+
+    # --- this rank's timesteps --------------------------------------------
     B = args.batch
-    steps_total = args.warmup + args.steps
-    K_rank = steps_total * B
-    k_off, _ = rank_k_range(rank, world, 0, world * K_rank)  # this rank's timesteps
-    # generated on the device: (K_rank + 1) x N f64 is 7.4 GB per rank at the
-    # default C3 sizes, which 8 ranks would otherwise hold in host memory
-    dev = torch.device("cuda", local)
+    strong = args.fixed_timesteps > 0
+    if strong:
+        # the fixed job, split over the ranks; a step solves all of it
+        k_off, k_end = rank_k_range(rank, world, 0, args.fixed_timesteps)
+        K_rank = k_end - k_off
+    else:
+        K_rank = (args.warmup + args.steps) * B
+        k_off, _ = rank_k_range(rank, world, 0, world * K_rank)
+    # synthetic signal rows k_off .. k_off + K_rank, generated on the device:
+    # (K_rank + 1) x N f64 is 7.4 GB per rank at the default C3 sizes, which
+    # 8 ranks would otherwise hold in host memory
+    dev = torch.device("cpu") if dry else torch.device("cuda", local)
     pts = torch.from_numpy(np.ascontiguousarray(p[:, :2])).to(dev)
     phi = torch.atan2(pts[:, 1], pts[:, 0])
     kk = k_off + torch.arange(K_rank + 1, dtype=torch.float64, device=dev)
     I_dev = torch.empty((K_rank + 1, N), dtype=torch.float64, device=dev)
-    for r0 in range(0, K_rank + 1, 256):
+    for r0 in range(0, (K_rank + 1) if not dry else 0, 256):
         r1 = min(K_rank + 1, r0 + 256)
         I_dev[r0:r1] = torch.sin(3.0 * phi[None, :] - 0.3 * kk[r0:r1, None])
     del pts, phi, kk
-    V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
+    host_io = args.io == "host"
+    I_host = V_host = None
+    if host_io:
+        I_host = I_dev.cpu().numpy()  # pageable, as S3's numpy array
+        del I_dev
+        I_dev = None
+    else:
+        V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(K_rank + 1, dtype=np.float64)
-    torch.cuda.synchronize(dev)
+    sync()
     precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
     opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol)
 
-    def step(s, timed):
-        return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), K_rank + 1, tk, s * B,
-                                       (s + 1) * B, args.lambda_, V_dev.data_ptr(), device=local,
-                                       time_spmv=timed, **opts)
+    kept = []  # host V of the timed calls, freed after the clock stops (the caller keeps its result)
 
-    for s in range(args.warmup):
-        step(s, False)
+    def solve(a, b, timed):
+        """timesteps [a, b) of this rank's rows"""
+        if dry:
+            return dict.fromkeys(("iterations", "failed", "recovered", "ms_spmv", "spmv_bytes", "spmv_launches",
+                                  "spmv_systems", "spmv_full_launches", "ms_spmv_full", "ms_assembly",
+                                  "ms_solve", "max_rel_residual", "outer_steps"), 0) | {"systems": b - a}
+        if host_io:
+            V, st = mesh.solve_range(I_host, tk, a, b, args.lambda_, device=local, time_spmv=timed, **opts)
+            if timed:
+                kept.append(V)
+            return st
+        return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), K_rank + 1, tk, a, b, args.lambda_,
+                                       V_dev.data_ptr(), device=local, time_spmv=timed, **opts)
+
+    if strong:
+        batches = [(a, min(a + B, K_rank)) for a in range(0, K_rank, B)]
+        warm = batches[:max(1, args.warmup)] if batches else []
+        if host_io:
+            step_calls = [(0, K_rank)]
+        else:
+            step_calls = batches
+        timed_calls = step_calls * args.steps
+    else:
+        warm = [(s * B, (s + 1) * B) for s in range(args.warmup)]
+        timed = [(s * B, (s + 1) * B) for s in range(args.warmup, args.warmup + args.steps)]
+        timed_calls = [(timed[0][0], timed[-1][1])] if host_io else timed
+        if host_io and warm:
+            warm = [(warm[0][0], warm[-1][1])]
+    for a_, b_ in warm:
+        solve(a_, b_, False)
 
     # --- timed region -------------------------------------------------------
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
-    agg = {"iterations": 0, "failed": 0, "ms_spmv": 0.0, "spmv_bytes": 0.0, "spmv_launches": 0,
-           "max_rel_residual": 0.0, "ms_assembly": 0.0, "ms_solve": 0.0}
-    for s in range(args.warmup, steps_total):
-        st = step(s, True)
-        for k in ("iterations", "failed", "ms_spmv", "spmv_bytes", "spmv_launches", "ms_assembly",
-                  "ms_solve"):
+    agg = {"iterations": 0, "failed": 0, "recovered": 0, "ms_spmv": 0.0, "spmv_bytes": 0.0, "spmv_launches": 0,
+           "spmv_systems": 0, "spmv_full_launches": 0, "ms_spmv_full": 0.0, "max_rel_residual": 0.0,
+           "ms_assembly": 0.0, "ms_solve": 0.0, "systems": 0}
+    for a_, b_ in timed_calls:
+        st = solve(a_, b_, True)
+        for k in ("iterations", "failed", "recovered", "ms_spmv", "spmv_bytes", "spmv_launches", "spmv_systems",
+                  "spmv_full_launches", "ms_spmv_full", "ms_assembly", "ms_solve", "systems"):
             agg[k] += st[k]
         agg["max_rel_residual"] = max(agg["max_rel_residual"], st["max_rel_residual"])
         agg["max_outer_steps"] = max(agg.get("max_outer_steps", 0), st["outer_steps"])
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
-    cdev = torch.device("cpu") if rehearse else dev
+    kept.clear()
+    cdev = torch.device("cpu") if (rehearse or dry) else dev
     elapsed = max_over_ranks(elapsed, dist, cdev)
     agg["failed"] = int(sum_over_ranks(agg["failed"], dist, cdev))
-    n_ts = world * args.steps * B
+    n_ts = int(sum_over_ranks(agg["systems"], dist, cdev))
     value = n_ts / elapsed
+    n_local = max(1, agg["systems"])
+    rank_ranges = None
+    if dry and dist:
+        got = [None] * world
+        dist.all_gather_object(got, [k_off, k_off + K_rank, agg["systems"]])
+        rank_ranges = got
+    elif dry:
+        rank_ranges = [[k_off, k_off + K_rank, agg["systems"]]]
 
-    # roofline of the dominant kernel (k_pcg_spmv), live over the timed region
+    # roofline of the dominant kernel (k_pcg_spmv), live over the timed region:
+    # every timed launch is charged with the systems it processed
     achieved = agg["spmv_bytes"] / (agg["ms_spmv"] * 1e-3) / 1e9 if agg["ms_spmv"] > 0 else 0.0
     kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
     traffic, traffic_src = pmc_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), kname)
+    sv = 4 if precision == "mixed" else 8
+    per_sys = info["nblocks"] * 4 * sv + N * 2 * sv * 5
+    nl = max(1, agg["spmv_launches"])
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": traffic_src, "kernel": kname,
-                "bytes_per_launch": round(agg["spmv_bytes"] / max(1, agg["spmv_launches"])),
-                "us_per_launch": round(1e3 * agg["ms_spmv"] / max(1, agg["spmv_launches"]), 2),
-                "launches": agg["spmv_launches"]}
+                "bytes_per_launch": round(agg["spmv_bytes"] / nl),
+                "bytes_per_system": per_sys, "shared_bytes_per_launch": info["nblocks"] * 4,
+                "systems_per_launch": round(agg["spmv_systems"] / nl, 2),
+                "us_per_launch": round(1e3 * agg["ms_spmv"] / nl, 2),
+                "launches": agg["spmv_launches"],
+                "full_launches": agg["spmv_full_launches"],
+                "us_per_full_launch": round(1e3 * agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]), 2),
+                "full_launch_frac": round((B * per_sys + info["nblocks"] * 4)
+                                          / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3)
+                                          / 1e9 / HBM_PEAK_GBS, 4) if agg["ms_spmv_full"] > 0 else None}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and not dry:
         cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac)
 
     if rank == 0:
@@ -211,27 +323,35 @@ def main():
             "value": round(value, 3), "unit": "timesteps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "f32" if precision == "mixed" else "f64",
             "data": "synthetic travelling wave sin(3 phi - 0.3 k), dt = 1, lambda = 0.01",
             "config": {"workload": CONFIG_NAMES[args.config], "vertices": N, "triangles": len(t),
-                       "timesteps_per_step": B, "timesteps_timed": n_ts, "precision": precision,
-                       "precond": opts["precond"],
-                       "rtol": args.rtol, "parallelism": "timestep shards x%d" % world},
+                       "timesteps_per_step": args.fixed_timesteps if strong else world * B,
+                       "timesteps_timed": n_ts, "batch": B, "precision": precision,
+                       "precond": opts["precond"], "rtol": args.rtol,
+                       "io": "host (pageable numpy I in, numpy V out; PCIe inclusive)" if host_io
+                             else "device (I and V resident in HBM)",
+                       "parallelism": "timestep shards x%d" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / (args.steps * B), 1),
-                       "failed": agg["failed"], "max_rel_residual": agg["max_rel_residual"],
+            "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / n_local, 1),
+                       "failed": agg["failed"], "recovered": agg["recovered"],
+                       "max_rel_residual": agg["max_rel_residual"],
                        "max_refinement_steps": agg.get("max_outer_steps", 0),
-                       "ms_assembly_per_timestep": round(agg["ms_assembly"] / (args.steps * B), 4),
-                       "ms_solve_per_timestep": round(agg["ms_solve"] / (args.steps * B), 4),
+                       "ms_assembly_per_timestep": round(agg["ms_assembly"] / n_local, 4),
+                       "ms_solve_per_timestep": round(agg["ms_solve"] / n_local, 4),
                        "mesh_build_s": round(mesh_s, 3), "mesh_geometry_ms": round(info["ms_geometry"], 3),
                        "mesh_pattern_ms": round(info["ms_pattern"], 3)},
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if dry:
+            line["dry_run"] = True
+            line["rank_ranges"] = rank_ranges
         print(json.dumps(line), flush=True)
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 

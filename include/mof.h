@@ -64,6 +64,15 @@ extern "C" {
                                   levels; the environment variables
                                   MOF_AMG_OMEGA / MOF_AMG_OMEGA1, read when
                                   the hierarchy is built, override them */
+#define MOF_NO_RECOVERY 16u    /* systems whose solve fails (breakdown,
+                                  divergence, stagnation, max_iter) are
+                                  NaN-filled at once. Default: they are
+                                  re-solved, alone, with block-Jacobi PCG in
+                                  the same precision (after a multigrid
+                                  solve) and then in fp64, and only a system
+                                  all of these fail is NaN-filled -- spsolve
+                                  is direct and always answers an SPD system
+                                  (compute_optical_flow.py:147) */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */
@@ -77,7 +86,10 @@ typedef struct mof_opts {
     uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI | MOF_TIME_SPMV | MOF_PRECOND_AMG */
     int32_t batch;         /* timesteps solved together per launch (0: auto =
                               256, fewer if device memory is short) */
-    int32_t max_iter;      /* PCG iterations per inner solve (0: 10000) */
+    int32_t max_iter;      /* PCG iterations per inner solve (0: 10000; 1000
+                              with MOF_PRECOND_AMG, whose inner solves take
+                              tens: more means a bad preconditioner, and
+                              the system goes to the recovery solves) */
     int32_t max_outer;     /* refinement steps, MOF_PREC_MIXED (0: 10) */
     double rtol;           /* stop at ||f - A V||_2 <= rtol ||f||_2 (0: 1e-8) */
     double inner_rtol;     /* MOF_PREC_MIXED inner PCG tolerance (0: 1e-4) */
@@ -97,7 +109,17 @@ typedef struct mof_stats {
     int64_t spmv_launches;    /* MOF_TIME_SPMV: PCG SpMV launches timed */
     double ms_spmv;           /* MOF_TIME_SPMV: summed SpMV launch time */
     double spmv_bytes;        /* MOF_TIME_SPMV: summed algorithmic bytes of
-                                 those launches */
+                                 those launches, each charged with the systems
+                                 it processed */
+    int64_t spmv_systems;     /* MOF_TIME_SPMV: systems processed, summed over
+                                 the timed launches (a system that converged
+                                 earlier in a chunk exits at once) */
+    int64_t spmv_full_launches; /* MOF_TIME_SPMV: launches in which every
+                                   system of the inner solve worked ... */
+    double ms_spmv_full;      /* ... and their summed time */
+    int32_t recovered;        /* systems the first solve failed and a recovery
+                                 solve (block Jacobi, then fp64) solved */
+    int32_t recovered_f64;    /* of those, solved by the fp64 recovery */
 } mof_stats;
 
 typedef struct mof_mesh_info {

@@ -8,11 +8,15 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <cstdio>
+#include <cstdlib>
 #include <functional>
+#include <future>
 #include <new>
 
 #include "mof_amg.h"
 #include "mof_dd.h"
+#include "mof_hostio.h"
 #include "mof_internal.h"
 
 namespace {
@@ -95,6 +99,62 @@ void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop
         indptr[r + 1] = (int32_t)nnz;
     }
     *nnz_out = nnz;
+}
+
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// Pinned ring, copy stream and the two device slots of a host-pointer solve
+// (mof_hostio.h); kept on the handle across calls.
+void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
+    if (!m->stage) {
+        m->stage = new mof::HostStage((size_t)env_int("MOF_STAGE_MB", 32) << 20, mof::stage_threads());
+        for (auto &e : m->hev) {
+            MOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            MOF_HIP(hipEventRecord(e, m->stage->stream()));  // every wait has a recorded event
+        }
+    }
+    for (int sl = 0; sl < 2; ++sl) {
+        if ((int64_t)m->hin[sl].n < in_elems) m->hin[sl].alloc(in_elems);
+        if ((int64_t)m->hout[sl].n < out_elems) m->hout[sl].alloc(out_elems);
+    }
+}
+
+// Systems of the batch whose solve failed are re-solved alone: with 2x2
+// block-Jacobi PCG in the same precision after a multigrid solve, then in
+// fp64 (no stagnation test, the full iteration budget); only what all of
+// them fail stays failed (NaN-filled by k_to_planar).
+void recover_failed(mof_mesh *m, int32_t nb, const mof::SolveParams &sp, int32_t user_max_iter, hipStream_t s,
+                    std::vector<uint8_t> &only, mof_stats &st) {
+    auto failed = [&](int32_t b) { return m->h_sysi[b * mof::kSysStride + mof::SI_FAILED] != 0; };
+    std::vector<uint32_t> passes;
+    if (sp.precision == MOF_PREC_MIXED && sp.amg) passes.push_back(MOF_PREC_MIXED);
+    if (sp.precision == MOF_PREC_MIXED) passes.push_back(MOF_PREC_F64);
+    std::vector<uint8_t> first(nb, 0);
+    for (int32_t b = 0; b < nb; ++b) first[b] = failed(b);
+    for (uint32_t prec : passes) {
+        int32_t n = 0;
+        for (int32_t b = 0; b < nb; ++b) n += (only[b] = failed(b));
+        if (!n) break;
+        mof::SolveParams rp = sp;
+        rp.precision = prec;
+        rp.amg = false;
+        rp.block_jacobi = true;
+        rp.stall = 0;
+        rp.fail_at_max_iter = false;
+        rp.time_spmv = false;
+        rp.max_iter = user_max_iter > 0 ? user_max_iter : 10000;
+        mof::ensure_workspace(m, nb, prec);
+        mof::launch_recovery_operator(m, nb, prec, s);
+        int32_t outer = 0;
+        st.iterations += mof::solve_batch(m, nb, rp, s, &outer, &st.max_iterations, nullptr, only.data());
+        for (int32_t b = 0; b < nb; ++b)
+            if (only[b] && !failed(b) && prec == MOF_PREC_F64) st.recovered_f64++;
+    }
+    for (int32_t b = 0; b < nb; ++b)
+        if (first[b] && !failed(b)) st.recovered++;
 }
 
 }  // namespace
@@ -265,6 +325,10 @@ int mof_mesh_destroy(mof_mesh *m) {
             if (m->h_sysi) (void)hipHostFree(m->h_sysi);
             if (m->h_sysd) (void)hipHostFree(m->h_sysd);
             for (auto e : m->spmv_events) (void)hipEventDestroy(e);
+            delete m->stage;
+            m->stage = nullptr;
+            for (auto &e : m->hev)
+                if (e) (void)hipEventDestroy(e);
             mof::amg_destroy(m->amg);
             m->amg = nullptr;
             if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -388,10 +452,15 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         sp.block_jacobi = sp.amg || !(o.flags & MOF_NO_BLOCK_JACOBI);
         sp.time_spmv = (o.flags & MOF_TIME_SPMV) != 0;
         mof::SpmvTiming timing;
-        sp.max_iter = o.max_iter > 0 ? o.max_iter : 10000;
+        sp.max_iter = o.max_iter > 0 ? o.max_iter : (sp.amg ? 1000 : 10000);
         sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
         sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
         sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
+        // a multigrid-preconditioned inner solve takes tens of iterations:
+        // one that stops improving, or hits max_iter, has a bad preconditioner
+        sp.stall = sp.amg ? env_int("MOF_PCG_STALL", 64) : 0;
+        sp.fail_at_max_iter = sp.amg;
+        const bool recovery = !(o.flags & MOF_NO_RECOVERY);
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
         if (!I2) I2 = I;
         DeviceGuard dg(m->device);
@@ -419,9 +488,57 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
             // level-0 smoother's bf16 copies)
             const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && mof::amg_build(m);
             if (amg) mof::amg_ensure(m, B);
+            // host pointers: one upload of the nb+1 rows when I2 is I (S3
+            // passes I_k twice), else nb rows of each
+            const bool shared_I = (I2 == I);
+            const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
+            if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B);
+            const int32_t nbat = (K + B - 1) / B;
+            auto bk = [&](int32_t j) { return k0 + j * B; };
+            auto bn = [&](int32_t j) { return std::min(B, k1 - bk(j)); };
+            // helper-thread steps of the host pipeline (copy stream): batch j's
+            // I rows into slot j&1 once batch j-2's assembly has read it, and
+            // batch j's V out of slot j&1 into V_out
+            // MOF_HOSTIO_VERBOSE: helper-thread and wait times on stderr
+            const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
+            double t_in = 0.0, t_out = 0.0, t_wait = 0.0;
+            const double t_call = now_ms();
+            auto stage_in = [&](int32_t j) {
+                const double t0 = now_ms();
+                struct Acc {
+                    double &t, t0;
+                    ~Acc() { t += now_ms() - t0; }
+                } acc{t_in, t0};
+                MOF_HIP(hipSetDevice(m->device));
+                const int32_t sl = j & 1, kj = bk(j), nb = bn(j);
+                hipStream_t cs = m->stage->stream();
+                MOF_HIP(hipStreamWaitEvent(cs, m->hev[2 + sl], 0));
+                if (shared_I) {
+                    m->stage->h2d(m->hin[sl].p, I + (int64_t)kj * N, sizeof(double) * N * (nb + 1));
+                } else {
+                    m->stage->h2d(m->hin[sl].p, I + (int64_t)kj * N, sizeof(double) * N * nb);
+                    m->stage->h2d(m->hin[sl].p + N * B, I2 + (int64_t)(kj + 1) * N, sizeof(double) * N * nb);
+                }
+                MOF_HIP(hipEventRecord(m->hev[sl], cs));
+            };
+            auto drain_out = [&](int32_t j) {
+                struct Acc {
+                    double &t, t0;
+                    ~Acc() { t += now_ms() - t0; }
+                } acc{t_out, now_ms()};
+                MOF_HIP(hipSetDevice(m->device));
+                const int32_t sl = j & 1;
+                m->stage->d2h(V_out + (int64_t)(bk(j) - k0) * 2 * N, m->hout[sl].p, sizeof(double) * 2 * N * bn(j),
+                              m->hev[4 + sl]);
+            };
             std::vector<double> dts(B);
-            for (int32_t k = k0; k < k1; k += B) {
-                const int32_t nb = std::min(B, k1 - k);
+            std::vector<uint8_t> only(B);
+            // declared after everything its tasks reference: its destructor
+            // waits for a task still running when an error unwinds
+            std::future<void> io;
+            if (!dev_io) io = std::async(std::launch::async, [&] { stage_in(0); });
+            for (int32_t j = 0; j < nbat; ++j) {
+                const int32_t k = bk(j), nb = bn(j), sl = j & 1;
                 for (int32_t b = 0; b < nb; ++b) dts[b] = t_k[k + b + 1] - t_k[k + b];
                 MOF_HIP(hipMemcpyAsync(w.dt.p, dts.data(), sizeof(double) * nb, hipMemcpyHostToDevice, s));
                 const double *I0p, *I1p;
@@ -429,26 +546,31 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                     I0p = I + (int64_t)k * N;
                     I1p = I2 + (int64_t)(k + 1) * N;
                 } else {
-                    MOF_HIP(hipMemcpyAsync(w.Ibuf.p, I + (int64_t)k * N, sizeof(double) * N * nb,
-                                           hipMemcpyHostToDevice, s));
-                    MOF_HIP(hipMemcpyAsync(w.Ibuf.p + N * B, I2 + (int64_t)(k + 1) * N,
-                                           sizeof(double) * N * nb, hipMemcpyHostToDevice, s));
-                    I0p = w.Ibuf.p;
-                    I1p = w.Ibuf.p + N * B;
+                    const double tw = now_ms();
+                    io.get();  // batch j staged, batch j-1 drained
+                    t_wait += now_ms() - tw;
+                    if (j + 1 < nbat || j > 0)
+                        io = std::async(std::launch::async, [&, j] {
+                            if (j + 1 < nbat) stage_in(j + 1);
+                            if (j > 0) drain_out(j - 1);
+                        });
+                    MOF_HIP(hipStreamWaitEvent(s, m->hev[sl], 0));
+                    I0p = m->hin[sl].p;
+                    I1p = shared_I ? I0p + N : I0p + N * B;
                 }
                 MOF_HIP(hipEventRecord(ev.e[0], s));
                 mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s, amg);
+                if (!dev_io) MOF_HIP(hipEventRecord(m->hev[2 + sl], s));
                 MOF_HIP(hipEventRecord(ev.e[1], s));
                 int32_t outer = 0;
                 st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
                 st.outer_steps = outer;
-                double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : w.Vbuf.p;
+                if (recovery) recover_failed(m, nb, sp, o.max_iter, s, only, st);
+                double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[sl].p;
                 mof::launch_to_planar(m, nb, Vdst, s);
+                if (!dev_io) MOF_HIP(hipEventRecord(m->hev[4 + sl], s));
                 MOF_HIP(hipEventRecord(ev.e[2], s));
-                if (!dev_io)
-                    MOF_HIP(hipMemcpyAsync(V_out + (int64_t)(k - k0) * 2 * N, w.Vbuf.p,
-                                           sizeof(double) * 2 * N * nb, hipMemcpyDeviceToHost, s));
-                MOF_HIP(hipStreamSynchronize(s));
+                MOF_HIP(hipEventSynchronize(ev.e[2]));
                 st.ms_assembly += ev.ms(0, 1);
                 st.ms_solve += ev.ms(1, 2);
                 for (int32_t b = 0; b < nb; ++b) {
@@ -458,11 +580,23 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 }
                 st.batches++;
             }
+            if (!dev_io) {
+                if (io.valid()) io.get();
+                drain_out(nbat - 1);
+                if (hostio_verbose)
+                    fprintf(stderr,
+                            "[mof hostio] K=%d B=%d: stage_in %.1f ms, drain %.1f ms, main waited %.1f ms, "
+                            "call %.1f ms\n",
+                            K, B, t_in, t_out, t_wait, now_ms() - t_call);
+            }
         }
         st.systems = K;
         st.spmv_launches = timing.launches;
         st.ms_spmv = timing.ms;
         st.spmv_bytes = timing.bytes;
+        st.spmv_systems = timing.systems;
+        st.spmv_full_launches = timing.full_launches;
+        st.ms_spmv_full = timing.ms_full;
         if (stats) *stats = st;
         if (st.failed) {
             nonconv = 1;

@@ -567,6 +567,20 @@ __global__ __launch_bounds__(kWG) void k_velocity_vectors(int32_t N, int32_t K, 
     }
 }
 
+// Recovery solve after a multigrid solve failed: the 2x2 block-Jacobi
+// inverses of the fp32 A (that assembly kept D^-1 only in bf16).
+__global__ __launch_bounds__(kWG) void k_dinv_from_A32(int32_t N, int64_t sell_nb, const int32_t *__restrict__ diag_pos,
+                                                       const float *__restrict__ A, float *__restrict__ dinv32) {
+    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t b = blockIdx.y;
+    if (i >= N) return;
+    const float4 d = reinterpret_cast<const float4 *>(A)[(int64_t)b * sell_nb + diag_pos[i]];
+    const double d0 = d.x, d1 = d.y, d2 = d.z, d3 = d.w;
+    const double det = d0 * d3 - d1 * d2;
+    reinterpret_cast<float4 *>(dinv32)[(int64_t)b * N + i] =
+        make_float4((float)(d3 / det), (float)(-d1 / det), (float)(-d2 / det), (float)(d0 / det));
+}
+
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + kWG - 1) / kWG)); }
 
 // Host-side guard before any launch: every device array a kernel indexes is
@@ -676,6 +690,26 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,
                                                      m->a2s64.p, w.u64.p, w.fc.p, bj, w.A64.p,
                                                      w.dinv64.p, w.dinv32.p, w.rhs.p);
+    MOF_HIP(hipGetLastError());
+}
+
+void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStream_t s) {
+    Workspace &w = m->ws;
+    check_mesh_arrays(m);
+    const int64_t snb = m->pat.sell_nb();
+    MOF_REQUIRE(B >= 1 && B <= w.cap && m->a2s_valid, "recovery: workspace / operator not prepared");
+    if (precision == MOF_PREC_MIXED) {
+        MOF_REQUIRE(w.A32.n >= 4 * (size_t)snb * B && w.dinv32.n >= 4 * (size_t)m->N * B,
+                    "recovery: fp32 A not assembled");
+        k_dinv_from_A32<<<dim3((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B), kWG, 0, s>>>(
+            m->N, snb, m->diag_pos.p, w.A32.p, w.dinv32.p);
+    } else {
+        MOF_REQUIRE(w.A64.n >= 4 * (size_t)snb * B, "recovery: fp64 A not allocated");
+        const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
+        k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
+                                                     m->cptr.p, m->clist.p, m->iw.p, m->a2s64.p, w.u64.p, w.fc.p,
+                                                     1, w.A64.p, w.dinv64.p, w.dinv32.p, w.rhs.p);
+    }
     MOF_HIP(hipGetLastError());
 }
 

@@ -124,11 +124,16 @@ struct Workspace {
 };
 
 // per-system scalar slots (Workspace::sysd / sysi)
-enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3 };
-enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_ITERS = 3 };
+//  SD_RR0 / SD_BEST: |r|^2 at the start of the inner solve / smallest so far
+//  SI_BEST_IT: iteration of SD_BEST (stagnation detector)
+//  SI_FAIL_IT / SI_FAIL_WHY: inner iteration and reason (FailWhy) of a failure
+enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST = 5 };
+enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_BEST_IT = 4, SI_FAIL_IT = 5, SI_FAIL_WHY = 6 };
+enum FailWhy { FW_BREAKDOWN = 1, FW_DIVERGED = 2, FW_STALLED = 3, FW_MAXITER = 4, FW_RESIDUAL = 5 };
 constexpr int kSysStride = 8;
 
 struct AmgDevice;  // mof_amg.h
+class HostStage;   // mof_hostio.h
 
 // Cross-part reduction layout of the PCG kernels: partial record of
 // (part, system b, workgroup w) at ((part * B + b) * nmax + w) * NV; rows
@@ -180,6 +185,13 @@ struct mof_mesh {
     std::vector<int32_t> iter_hint;
     // aggregation multigrid hierarchy (MOF_PRECOND_AMG), built on first use
     mof::AmgDevice *amg = nullptr;
+    // host-pointer solves: pinned staging ring + copy stream, and two device
+    // slots each for a batch's I rows and its planar V (double buffering);
+    // events: [0..1] I rows uploaded, [2..3] I rows consumed by the assembly,
+    // [4..5] V written
+    mof::HostStage *stage = nullptr;
+    mof::DevArray<double> hin[2], hout[2];
+    hipEvent_t hev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace mof {
@@ -211,9 +223,15 @@ void launch_singularities_compact(int32_t N, int32_t M, int32_t K, const void *c
 void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double *V, double *Vc,
                              double *speed, hipStream_t s);
 
+// Timed SpMV launches: each is charged with the systems it actually
+// processed (a system that converged, or failed, earlier in a chunk of
+// launches returns at once and moves no block bytes).
 struct SpmvTiming {
     int64_t launches = 0;
+    int64_t systems = 0;         // systems processed, summed over the launches
+    int64_t full_launches = 0;   // launches in which every system of the solve worked
     double ms = 0.0, bytes = 0.0;
+    double ms_full = 0.0;        // their summed time
 };
 
 // Algorithmic bytes of one k_pcg_spmv launch over `active` systems
@@ -227,11 +245,24 @@ struct SolveParams {
     bool amg;  // mixed precision only: multigrid V-cycle preconditioner
     int32_t max_iter, max_outer;
     double rtol, inner_rtol;
+    // stagnation window: an inner solve whose |r|^2 sets no new minimum for
+    // this many iterations fails (0: off)
+    int32_t stall = 0;
+    // an inner solve that ends at max_iter unconverged fails the system
+    // (instead of handing the partial correction to the next refinement step)
+    bool fail_at_max_iter = false;
 };
 // Solve the B assembled systems in the workspace; fills sysd/sysi.
 // Returns total inner iterations; sets *outer to the refinement steps used.
+// only (B flags, optional): re-solve just these systems; the others keep
+// their x64 and flags from the previous solve of the batch.
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
-                    int32_t *max_iters, SpmvTiming *timing);
+                    int32_t *max_iters, SpmvTiming *timing, const uint8_t *only = nullptr);
+// Operators a recovery solve needs that the first solve's assembly did not
+// write: with MOF_PREC_MIXED the fp32 2x2 block-Jacobi inverses from the fp32
+// A (the multigrid assembly keeps D^-1 in bf16 only); with MOF_PREC_F64 the
+// fp64 A and D^-1 (from the u / f terms the assembly left in the workspace).
+void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStream_t s);
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision);
 // aggregation multigrid preconditioner (mof_amg.hip)
 bool amg_build(mof_mesh *m);  // hierarchy from the mesh (once); false: mesh too small

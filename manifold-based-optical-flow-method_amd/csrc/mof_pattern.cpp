@@ -213,16 +213,6 @@ std::vector<int32_t> rcm_order(const Pattern &pat) {
         }
     }
     std::reverse(order.begin(), order.end());
-    // SELL-C-sigma: within windows of sigma consecutive rows, rows sorted by
-    // descending degree (stable), so each 64-row slice holds rows of similar
-    // length and pads little on meshes of irregular valence
-    if (const char *e = std::getenv("MOF_SELL_SIGMA")) {
-        const int32_t sigma = std::atoi(e);
-        if (sigma > 1)
-            for (int32_t w0 = 0; w0 < N; w0 += sigma)
-                std::stable_sort(order.begin() + w0, order.begin() + std::min(N, w0 + sigma),
-                                 [&](int32_t a, int32_t b) { return deg[a] > deg[b]; });
-    }
     for (int32_t k = 0; k < N; ++k) perm[order[k]] = k;
     return perm;
 }

@@ -74,7 +74,12 @@ struct PcgArgs {
     V omega;
     const uint2 *dh;       // ext (multigrid, fp32): the smoother's 2x2 D^-1, 4 bf16 [B][N]
     RedArgs red;           // partial-record layout; rows >= red.nown (ghosts) are not summed
+    int32_t stall;         // stagnation window in iterations (0: off)
 };
+
+// |r|^2 growth over the start of the inner solve taken as divergence (CG's
+// residual is not monotone, but 1e5 in norm is far past any transient)
+constexpr double kDiverge = 1e10;
 
 // Record of (this part, system b, workgroup w) in a partial array.
 __device__ __forceinline__ int64_t red_rec(const RedArgs &rd, int32_t B, int32_t b, int32_t w) {
@@ -228,6 +233,9 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol) {
     reduce_sys<2>(a.part_rzrr, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) {
         a.sysd[b * kSysStride + SD_TOL2] = rtol * rtol * v[1];
+        a.sysd[b * kSysStride + SD_RR0] = v[1];
+        a.sysd[b * kSysStride + SD_BEST] = v[1];
+        si[SI_BEST_IT] = 0;
         si[SI_CONV] = -1;
     }
 }
@@ -249,6 +257,12 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
         if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
             a.sysi[b * kSysStride + SI_CONV] = it;
         return;
+    }
+    // stagnation bookkeeping: one thread of the system's first row block (no
+    // other workgroup reads these slots; k_pcg_update reads them next launch)
+    if (!force && rb == 0 && threadIdx.x == 0 && cur[1] < a.sysd[b * kSysStride + SD_BEST]) {
+        a.sysd[b * kSysStride + SD_BEST] = cur[1];
+        a.sysi[b * kSysStride + SI_BEST_IT] = it;
     }
     V beta = 0;
     if (!FIRST) {
@@ -298,11 +312,24 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     if (cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) return;
     double pqv[1];
     reduce_sys<1>(a.part_pq, a.red, a.B, b, pqv, lds);
-    if (!(pqv[0] > 0.0) || !isfinite(pqv[0]) || !isfinite(cur[0])) {
-        // breakdown: A (or the preconditioner) is not SPD / singular
+    // Every workgroup of the system reduces the same partials, so all take
+    // the same decision: breakdown (p.q <= 0 or r.z <= 0: A or the
+    // preconditioner is not SPD, e.g. an indefinite V-cycle; non-finite
+    // values), divergence (|r|^2 grew kDiverge-fold), or stagnation (no new
+    // smallest |r|^2 for `stall` iterations).
+    int why = 0;
+    if (!(pqv[0] > 0.0) || !(cur[0] > 0.0) || !isfinite(pqv[0]) || !isfinite(cur[0]) || !isfinite(cur[1]))
+        why = FW_BREAKDOWN;
+    else if (cur[1] > kDiverge * a.sysd[b * kSysStride + SD_RR0])
+        why = FW_DIVERGED;
+    else if (a.stall > 0 && it - si[SI_BEST_IT] > a.stall)
+        why = FW_STALLED;
+    if (why) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
+            si[SI_FAIL_IT] = it;
+            si[SI_FAIL_WHY] = why;
         }
         return;
     }
@@ -420,6 +447,7 @@ __global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, cons
         if (!isfinite(rel)) {
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
+            si[SI_FAIL_WHY] = FW_RESIDUAL;
         } else if (rel <= rtol) {
             si[SI_ACTIVE] = 0;
         }
@@ -443,6 +471,20 @@ __global__ void k_mark_unconverged(int32_t B, int32_t *__restrict__ sysi) {
     if (sysi[b * kSysStride + SI_ACTIVE]) {
         sysi[b * kSysStride + SI_FAILED] = 1;
         sysi[b * kSysStride + SI_ACTIVE] = 0;
+        sysi[b * kSysStride + SI_FAIL_WHY] = FW_MAXITER;
+    }
+}
+
+// Systems still iterating when an inner solve ends at max_iter fail.
+__global__ void k_fail_running(int32_t B, int32_t it, int32_t *__restrict__ sysi) {
+    const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    int32_t *si = sysi + b * kSysStride;
+    if (si[SI_ACTIVE] && !si[SI_FAILED] && si[SI_CONV] < 0) {
+        si[SI_FAILED] = 1;
+        si[SI_ACTIVE] = 0;
+        si[SI_FAIL_IT] = it;
+        si[SI_FAIL_WHY] = FW_MAXITER;
     }
 }
 
@@ -496,6 +538,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.x0 = nullptr;
     a.omega = (V)0;
     a.dh = nullptr;
+    a.stall = 0;
     return a;
 }
 
@@ -507,13 +550,48 @@ void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
     MOF_HIP(hipStreamSynchronize(s));
 }
 
+// Longest first chunk of launches queued before the host looks at the flags.
+constexpr int32_t kMaxChunk = 256;
+
+// Systems of a chunk [it0, it0 + n) each timed SpMV launch processed: system
+// b works in launch it while it < last_b (SI_CONV = the launch that saw it
+// converged; a failure at update iteration f: f + 1), all n launches if it
+// is still running.
+void charge_chunk(const mof_mesh *m, int32_t B, const std::vector<int32_t> &running_at, int32_t it0,
+                  int32_t n, uint32_t precision, int32_t solve_systems, const std::vector<float> &ms,
+                  SpmvTiming *t) {
+    std::vector<int32_t> active(n, 0);
+    for (int32_t b = 0; b < B; ++b) {
+        if (!running_at[b]) continue;
+        const int32_t *si = m->h_sysi + b * kSysStride;
+        int32_t last = it0 + n;
+        if (si[SI_CONV] >= 0)
+            last = si[SI_CONV];
+        else if (si[SI_FAILED] && si[SI_FAIL_WHY] != FW_MAXITER)
+            last = si[SI_FAIL_IT] + 1;
+        for (int32_t c = 0; c < n && it0 + c < last; ++c) active[c]++;
+    }
+    for (int32_t c = 0; c < n; ++c) {
+        t->ms += ms[c];
+        t->launches++;
+        t->systems += active[c];
+        if (active[c]) t->bytes += spmv_launch_bytes(m, precision, active[c]);
+        if (active[c] == solve_systems) {
+            t->full_launches++;
+            t->ms_full += ms[c];
+        }
+    }
+}
+
 // Inner PCG on all active systems; returns iterations summed over systems.
 template <typename V>
 int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
-            double rtol, int32_t max_iter, hipStream_t s, int32_t *max_iters, uint32_t precision,
-            SpmvTiming *timing, int32_t *hint, bool amg) {
+            double rtol, const SolveParams &sp, hipStream_t s, int32_t *max_iters, SpmvTiming *timing,
+            int32_t *hint, bool amg) {
+    const int32_t max_iter = sp.max_iter;
     PcgArgs<V> a = make_args<V>(m, B, mat, dinv);
     a.ext = amg ? 1 : 0;
+    a.stall = sp.stall;
     if constexpr (sizeof(V) == 4) {
         if (amg) {
             AmgFine f = amg_fine(m);
@@ -535,32 +613,30 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     MOF_HIP(hipGetLastError());
     // systems active at the start of this solve: the host mirror is current
     // (reset by solve_batch, refreshed by every outer check)
-    std::vector<int32_t> was_active(B);
-    int32_t running = 0;
+    std::vector<int32_t> was_active(B), running_at(B);
+    int32_t solve_systems = 0;
     for (int32_t b = 0; b < B; ++b) {
         was_active[b] = m->h_sysi[b * kSysStride + SI_ACTIVE];
-        running += was_active[b];
+        solve_systems += was_active[b];
     }
+    running_at = was_active;
     // The first chunk runs as many iterations as the same solve of the
     // previous batch needed (timesteps of one run converge alike), so the
     // host usually synchronises once per inner solve; converged systems
     // retire on the device, so overshooting costs only early-exit launches.
     int32_t it = 0;
-    int32_t chunk = *hint > 0 ? *hint : 8;
+    int32_t chunk = *hint > 0 ? std::min(*hint, kMaxChunk) : 8;
     bool done = false;
     std::vector<hipEvent_t> &ev = m->spmv_events;
-    if (timing && (int32_t)ev.size() < 2 * chunk) {
-        const size_t old = ev.size();
-        ev.resize(2 * (size_t)std::max(chunk, 64));
-        for (size_t q = old; q < ev.size(); ++q) MOF_HIP(hipEventCreate(&ev[q]));
-    }
+    std::vector<float> ms;
     while (!done && it < max_iter) {
         const int32_t n = std::min(chunk, max_iter - it);
         if (timing && (int32_t)ev.size() < 2 * n) {
             const size_t old = ev.size();
-            ev.resize(2 * (size_t)n);
+            ev.resize(2 * (size_t)std::max(n, 64));
             for (size_t q = old; q < ev.size(); ++q) MOF_HIP(hipEventCreate(&ev[q]));
         }
+        const int32_t it0 = it;
         for (int32_t c = 0; c < n; ++c, ++it) {
             if (timing) MOF_HIP(hipEventRecord(ev[2 * c], s));
             if (it == 0)
@@ -574,41 +650,41 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
         if (timing) {
-            for (int32_t c = 0; c < n; ++c) {
-                float ms = 0.f;
-                MOF_HIP(hipEventElapsedTime(&ms, ev[2 * c], ev[2 * c + 1]));
-                timing->ms += ms;
-            }
-            timing->launches += n;
-            timing->bytes += n * spmv_launch_bytes(m, precision, running);
+            ms.assign(n, 0.f);
+            for (int32_t c = 0; c < n; ++c) MOF_HIP(hipEventElapsedTime(&ms[c], ev[2 * c], ev[2 * c + 1]));
+            charge_chunk(m, B, running_at, it0, n, sp.precision, solve_systems, ms, timing);
         }
         done = true;
-        running = 0;
         for (int32_t b = 0; b < B; ++b) {
             const int32_t *si = m->h_sysi + b * kSysStride;
-            if (si[SI_ACTIVE] && !si[SI_FAILED] && si[SI_CONV] < 0) {
-                done = false;
-                ++running;
-            }
+            running_at[b] = si[SI_ACTIVE] && !si[SI_FAILED] && si[SI_CONV] < 0;
+            if (running_at[b]) done = false;
         }
         chunk = 8;
     }
     if (!done) {
         // one more check launch so SI_CONV records systems converged at max_iter
         k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(a, it, 0);
+        if (sp.fail_at_max_iter) k_fail_running<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, it, a.sysi);
+        MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
     }
     int64_t total = 0;
-    int32_t slowest = 0;
+    int32_t slowest = 0, slowest_conv = 0;
     for (int32_t b = 0; b < B; ++b) {
         if (!was_active[b]) continue;
-        const int32_t c = m->h_sysi[b * kSysStride + SI_CONV];
-        const int32_t its = c >= 0 ? c : it;
+        const int32_t *si = m->h_sysi + b * kSysStride;
+        const int32_t c = si[SI_CONV];
+        const int32_t its = c >= 0 ? c : (si[SI_FAILED] && si[SI_FAIL_WHY] != FW_MAXITER ? si[SI_FAIL_IT] + 1 : it);
         total += its;
         slowest = std::max(slowest, its);
+        if (c >= 0) slowest_conv = std::max(slowest_conv, c);
     }
     *max_iters = std::max(*max_iters, slowest);
-    if (slowest > 0) *hint = slowest + 1;  // +1: convergence is seen by the launch after
+    // the next batch's first chunk: +1 because convergence is seen by the
+    // launch after; only converged systems count (a failed or capped solve
+    // must not queue max_iter launches before the next look at the flags)
+    if (slowest_conv > 0) *hint = std::min(slowest_conv + 1, kMaxChunk);
     return total;
 }
 
@@ -682,18 +758,32 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
 }
 
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
-                    int32_t *max_iters, SpmvTiming *timing) {
+                    int32_t *max_iters, SpmvTiming *timing, const uint8_t *only) {
     SpmvTiming *tm = sp.time_spmv ? timing : nullptr;
     Workspace &w = m->ws;
-    k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
-    MOF_HIP(hipGetLastError());
-    for (int32_t b = 0; b < B; ++b) {  // host mirror of the reset state
-        int32_t *si = m->h_sysi + b * kSysStride;
-        for (int k = 0; k < kSysStride; ++k) si[k] = 0;
-        si[SI_ACTIVE] = 1;
-        si[SI_CONV] = -1;
+    if (!only) {
+        k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
+        MOF_HIP(hipGetLastError());
+        for (int32_t b = 0; b < B; ++b) {  // host mirror of the reset state
+            int32_t *si = m->h_sysi + b * kSysStride;
+            for (int k = 0; k < kSysStride; ++k) si[k] = 0;
+            si[SI_ACTIVE] = 1;
+            si[SI_CONV] = -1;
+        }
+    } else {
+        // re-solve the selected systems from x = 0; the others stay retired
+        // with their solution, residual and flags (the host mirror is the
+        // state of the previous solve's last fetch)
+        for (int32_t b = 0; b < B; ++b) {
+            int32_t *si = m->h_sysi + b * kSysStride;
+            if (!only[b]) continue;
+            for (int k = 0; k < kSysStride; ++k) si[k] = 0;
+            si[SI_ACTIVE] = 1;
+            si[SI_CONV] = -1;
+        }
+        MOF_HIP(hipMemcpyAsync(w.sysi.p, m->h_sysi, sizeof(int32_t) * kSysStride * B, hipMemcpyHostToDevice, s));
     }
-    if (m->iter_hint.size() < 2 * 16) m->iter_hint.assign(2 * 16, 0);
+    if (m->iter_hint.size() < 3 * 16) m->iter_hint.assign(3 * 16, 0);
     const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && amg_build(m);
     if (amg) {
         amg_ensure(m, B);
@@ -707,15 +797,15 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     for (; o < sp.max_outer; ++o) {
         const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
         if (sp.precision == MOF_PREC_MIXED) {
-            iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol,
-                                sp.max_iter, s, max_iters, sp.precision, tm,
-                                &m->iter_hint[16 + std::min(o, 15)], amg);
+            // hints per (precision, preconditioner, refinement step)
+            iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol, sp, s,
+                                max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg);
             k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
                                                     w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
-                                 o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s, max_iters,
-                                 sp.precision, tm, &m->iter_hint[std::min(o, 15)], false);
+                                 o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
+                                 &m->iter_hint[std::min(o, 15)], false);
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
@@ -806,7 +896,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
     std::vector<int32_t> was_active(B);
     for (int32_t b = 0; b < B; ++b) was_active[b] = m0->h_sysi[b * kSysStride + SI_ACTIVE];
     int32_t it = 0;
-    int32_t chunk = *hint > 0 ? *hint : 8;
+    int32_t chunk = *hint > 0 ? std::min(*hint, kMaxChunk) : 8;
     bool done = false;
     auto spmv = [&](bool first, int32_t it_) {
         dd_halo(d, B, sizeof(V) == 4, 0, s);
@@ -841,16 +931,17 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
         fetch_flags(m0, B, s);
     }
     int64_t total = 0;
-    int32_t slowest = 0;
+    int32_t slowest = 0, slowest_conv = 0;
     for (int32_t b = 0; b < B; ++b) {
         if (!was_active[b]) continue;
         const int32_t c = m0->h_sysi[b * kSysStride + SI_CONV];
         const int32_t its = c >= 0 ? c : it;
         total += its;
         slowest = std::max(slowest, its);
+        if (c >= 0) slowest_conv = std::max(slowest_conv, c);
     }
     *max_iters = std::max(*max_iters, slowest);
-    if (slowest > 0) *hint = slowest + 1;
+    if (slowest_conv > 0) *hint = std::min(slowest_conv + 1, kMaxChunk);
     return total;
 }
 

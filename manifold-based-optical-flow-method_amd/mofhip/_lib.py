@@ -33,6 +33,7 @@ MOF_IO_DEVICE = 1
 MOF_NO_BLOCK_JACOBI = 2
 MOF_TIME_SPMV = 4
 MOF_PRECOND_AMG = 8
+MOF_NO_RECOVERY = 16
 MOF_CSV_ROUND_TRIP = 1
 MOF_COORDS_F32 = 32
 MOF_DD_STAGED = 64
@@ -81,6 +82,9 @@ class MofStats(ctypes.Structure):
         ("max_rel_residual", ctypes.c_double), ("ms_assembly", ctypes.c_double),
         ("ms_solve", ctypes.c_double), ("spmv_launches", ctypes.c_int64),
         ("ms_spmv", ctypes.c_double), ("spmv_bytes", ctypes.c_double),
+        ("spmv_systems", ctypes.c_int64), ("spmv_full_launches", ctypes.c_int64),
+        ("ms_spmv_full", ctypes.c_double), ("recovered", ctypes.c_int32),
+        ("recovered_f64", ctypes.c_int32),
     ]
 
     def as_dict(self):

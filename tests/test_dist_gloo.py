@@ -80,3 +80,52 @@ def test_shard_ranges_cover():
         assert all(r[i][1] == r[i + 1][0] for i in range(p - 1))
         sizes = [b - a for a, b in r]
         assert max(sizes) - min(sizes) <= 1
+
+
+def _bench_dry(*argv, env_extra=None):
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MOF_BENCH_DRYRUN="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), *argv], env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_weak_two_ranks():
+    """bench.py --gpus 2 outside torchrun starts two gloo ranks itself (the
+    launcher path the driver's --gpus N hits); each rank solves its own
+    contiguous k-range of K batches, the whole-job count is summed."""
+    line = _bench_dry("--gpus", "2", "--steps", "2", "--warmup", "1", "--config", "C2", "--batch", "8",
+                      "--no-cpu-baseline")
+    assert line["dry_run"] and line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["timesteps_timed"] == 2 * 2 * 8
+    (a0, b0, n0), (a1, b1, n1) = line["rank_ranges"]
+    assert (a0, b0, n0) == (0, 24, 16) and (a1, b1, n1) == (24, 48, 16)
+
+
+def test_bench_fixed_timesteps_strong_split():
+    """--fixed-timesteps T: the T-timestep job (BASELINE configs[3]: 5000)
+    split into contiguous ranges over the ranks; one step covers all of it."""
+    line = _bench_dry("--gpus", "2", "--steps", "1", "--warmup", "1", "--config", "C2", "--batch", "256",
+                      "--fixed-timesteps", "5000", "--no-cpu-baseline")
+    assert line["scaling"] == "strong" and line["config"]["timesteps_timed"] == 5000
+    assert [r[:2] for r in line["rank_ranges"]] == [[0, 2500], [2500, 5000]]
+    assert sum(r[2] for r in line["rank_ranges"]) == 5000
+
+
+def test_bench_gpus_must_match_world_size():
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MOF_BENCH_DRYRUN="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--no-cpu-baseline"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr

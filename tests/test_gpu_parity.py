@@ -187,23 +187,6 @@ def test_irregular_meshes_vs_oracle(kind):
             assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), (prec, k)
 
 
-def test_sell_sigma_order_vs_oracle(monkeypatch):
-    """Opt-in SELL-C-sigma row order (MOF_SELL_SIGMA) only
-    changes the internal order: assembly bit-exact, V within 1e-6."""
-    monkeypatch.setenv("MOF_SELL_SIGMA", "64")
-    p, t = synth.random_sphere(3000, 10.0, seed=3)
-    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
-    I = synth.travelling_wave(p, 3)
-    m = DeviceMesh(p, n, t, a)
-    a2, gw, e, iw = oracle.geometry(p, n, t, a)
-    assert_csr_equal(m.tocsr(), a2)
-    V, st = m.solve_range(I, np.arange(3.0), 0, 2, 0.01, precision="mixed")
-    assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
-    for k in range(2):
-        Vo = oracle.worker(k, a2, gw, e, iw, t, list(range(3)), a, 0.01, I[k], I[k + 1])
-        assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
-
-
 @pytest.mark.slow
 def test_jittered_32k_vs_oracle():
     """C2-size jittered mesh: bit-exact assembly and V vs spsolve."""

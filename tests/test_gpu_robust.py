@@ -1,0 +1,187 @@
+"""Solver robustness, SpMV accounting and the host-pointer pipeline (round 2).
+
+* A solve the reference would complete (spsolve is direct,
+  compute_optical_flow.py:147) must not end as NaN because a preconditioner
+  misbehaves: failed systems are re-solved alone with block Jacobi, then in
+  fp64 (include/mof.h MOF_NO_RECOVERY). Forced failures: a diverging
+  multigrid smoother, a refinement budget too small for the mixed path.
+* MOF_TIME_SPMV charges each SpMV launch with the systems it processed: the
+  systems summed over the timed launches equal the PCG iterations.
+* Host-pointer solves (the drop-in's path) run a double-buffered upload /
+  download pipeline; results are bit-identical to the device-pointer path.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_golden
+from mofhip import DeviceMesh, synth
+
+pytestmark = pytest.mark.gpu
+
+VTOL = 1e-6
+
+
+def _random_hull():
+    p, t = synth.random_sphere(3000, 10.0, seed=3)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    return p, t, n, a
+
+
+def _oracle_V(p, t, n, a, I, ks, lam=0.01):
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    tk = list(range(len(I)))
+    return [oracle.worker(k, a2, gw, e, iw, t, tk, a, lam, I[k], I[k + 1]) for k in ks]
+
+
+@pytest.fixture
+def diverging_smoother(monkeypatch):
+    # read when the hierarchy is built (first multigrid solve of a handle):
+    # fine-level block-Jacobi damping far past its divergence edge (1.0 on R3)
+    monkeypatch.setenv("MOF_AMG_OMEGA", "2.5")
+    monkeypatch.setenv("MOF_AMG_OMEGA1", "2.5")
+    yield
+
+
+def test_diverging_multigrid_recovers(diverging_smoother):
+    p, t, n, a = _random_hull()
+    I = synth.travelling_wave(p, 5)
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(5.0), 0, 4, 0.01, precision="mixed", precond="amg")
+    assert st["failed"] == 0, st
+    assert st["recovered"] >= 1, st  # the forced failure happened and was repaired
+    assert st["max_rel_residual"] <= 1e-8
+    for k, Vo in enumerate(_oracle_V(p, t, n, a, I, range(4))):
+        assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
+
+
+def test_diverging_multigrid_without_recovery_is_nan(diverging_smoother):
+    """MOF_NO_RECOVERY keeps the old contract: NaN-filled, reported failed,
+    and the detector ends the bad solve early (no 10^4-iteration grind)."""
+    p, t, n, a = _random_hull()
+    I = synth.travelling_wave(p, 3)
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(3.0), 0, 2, 0.01, precision="mixed", precond="amg", recovery=False)
+    assert st["failed"] == 2 and st["recovered"] == 0
+    assert np.isnan(V).all()
+    assert st["max_iterations"] <= 1000
+
+
+@pytest.mark.parametrize("precond", ["jacobi", "amg"])
+def test_recovery_reaches_fp64(precond):
+    """One refinement step cannot take the mixed path to 1e-8: every system
+    fails its first solve(s) and the fp64 recovery (inner tolerance rtol/2)
+    solves it; V matches spsolve."""
+    g = load_golden("G1_ico642")
+    I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+    V, st = m.solve_range(I, tk, 0, 6, lam, precision="mixed", precond=precond, max_outer=1)
+    assert st["failed"] == 0 and st["recovered"] == 6 and st["recovered_f64"] == 6, st
+    assert np.abs(V - g["V_k"][:6]).max() < VTOL
+
+
+@pytest.mark.parametrize("precision,precond", [("mixed", "amg"), ("mixed", "jacobi"), ("f64", "jacobi")])
+def test_spmv_accounting_systems_equal_iterations(precision, precond):
+    """Every timed SpMV launch is charged with the systems that worked in it:
+    summed over launches that is exactly the PCG iteration count."""
+    g = load_golden("G1_ico642")
+    T = 40
+    I = synth.travelling_wave(g["coordinates"], T)
+    m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+    _, st = m.solve_range(I, np.arange(float(T)), 0, T - 1, 0.01, precision=precision, precond=precond,
+                          batch=16, time_spmv=True)
+    assert st["failed"] == 0
+    assert st["spmv_systems"] == st["iterations"]
+    assert st["spmv_launches"] >= st["max_iterations"]
+    assert 0 < st["spmv_full_launches"] <= st["spmv_launches"]
+    assert 0 < st["ms_spmv_full"] <= st["ms_spmv"]
+    N = len(g["coordinates"])
+    info = m.info()
+    sv = 4 if precision == "mixed" else 8
+    per_sys = info["nblocks"] * 4 * sv + N * 2 * sv * 5
+    shared = info["nblocks"] * 4
+    lo = st["spmv_systems"] * per_sys
+    assert lo <= st["spmv_bytes"] <= lo + st["spmv_launches"] * shared
+
+
+@pytest.mark.parametrize("same_I2", [True, False])
+def test_host_pipeline_matches_device_path(same_I2):
+    """Host pointers over several batches (double-buffered copy stream,
+    pinned ring smaller than a batch) give the device-pointer path's bits."""
+    import torch
+    p, t, n, a = synth.mesh_for_config("C2")
+    T = 45
+    I = synth.travelling_wave(p, T)
+    I2 = I if same_I2 else np.ascontiguousarray(I[::-1] * 0.5 + 0.25)
+    tk = np.arange(float(T))
+    old = os.environ.get("MOF_STAGE_MB")
+    os.environ["MOF_STAGE_MB"] = "4"  # ring chunks far smaller than one batch's 20 MB
+    try:
+        m = DeviceMesh(p, n, t, a)
+        Vh, sh = m.solve_range(I, tk, 2, T - 1, 0.01, I2=I2, precision="mixed", precond="amg", batch=16)
+    finally:
+        if old is None:
+            os.environ.pop("MOF_STAGE_MB")
+        else:
+            os.environ["MOF_STAGE_MB"] = old
+    dev = torch.device("cuda", 0)
+    Id = torch.from_numpy(I).to(dev)
+    I2d = torch.from_numpy(I2).to(dev) if not same_I2 else Id
+    Vd = torch.empty((T - 3, 2 * len(p)), dtype=torch.float64, device=dev)
+    sd = m.solve_range_device(Id.data_ptr(), I2d.data_ptr(), T, tk, 2, T - 1, 0.01, Vd.data_ptr(),
+                              precision="mixed", precond="amg", batch=16)
+    assert sh["batches"] == 3 and sh["failed"] == 0 and sd["failed"] == 0
+    assert np.array_equal(Vh, Vd.cpu().numpy())
+    if not same_I2:  # timestep k pairs I[k] with I2[k+1] (compute_velocity_field's I_k, I_k_2)
+        a2, gw, e, iw = oracle.geometry(p, n, t, a)
+        Vk = oracle.worker(5, a2, gw, e, iw, t, list(tk), a, 0.01, I[5], I2[6])
+        assert np.abs(Vh[3] - Vk).max() < VTOL
+
+
+@pytest.mark.slow
+def test_c3_bench_config_vs_spsolve():
+    """The bench's exact configuration (C3 163,842 vertices, mixed + multigrid,
+    B = 256: 32 XCD system groups of 8, 8 of 32) against the reference's
+    spsolve on two sampled timesteps of the batch (north-star bar 1e-6)."""
+    from scipy.sparse.linalg import spsolve
+    p, t, n, a = synth.mesh_for_config("C3")
+    T = 257
+    I = synth.travelling_wave(p, T)
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(float(T)), 0, T - 1, 0.01, precision="mixed", precond="amg", batch=256)
+    assert st["batches"] == 1 and st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    for k in (0, 203):
+        Ao, fo = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
+        Vo = spsolve(Ao.tocsc(), fo)
+        err = np.abs(V[k] - Vo).max()
+        print("C3 B=256 timestep %d: max|V - V_spsolve| = %.3e (max|V| %.3f)" % (k, err, np.abs(Vo).max()))
+        assert err < VTOL, (k, err)
+
+
+@pytest.mark.slow
+def test_c5_640k_single_domain_and_decomposed():
+    """C5 (640,092 vertices) on the GPU: the mixed + multigrid solve meets the
+    fp64 residual bound and agrees with the fp64 solve; the 8-part in-process
+    decomposition agrees with the single-domain solve."""
+    from mofhip import DecomposedMesh
+    p, t, n, a = synth.mesh_for_config("C5")
+    I = synth.travelling_wave(p, 3)
+    tk = np.arange(3.0)
+    m = DeviceMesh(p, n, t, a)
+    Vm, sm = m.solve_range(I, tk, 0, 2, 0.01, precision="mixed", precond="amg", batch=2)
+    V64, s64 = m.solve_range(I, tk, 0, 2, 0.01, precision="f64", batch=2)
+    assert sm["failed"] == 0 and s64["failed"] == 0
+    assert sm["max_rel_residual"] <= 1e-8 and s64["max_rel_residual"] <= 1e-8
+    assert np.abs(Vm - V64).max() < VTOL
+    A, f = m.assemble(I[0], I[1], 1.0, 0.01)
+    r = f - A @ Vm[0]
+    assert np.linalg.norm(r) <= 1e-8 * np.linalg.norm(f) * 1.01
+    m.close()
+    dd = DecomposedMesh(p, n, t, a, 8, device=0)
+    Vd, sd = dd.solve_range(I, tk, 0, 2, 0.01, precision="mixed", batch=2)
+    dd.close()
+    assert sd["failed"] == 0
+    assert np.abs(Vd - Vm).max() < VTOL
