@@ -503,6 +503,8 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
             const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
             double t_in = 0.0, t_out = 0.0, t_wait = 0.0;
             const double t_call = now_ms();
+            mof::g_fetch_ms = 0.0;
+            mof::g_fetch_n = 0;
             auto stage_in = [&](int32_t j) {
                 const double t0 = now_ms();
                 struct Acc {
@@ -580,14 +582,17 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 }
                 st.batches++;
             }
+            if (dev_io && hostio_verbose)
+                fprintf(stderr, "[mof hostio] device K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n", K, B,
+                        now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
             if (!dev_io) {
                 if (io.valid()) io.get();
                 drain_out(nbat - 1);
                 if (hostio_verbose)
                     fprintf(stderr,
                             "[mof hostio] K=%d B=%d: stage_in %.1f ms, drain %.1f ms, main waited %.1f ms, "
-                            "call %.1f ms\n",
-                            K, B, t_in, t_out, t_wait, now_ms() - t_call);
+                            "call %.1f ms, %lld flag fetches %.1f ms\n",
+                            K, B, t_in, t_out, t_wait, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
             }
         }
         st.systems = K;

@@ -226,6 +226,10 @@ void launch_velocity_vectors(int32_t N, int32_t K, const double *e, const double
 // Timed SpMV launches: each is charged with the systems it actually
 // processed (a system that converged, or failed, earlier in a chunk of
 // launches returns at once and moves no block bytes).
+// host time spent in the flag fetches of the solver (diagnostics)
+extern thread_local double g_fetch_ms;
+extern thread_local int64_t g_fetch_n;
+
 struct SpmvTiming {
     int64_t launches = 0;
     int64_t systems = 0;         // systems processed, summed over the launches
