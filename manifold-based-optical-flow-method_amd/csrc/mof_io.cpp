@@ -184,6 +184,10 @@ struct Mapped {
 
 // [begin, end) of the data lines (after the header line)
 void data_region(const Mapped &f, const char *&b, const char *&e) {
+    if (f.n == 0) {  // empty file: nothing mapped
+        b = e = nullptr;
+        return;
+    }
     const char *nl = static_cast<const char *>(std::memchr(f.p, '\n', f.n));
     b = nl ? nl + 1 : f.p + f.n;
     e = f.p + f.n;
@@ -275,7 +279,9 @@ bool pandas_high_strtod(const char *p, const char *end, double &out) {
         if (q < end && (*q == '-' || *q == '+')) eneg = (*q++ == '-');
         int n = 0, ed = 0;
         while (ed < kMaxDigits && q < end && *q >= '0' && *q <= '9') {
-            n = n * 10 + (*q - '0');
+            // saturate: any |exponent| past 616 gives inf / 0 either way, and
+            // 17 digits would overflow an int
+            n = n < 100000000 ? n * 10 + (*q - '0') : n;
             ++ed;
             ++q;
         }

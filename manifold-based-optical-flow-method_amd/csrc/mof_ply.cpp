@@ -87,6 +87,9 @@ Ply parse_header(const char *path) {
         } else if (kw == "element") {
             Elem e;
             ss >> e.name >> e.count;
+            MOF_REQUIRE(!ss.fail() && e.count >= 0, "PLY: bad element count");
+            for (const Elem &o : ply.elems)
+                MOF_REQUIRE(o.name != e.name, "PLY: duplicate element " + e.name);
             ply.elems.push_back(e);
         } else if (kw == "property") {
             MOF_REQUIRE(!ply.elems.empty(), "PLY: property before element");
@@ -95,10 +98,12 @@ Ply parse_header(const char *path) {
             ss >> t;
             if (t == "list") {
                 ss >> p.count_type >> p.type >> p.name;
+                (void)type_size(p.count_type);
             } else {
                 p.type = t;
                 ss >> p.name;
             }
+            (void)type_size(p.type);  // unknown types are rejected here
             ply.elems.back().props.push_back(p);
         } else if (kw == "end_header") {
             ended = true;
@@ -107,6 +112,20 @@ Ply parse_header(const char *path) {
     }
     MOF_REQUIRE(ended, "PLY: no end_header");
     ply.body.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    // every record needs at least one byte per value (ascii: a digit; binary:
+    // the scalar / list-count sizes): element counts the body cannot hold
+    // are rejected before anything is allocated from them
+    const size_t nbody = ply.body.size();
+    size_t need = 0;
+    for (const Elem &e : ply.elems) {
+        size_t rec = 0;
+        for (const Prop &q : e.props)
+            rec += ply.fmt == Fmt::Ascii ? 1 : (size_t)type_size(q.list() ? q.count_type : q.type);
+        if (rec == 0) continue;
+        MOF_REQUIRE((uint64_t)e.count <= nbody / rec, "PLY: element " + e.name + " count exceeds the file body");
+        need += (size_t)e.count * rec;
+        MOF_REQUIRE(need <= nbody, "PLY: element counts exceed the file body");
+    }
     return ply;
 }
 
@@ -116,6 +135,14 @@ struct Reader {
     std::istringstream txt;
     explicit Reader(const Ply &p) : ply(p) {
         if (p.fmt == Fmt::Ascii) txt.str(std::string(p.body.begin(), p.body.end()));
+    }
+    // upper bound on the values still to be read (a list length must not exceed it)
+    size_t remaining() {
+        if (ply.fmt == Fmt::Ascii) {
+            const std::streampos at = txt.tellg();
+            return at < 0 ? 0 : ply.body.size() - (size_t)at;
+        }
+        return ply.body.size() - pos;
     }
     double scalar(const std::string &t) {
         if (ply.fmt == Fmt::Ascii) {
@@ -172,14 +199,19 @@ Surface read_ply(const char *path, bool want_data) {
         for (int64_t r = 0; r < e.count; ++r) {
             for (auto &p : e.props) {
                 if (p.list()) {
-                    const int64_t n = (int64_t)rd.scalar(p.count_type);
-                    std::vector<int64_t> ids(n);
-                    for (int64_t k = 0; k < n; ++k) ids[k] = (int64_t)rd.scalar(p.type);
+                    const double nd = rd.scalar(p.count_type);
+                    MOF_REQUIRE(nd >= 0.0 && nd <= (double)rd.remaining() && nd == std::floor(nd),
+                                "PLY: bad list length");
+                    const int64_t n = (int64_t)nd;
+                    std::vector<double> ids(n);
+                    for (int64_t k = 0; k < n; ++k) ids[k] = rd.scalar(p.type);
                     if (e.name == "face" && (p.name == "vertex_indices" || p.name == "vertex_index")) {
                         MOF_REQUIRE(n == 3, "PLY: only triangle faces are supported (S3 reshapes faces to (-1, 4))");
                         for (int64_t k = 0; k < 3; ++k) {
-                            MOF_REQUIRE(ids[k] >= 0 && ids[k] < s.N, "PLY: face index out of range");
-                            s.tri.push_back(ids[k]);
+                            // range-checked as a double, before the integer cast
+                            MOF_REQUIRE(ids[k] >= 0.0 && ids[k] < (double)s.N && ids[k] == std::floor(ids[k]),
+                                        "PLY: face index out of range");
+                            s.tri.push_back((int64_t)ids[k]);
                         }
                     }
                 } else {
