@@ -334,6 +334,28 @@ int mof_dd_unique_id(uint8_t *id /* MOF_DD_ID_BYTES */);
 int mof_dd_create_rank(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
                        int32_t N, int32_t M, int32_t nranks, const int32_t *part, int32_t rank,
                        const uint8_t *id, int32_t device, uint32_t flags, mof_dd **out);
+
+/* Host-staged transport (no RCCL): the same one-part-per-rank plans, pack /
+ * unpack kernels, segment order and all-gathers as the RCCL transport, with
+ * every exchange staged through host memory and carried by the caller's
+ * callbacks (e.g. torch.distributed over gloo). For hosts without RCCL
+ * between the ranks' devices, and to run the per-rank path of a P-part
+ * decomposition on one GPU (RCCL refuses two ranks on one device). Each
+ * callback returns 0 on success and is called by every rank in the same
+ * order. */
+typedef struct mof_dd_transport {
+    void *ctx;
+    /* every rank passes `bytes` at send; recv (nranks * bytes) receives all
+       contributions in rank order (send may alias its own slot of recv) */
+    int (*allgather)(void *ctx, const void *send, void *recv, int64_t bytes);
+    /* with each of the n peer ranks: send[k] (sbytes[k]) to peers[k] and
+       receive rbytes[k] from it into recv[k] */
+    int (*exchange)(void *ctx, int32_t n, const int32_t *peers, const void *const *send, const int64_t *sbytes,
+                    void *const *recv, const int64_t *rbytes);
+} mof_dd_transport;
+int mof_dd_create_rank_host(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
+                            int32_t N, int32_t M, int32_t nranks, const int32_t *part, int32_t rank,
+                            const mof_dd_transport *transport, int32_t device, uint32_t flags, mof_dd **out);
 int mof_dd_destroy(mof_dd *dd);
 int mof_dd_get_info(const mof_dd *dd, mof_dd_info *info);
 

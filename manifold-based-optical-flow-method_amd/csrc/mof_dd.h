@@ -82,6 +82,11 @@ struct mof_dd {
     // RCCL transport (rank >= 0)
     mof::RcclApi *nccl = nullptr;
     void *comm = nullptr;
+    // host-staged transport (rank >= 0, mof_dd_create_rank_host): the caller's
+    // callbacks over host staging buffers
+    bool hosted = false;
+    mof_dd_transport host{};
+    std::vector<char> hsend, hrecv;
     // pack -> exchange -> unpack (RCCL, or in-process with MOF_DD_STAGED):
     // entries {row, segment offset, segment rows, -} of the local parts,
     // concatenated; part l's entries start at send_base[l] / recv_base[l] and

@@ -191,8 +191,34 @@ inline unsigned blocks(int64_t n) { return (unsigned)((n + kWG - 1) / kWG); }
 
 // ---- transport hooks ---------------------------------------------------------
 
+namespace {
+
+void host_check(int rc, const char *what) {
+    if (rc != 0) throw Error{MOF_E_HIP, std::string("host transport: ") + what + " failed (" + std::to_string(rc) + ")"};
+}
+
+// host-staged all-gather of `per` elements of esz bytes at base + per*rank
+// into base[0 .. P*per) of every rank
+void host_allgather(mof_dd *d, void *base, size_t per, size_t esz, hipStream_t s) {
+    const size_t bytes = per * esz, all = bytes * (size_t)d->P;
+    if (d->hrecv.size() < all) d->hrecv.resize(all);
+    char *h = d->hrecv.data();
+    MOF_HIP(hipMemcpyAsync(h + bytes * d->rank, static_cast<char *>(base) + bytes * d->rank, bytes,
+                           hipMemcpyDeviceToHost, s));
+    MOF_HIP(hipStreamSynchronize(s));
+    host_check(d->host.allgather(d->host.ctx, h + bytes * d->rank, h, (int64_t)bytes), "allgather");
+    MOF_HIP(hipMemcpyAsync(base, h, all, hipMemcpyHostToDevice, s));
+    MOF_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace
+
 void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s) {
     if (d->rank < 0 || d->P == 1) return;  // in-process: one shared array
+    if (d->hosted) {
+        host_allgather(d, base, per_part, sizeof(double), s);
+        return;
+    }
     nccl_check(d->nccl,
                d->nccl->all_gather(base + per_part * (size_t)d->rank, base, per_part, ncclFloat64, static_cast<ncclComm_t>(d->comm), s),
                "ncclAllGather(partials)");
@@ -239,7 +265,30 @@ void dd_halo(mof_dd *d, int32_t B, bool f32, int which, hipStream_t s) {
                                                            reinterpret_cast<double *>(sptr(l, 0)));
     }
     MOF_HIP(hipGetLastError());
-    if (d->rank >= 0) {
+    if (d->rank >= 0 && d->hosted) {
+        // the rank's packed segments to the host, one exchange call with all
+        // neighbours, the received segments back to the device
+        const DdPart &D = d->plan.parts[d->rank];
+        const size_t sb = 2 * (size_t)B * D.send_idx.size() * esz, rb = 2 * (size_t)B * D.n_ghost * esz;
+        if (d->hsend.size() < sb) d->hsend.resize(sb);
+        if (d->hrecv.size() < rb) d->hrecv.resize(rb);
+        if (sb) MOF_HIP(hipMemcpyAsync(d->hsend.data(), sptr(0, 0), sb, hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipStreamSynchronize(s));
+        const size_t nn = D.nbr.size();
+        std::vector<const void *> sp(nn);
+        std::vector<void *> rp(nn);
+        std::vector<int64_t> sc(nn), rc(nn);
+        for (size_t k = 0; k < nn; ++k) {
+            sp[k] = d->hsend.data() + 2 * (size_t)B * D.send_off[k] * esz;
+            sc[k] = (int64_t)(2 * (size_t)B * (D.send_off[k + 1] - D.send_off[k]) * esz);
+            rp[k] = d->hrecv.data() + 2 * (size_t)B * D.recv_off[k] * esz;
+            rc[k] = (int64_t)(2 * (size_t)B * (D.recv_off[k + 1] - D.recv_off[k]) * esz);
+        }
+        host_check(d->host.exchange(d->host.ctx, (int32_t)nn, D.nbr.data(), sp.data(), sc.data(), rp.data(), rc.data()),
+                   "exchange");
+        if (rb) MOF_HIP(hipMemcpyAsync(rptr(0, 0), d->hrecv.data(), rb, hipMemcpyHostToDevice, s));
+        MOF_HIP(hipStreamSynchronize(s));
+    } else if (d->rank >= 0) {
         const DdPart &D = d->plan.parts[d->rank];
         const ncclDataType_t dt = f32 ? ncclFloat32 : ncclFloat64;
         RcclApi *a = d->nccl;
@@ -307,7 +356,9 @@ void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s) {
                                                                          m->ws.sysi.p, d->vgather.p + per * p);
     }
     MOF_HIP(hipGetLastError());
-    if (d->rank >= 0 && d->P > 1)
+    if (d->rank >= 0 && d->P > 1 && d->hosted)
+        host_allgather(d, d->vgather.p, per, sizeof(double), s);
+    else if (d->rank >= 0 && d->P > 1)
         nccl_check(d->nccl, d->nccl->all_gather(d->vgather.p + per * d->rank, d->vgather.p, per, ncclFloat64,
                                                 static_cast<ncclComm_t>(d->comm), s),
                    "ncclAllGather(V)");
@@ -585,6 +636,37 @@ int mof_dd_create_rank(const double *xyz, const double *nrm, const int32_t *tri,
             ncclComm_t comm = nullptr;
             mof::nccl_check(d->nccl, d->nccl->comm_init_rank(&comm, nranks, u, rank), "ncclCommInitRank");
             d->comm = comm;
+            dd_setup(d, xyz, nrm, tri, area, part);
+        } catch (...) {
+            dd_free(d);
+            throw;
+        }
+        *out = d;
+    });
+}
+
+int mof_dd_create_rank_host(const double *xyz, const double *nrm, const int32_t *tri, const double *area,
+                            int32_t N, int32_t M, int32_t nranks, const int32_t *part, int32_t rank,
+                            const mof_dd_transport *transport, int32_t device, uint32_t flags, mof_dd **out) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(out && transport && transport->allgather && transport->exchange, "NULL argument");
+        *out = nullptr;
+        check_mesh_args(xyz, nrm, tri, area, N, M, nranks, part);
+        MOF_REQUIRE(rank >= 0 && rank < nranks, "rank out of range");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DevGuard g(device);
+        auto *d = new mof_dd();
+        d->N = N;
+        d->M = M;
+        d->P = nranks;
+        d->device = device;
+        d->flags = flags;
+        d->rank = rank;
+        d->hosted = true;
+        d->host = *transport;
+        try {
             dd_setup(d, xyz, nrm, tri, area, part);
         } catch (...) {
             dd_free(d);

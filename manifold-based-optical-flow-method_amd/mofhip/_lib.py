@@ -49,7 +49,7 @@ EXPORTS = (
     "mof_point_normals", "mof_cell_areas", "mof_singularities", "mof_amg_probe",
     "mof_partition_rcb", "mof_dd_plan_info", "mof_dd_create", "mof_dd_unique_id",
     "mof_dd_create_rank", "mof_dd_destroy", "mof_dd_get_info", "mof_dd_solve_range",
-    "mof_singularities_compact", "mof_xcd_map_check",
+    "mof_singularities_compact", "mof_xcd_map_check", "mof_dd_create_rank_host",
 )
 
 
@@ -111,6 +111,16 @@ class MofDdInfo(ctypes.Structure):
 
 MOF_DD_ID_BYTES = 128
 
+# mof_dd_transport callbacks
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64))
+
+
+class MofDdTransport(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("exchange", EXCHANGE_FN)]
+
 _lib = None
 _lock = threading.Lock()
 
@@ -171,6 +181,8 @@ def lib():
             "mof_dd_unique_id": ([P], ctypes.c_int),
             "mof_dd_create_rank": ([P, P, P, P, i32, i32, i32, P, i32, P, i32, u32, P],
                                    ctypes.c_int),
+            "mof_dd_create_rank_host": ([P, P, P, P, i32, i32, i32, P, i32, P, i32, u32, P],
+                                        ctypes.c_int),
             "mof_dd_destroy": ([P], ctypes.c_int),
             "mof_dd_get_info": ([P, P], ctypes.c_int),
             "mof_dd_solve_range": ([P, P, P, P, i32, i32, i32, f64, P, P, P], ctypes.c_int),

@@ -9,7 +9,10 @@ timestep. Two transports (include/mof.h, ``mof_dd_*``):
   (in-process halo gather, shared partial sums);
 * :class:`DecomposedMesh` with ``group=`` -- one part per rank of a
   ``torch.distributed`` job (one process per GPU), halo and scalar reductions
-  over RCCL; rank 0 makes the RCCL id and ``group`` broadcasts it.
+  over RCCL; rank 0 makes the RCCL id and ``group`` broadcasts it;
+* the same with ``transport="host"`` -- the per-rank plans and pack / unpack
+  kernels of the RCCL transport, every exchange staged through host memory
+  and carried by ``group`` itself (gloo): no RCCL, and ranks may share a GPU.
 
 Both return V in the reference's planar layout and caller order, like
 :meth:`DeviceMesh.solve_range` (compute_optical_flow.py:147, :190-191).
@@ -47,16 +50,71 @@ def plan_info(triangles, N: int, part) -> dict:
     return out
 
 
+class HostTransport:
+    """mof_dd_transport over a torch.distributed group (gloo, CPU tensors):
+    the all-gather of partial records / owned V and the neighbour exchange of
+    packed halo segments, called from inside the solver loop."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self._dist, self._torch, self.group = dist, torch, group
+        self.world = dist.get_world_size(group)
+        self._ag = L.ALLGATHER_FN(self._allgather)
+        self._ex = L.EXCHANGE_FN(self._exchange)
+        self.struct = L.MofDdTransport(None, self._ag, self._ex)
+
+    def _peer(self, r):
+        g = self.group
+        if g is None or not hasattr(self._dist, "get_global_rank"):
+            return int(r)
+        return self._dist.get_global_rank(g, int(r))
+
+    def _allgather(self, ctx, send, recv, nbytes):
+        try:
+            t = self._torch
+            src = t.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=t.uint8)
+            out = [t.empty(nbytes, dtype=t.uint8) for _ in range(self.world)]
+            self._dist.all_gather(out, src, group=self.group)
+            for r, o in enumerate(out):
+                ctypes.memmove(recv + r * nbytes, o.data_ptr(), nbytes)
+            return 0
+        except Exception:  # reported as a status to the library
+            return 1
+
+    def _exchange(self, ctx, n, peers, send, sbytes, recv, rbytes):
+        try:
+            t = self._torch
+            reqs, bufs = [], []
+            for k in range(n):
+                if sbytes[k]:
+                    st = t.frombuffer(bytearray(ctypes.string_at(send[k], sbytes[k])), dtype=t.uint8)
+                    reqs.append(self._dist.isend(st, self._peer(peers[k]), group=self.group))
+                if rbytes[k]:
+                    rt = t.empty(rbytes[k], dtype=t.uint8)
+                    bufs.append((k, rt))
+                    reqs.append(self._dist.irecv(rt, self._peer(peers[k]), group=self.group))
+            for q in reqs:
+                q.wait()
+            for k, rt in bufs:
+                ctypes.memmove(recv[k], rt.data_ptr(), rbytes[k])
+            return 0
+        except Exception:
+            return 1
+
+
 class DecomposedMesh:
     """One mesh decomposed into ``nparts`` vertex parts (RCB unless ``part``
     is given). Without ``group`` every part lives in this process on
     ``device``; with a torch.distributed ``group`` this rank drives part
     ``group.rank()`` on ``device`` and ``nparts`` must equal the group size.
     ``staged`` (in-process only): exchange through the pack / copy / unpack
-    kernels of the RCCL transport (a one-GPU rehearsal of that path)."""
+    kernels of the RCCL transport (a one-GPU rehearsal of that path).
+    ``transport`` (with ``group``): "rccl" (default) or "host" (host-staged
+    exchanges over ``group``, see :class:`HostTransport`)."""
 
     def __init__(self, coordinates, normals, triangles, areas, nparts: int, device: int = 0,
-                 part=None, group=None, rank=None, staged: bool = False):
+                 part=None, group=None, rank=None, staged: bool = False, transport: str = "rccl"):
         coords = np.asarray(coordinates)
         tri = np.asarray(triangles)
         if coords.ndim != 2 or coords.shape[1] != 3 or tri.ndim != 2 or tri.shape[1] != 3:
@@ -88,6 +146,16 @@ class DecomposedMesh:
             r = dist.get_rank(group) if rank is None else int(rank)
             if dist.get_world_size(group) != self.nparts:
                 raise ValueError("nparts must equal the group size (one part per rank)")
+            if transport == "host":
+                self._transport = HostTransport(group)
+                L.check(L.lib().mof_dd_create_rank_host(
+                    L.ptr(self._xyz), L.ptr(self._nrm), L.ptr(self._tri), L.ptr(self._area), self.N, self.M,
+                    self.nparts, pp, r, ctypes.byref(self._transport.struct), self.device, flags,
+                    ctypes.byref(h)))
+                self._h = h
+                return
+            if transport != "rccl":
+                raise ValueError("transport must be 'rccl' or 'host'")
             ident = np.zeros(L.MOF_DD_ID_BYTES, np.uint8)
             if r == 0:
                 L.check(L.lib().mof_dd_unique_id(L.ptr(ident)))
