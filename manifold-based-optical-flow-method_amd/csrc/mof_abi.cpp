@@ -83,9 +83,11 @@ void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop
         const int32_t io = r % N, al = r / N;
         const int32_t i = m->perm[io];
         row.clear();
+        const int32_t td = (int32_t)(std::lower_bound(P.vcol.begin() + P.vptr[i], P.vcol.begin() + P.vptr[i + 1], i) -
+                                     (P.vcol.begin() + P.vptr[i]));
         for (int32_t p = P.vptr[i], t = 0; p < P.vptr[i + 1]; ++p, ++t)
             row.emplace_back(m->inv[P.vcol[p]],
-                             (int64_t)P.sell_off[i >> 6] + (int64_t)t * mof::kSlice + (i & 63));
+                             (int64_t)P.sell_off[i >> 6] + (int64_t)mof::sell_slot(t, td) * mof::kSlice + (i & 63));
         std::sort(row.begin(), row.end());
         for (int half = 0; half < 2; ++half) {  // columns j, then j + N
             for (const auto &cp : row) {

@@ -112,14 +112,18 @@ void sell_layout(AmgLevel &L) {
         const int32_t w = (L.sell_off[s + 1] - L.sell_off[s]) / kSlice;
         for (int32_t l = 0; l < kSlice; ++l) {
             const int32_t i = s * kSlice + l;
+            int32_t td = 0;  // diagonal first in every row (sell_slot)
+            if (i < n)
+                while (td < L.vptr[i + 1] - L.vptr[i] - 1 && L.vcol[L.vptr[i] + td] != i) ++td;
             for (int32_t t = 0; t < w; ++t) {
                 const int64_t pos = L.sell_off[s] + (int64_t)t * kSlice + l;
                 int32_t c = std::min(i, n - 1);
                 if (i < n) {
                     const int32_t deg = L.vptr[i + 1] - L.vptr[i];
                     if (t < deg) {
-                        c = L.vcol[L.vptr[i] + t];
-                        L.sell_blk[pos] = L.vptr[i] + t;
+                        const int32_t tb = sell_block(t, td);
+                        c = L.vcol[L.vptr[i] + tb];
+                        L.sell_blk[pos] = L.vptr[i] + tb;
                         if (c == i) L.diag_pos[i] = (int32_t)pos;
                     } else {
                         c = i;

@@ -141,6 +141,8 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
     const int32_t i = blockIdx.x * kWG + threadIdx.x;
     if (i >= N) return;
     const double *ei = e + 6 * (int64_t)i;
+    int32_t td = 0;
+    while (vcol[vptr[i] + td] != i) ++td;
     for (int32_t p = vptr[i], t = 0; p < vptr[i + 1]; ++p, ++t) {
         const int32_t j = vcol[p];
         const double *ej = e + 6 * (int64_t)j;
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] += ee[q] * gg * A;
         }
-        double *o = a2 + 4 * sell_pos(sell_off, i, t);
+        double *o = a2 + 4 * sell_pos(sell_off, i, sell_slot(t, td));
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = acc[q];
     }

@@ -71,6 +71,16 @@ struct DevArray {
     size_t bytes() const { return n * sizeof(T); }
 };
 
+// SELL slot of block t (vcol order) of a row whose diagonal block is its
+// td-th: the diagonal goes first, so each wave of a per-position kernel (one
+// slot of 64 rows) holds only diagonal or only off-diagonal blocks -- the
+// diagonal ones fold every incident triangle (plus f and D^-1 in the
+// assembly), the others two. Also for the coarse multigrid levels.
+__host__ __device__ inline int32_t sell_slot(int32_t t, int32_t td) { return t == td ? 0 : (t < td ? t + 1 : t); }
+__host__ __device__ inline int32_t sell_block(int32_t slot, int32_t td) {
+    return slot == 0 ? td : (slot <= td ? slot - 1 : slot);
+}
+
 // Host-side sparsity structures, built once per mesh (mof_pattern.cpp).
 struct Pattern {
     int32_t N = 0, M = 0;

@@ -104,25 +104,25 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat, const
         int32_t w = (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice;
         for (int32_t l = 0; l < kSlice; ++l) {
             int32_t i = s * kSlice + l;
-            for (int32_t t = 0; t < w; ++t) {
+            int32_t td = 0;  // the diagonal's index in the row (vcol order)
+            if (i < N)
+                td = (int32_t)(std::lower_bound(pat.vcol.begin() + pat.vptr[i], pat.vcol.begin() + pat.vptr[i + 1], i) -
+                               (pat.vcol.begin() + pat.vptr[i]));
+            for (int32_t t = 0; t < w; ++t) {  // slot t: diagonal first (sell_slot)
                 int32_t c = 0;
                 const int64_t pos = pat.sell_off[s] + (int64_t)t * kSlice + l;
                 if (i < N) {
                     int32_t deg = pat.vptr[i + 1] - pat.vptr[i];
-                    c = t < deg ? pat.vcol[pat.vptr[i] + t] : i;
-                    if (t < deg) pat.sell_blk[pos] = pat.vptr[i] + t;
+                    const int32_t tb = sell_block(t, td);
+                    c = t < deg ? pat.vcol[pat.vptr[i] + tb] : i;
+                    if (t < deg) pat.sell_blk[pos] = pat.vptr[i] + tb;
                 }
                 pat.sell_col[pos] = c;
             }
         }
     }
     pat.diag_pos.assign(N, 0);
-    for (int32_t i = 0; i < N; ++i) {
-        int32_t t = (int32_t)(std::lower_bound(pat.vcol.begin() + pat.vptr[i],
-                                               pat.vcol.begin() + pat.vptr[i + 1], i) -
-                              (pat.vcol.begin() + pat.vptr[i]));
-        pat.diag_pos[i] = pat.sell_off[i / kSlice] + t * kSlice + (i % kSlice);
-    }
+    for (int32_t i = 0; i < N; ++i) pat.diag_pos[i] = pat.sell_off[i / kSlice] + (i % kSlice);  // slot 0
 
     // vertex -> incident (triangle, corner) in triangle order, SELL-64
     std::vector<int32_t> tdeg(N, 0);
