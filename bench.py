@@ -113,6 +113,22 @@ def pmc_traffic(key, kernel):
         return None, None
 
 
+def step_traffic(key, value):
+    """Whole-step HBM traffic from the committed PMC passes of this
+    configuration: every dispatch's FETCH_SIZE (x2) + WRITE_SIZE summed over
+    the profiled run, per timestep; at this line's rate that is the achieved
+    whole-step bandwidth (all kernels, not only the SpMV)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        run = json.load(open(path))[key]["run"]
+    except (OSError, ValueError, KeyError):
+        return None
+    bw = run["hbm_bytes_per_timestep"] * value / 1e9
+    return {"hbm_bytes_per_timestep": round(run["hbm_bytes_per_timestep"]), "achieved": round(bw, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bw / HBM_PEAK_GBS, 4),
+            "source": "profiles/pmc_traffic.json[%s] (PMC run of %d timesteps)" % (key, run["timesteps"])}
+
+
 def cpu_baseline(p, t, n, a, lam, frac):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
     host on a bounded sample: Pool(C) runs C timesteps; each assembles the
@@ -334,6 +350,7 @@ def main():
                              else "device (I and V resident in HBM)",
                        "parallelism": "timestep shards x%d" % world},
             "roofline": roofline,
+            "step_traffic": step_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), value),
             "cpu_baseline": cpu,
             "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / n_local, 1),
                        "failed": agg["failed"], "recovered": agg["recovered"],
