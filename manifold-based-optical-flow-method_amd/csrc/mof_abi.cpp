@@ -254,6 +254,7 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
     put(m->diag_pos, P.diag_pos);
     put(m->tsell_off, P.tsell_off);
     put(m->tinc, P.tinc);
+    put(m->tslot, P.tslot);
     mof::DevArray<double> dxyz, dnrm;
     dxyz.alloc(3 * (size_t)N);
     dxyz.upload(xyz_new.data(), 3 * (size_t)N, s);

@@ -439,6 +439,136 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
 }
 
+// Mixed-precision assembly by vertex rows (the PCG row layout and XCD-aware
+// (row block, system) order): thread i walks the incident triangles of
+// vertex i in the caller's triangle order (tinc, SELL-64) and adds each
+// triangle's three a1 terms of row i -- (i,i), (i,v_{a+1}), (i,v_{a+2}) --
+// to register accumulators of the row's SELL slots (tslot; WMAX >= the
+// widest row, unrolled predicated adds: no dynamic register indexing). A
+// triangle's 6 u values are one 24-B read per incident vertex instead of
+// two 8-B reads per term, and every row does the same work (the per-block
+// kernel's diagonal blocks fold every incident triangle, the others two).
+// Same results as k_assemble_mixed up to the fp32 summation order of a1
+// (the solve path's A32 is an fp32 fold either way); f is folded in fp64 in
+// the reference's triangle order, bit for bit.
+#ifndef MOF_ASM_ROWS_DEFAULT
+#define MOF_ASM_ROWS_DEFAULT 1
+#endif
+#ifndef MOF_ASM_ROWS_U
+#define MOF_ASM_ROWS_U 1
+#endif
+template <int WMAX>
+__global__ __launch_bounds__(kWG) void k_assemble_rows(
+    int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
+    const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
+    const int4 *__restrict__ tinc, const int32_t *__restrict__ tslot, const float *__restrict__ w12,
+    const float *__restrict__ a2s, const float *__restrict__ u, const double *__restrict__ fc, int block_jacobi,
+    float *__restrict__ A, float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
+    uint2 *__restrict__ Dh, int32_t nown) {
+    int32_t rb, b;
+    if (!xcd_map(nblk, B, rb, b, kGrpAsm)) return;
+    const float *ub = u + 6 * (int64_t)b * (M + 1);
+    const double *fb = fc + 6 * (int64_t)b * (M + 1);
+    constexpr int U = MOF_ASM_ROWS_U;
+#pragma unroll 1
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= N) break;
+        const int32_t s = i >> 6, l = i & 63;
+        float acc[WMAX][4];
+#pragma unroll
+        for (int q = 0; q < WMAX; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
+        double f0 = 0.0, f1 = 0.0;
+        const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
+        for (int32_t t0 = 0; t0 < tw; t0 += U) {
+            int4 q[U];
+            int32_t sl[U];
+#pragma unroll
+            for (int v = 0; v < U; ++v) {
+                const int64_t e = (int64_t)to + min(t0 + v, tw - 1) * kSlice + l;
+                q[v] = tinc[e];
+                sl[v] = tslot[e];
+            }
+            float2 P[U][3];
+            float w[U];
+            double2 fv[U];
+#pragma unroll
+            for (int v = 0; v < U; ++v) {
+                const float2 *uT = reinterpret_cast<const float2 *>(ub + 6 * (int64_t)q[v].x);
+                P[v][0] = uT[0];
+                P[v][1] = uT[1];
+                P[v][2] = uT[2];
+                w[v] = w12[q[v].x];
+                fv[v] = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)q[v].x + 2 * q[v].y);
+            }
+#pragma unroll
+            for (int v = 0; v < U; ++v) {
+                const bool on = t0 + v < tw;
+                const int c = q[v].y;
+                // corner rotation by 0/1 masks (exact; selects on a runtime
+                // corner index would put P in scratch memory)
+                const float m0 = c == 0 ? 1.f : 0.f, m1 = c == 1 ? 1.f : 0.f, m2 = c == 2 ? 1.f : 0.f;
+                const float2 ui = make_float2(m0 * P[v][0].x + m1 * P[v][1].x + m2 * P[v][2].x,
+                                              m0 * P[v][0].y + m1 * P[v][1].y + m2 * P[v][2].y);
+                const float2 uj = make_float2(m0 * P[v][1].x + m1 * P[v][2].x + m2 * P[v][0].x,
+                                              m0 * P[v][1].y + m1 * P[v][2].y + m2 * P[v][0].y);
+                const float2 uk = make_float2(m0 * P[v][2].x + m1 * P[v][0].x + m2 * P[v][1].x,
+                                              m0 * P[v][2].y + m1 * P[v][0].y + m2 * P[v][1].y);
+                const int32_t sj = sl[v] & 0xff, sk = sl[v] >> 8;
+                const float wv = on ? w[v] : 0.f;
+                // a term on the diagonal block takes A/6 = 2 A/12 (a
+                // degenerate triangle's second corner at i included)
+                const float wd = 2.f * wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
+                const float d[4] = {ui.x * ui.x * wd, ui.x * ui.y * wd, ui.y * ui.x * wd, ui.y * ui.y * wd};
+                const float cj[4] = {ui.x * uj.x * wj, ui.x * uj.y * wj, ui.y * uj.x * wj, ui.y * uj.y * wj};
+                const float ck[4] = {ui.x * uk.x * wk, ui.x * uk.y * wk, ui.y * uk.x * wk, ui.y * uk.y * wk};
+#pragma unroll
+                for (int z = 0; z < WMAX; ++z) {
+                    const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[z][e] += (z == 0 ? d[e] : 0.f) + mj * cj[e] + mk * ck[e];
+                }
+                if (on) {  // f in the reference's triangle order
+                    f0 += fv[v].x;
+                    f1 += fv[v].y;
+                }
+            }
+        }
+        const int32_t deg = vptr[i + 1] - vptr[i];
+        const int64_t o = sell_off[s];
+#pragma unroll
+        for (int z = 0; z < WMAX; ++z) {
+            if (z >= deg) continue;
+            const int64_t pos = o + (int64_t)z * kSlice + l;
+            const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
+            const float Av[4] = {acc[z][0] + s4.x, acc[z][1] + s4.y, acc[z][2] + s4.z, acc[z][3] + s4.w};
+            const int64_t qq = (int64_t)b * sell_nb + pos;
+            reinterpret_cast<float4 *>(A)[qq] = make_float4(Av[0], Av[1], Av[2], Av[3]);
+            if (Ah) {
+                const bool g = i >= nown || sell_col[pos] >= nown;
+                Ah[qq] = g ? bf16x4(z == 0 ? 1.f : 0.f, 0.f, 0.f, z == 0 ? 1.f : 0.f) : bf16x4(Av[0], Av[1], Av[2], Av[3]);
+            }
+            if (z != 0) continue;
+            double inv[4];
+            const double d0 = Av[0], d1 = Av[1], d2 = Av[2], d3 = Av[3];
+            if (block_jacobi) {
+                const double det = d0 * d3 - d1 * d2;
+                inv[0] = d3 / det; inv[1] = -d1 / det; inv[2] = -d2 / det; inv[3] = d0 / det;
+            } else {
+                inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
+            }
+            const int64_t vi = (int64_t)b * N + i;
+            if (Dh)
+                Dh[vi] = i >= nown ? bf16x4(1.f, 0.f, 0.f, 1.f)
+                                   : bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+            else
+                reinterpret_cast<float4 *>(dinv32)[vi] =
+                    make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+            *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kWG) void k_scale_a2(int64_t n, double lambda,
                                                   const double *__restrict__ a2,
                                                   double *__restrict__ s64,
@@ -598,7 +728,8 @@ void check_mesh_arrays(const mof_mesh *m) {
                     ok(m->clist, P.clist.size()) && ok(m->sell_off, P.sell_off.size()) &&
                     ok(m->sell_col, (size_t)P.sell_nb()) && ok(m->sell_blk, (size_t)P.sell_nb()) &&
                     ok(m->blk_row, P.blk_row.size()) && ok(m->diag_pos, N) &&
-                    ok(m->tsell_off, P.tsell_off.size()) && ok(m->tinc, 4 * (size_t)P.tsell_nb()),
+                    ok(m->tsell_off, P.tsell_off.size()) && ok(m->tinc, 4 * (size_t)P.tsell_nb()) &&
+                    ok(m->tslot, (size_t)P.tsell_nb()),
                 "pattern arrays not uploaded");
     MOF_REQUIRE(ok(m->e, 6 * N) && ok(m->gw, 9 * M) && ok(m->iw, 2 * M) &&
                     ok(m->a2, 4 * (size_t)P.sell_nb()) && ok(m->w12_64, M + 1) && ok(m->w12_32, M + 1),
@@ -683,7 +814,26 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     // multigrid: the level-0 smoother's bf16 operator and D^-1 come from here
     AmgBf16 bf{nullptr, nullptr};
     if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
-    if (precision == MOF_PREC_MIXED)
+    // row-wise assembly when the widest row fits the register accumulators
+    // (MOF_ASM_ROWS=0: the per-block kernel)
+    static const int rows_env = [] {
+        const char *v = std::getenv("MOF_ASM_ROWS");
+        return v ? std::atoi(v) : MOF_ASM_ROWS_DEFAULT;
+    }();
+    const int32_t W = m->pat.max_w;
+    const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
+    const dim3 gr(xcd_grid(nblk_rows, B, kGrpAsm));
+    if (precision == MOF_PREC_MIXED && rows_env && W <= 8)
+        k_assemble_rows<8><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p,
+                                             m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p,
+                                             m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p, w.dinv32.p,
+                                             w.rhs.p, bf.A0h, bf.D0h, m->n_own);
+    else if (precision == MOF_PREC_MIXED && rows_env && W <= 16)
+        k_assemble_rows<16><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p,
+                                              m->vptr.p, m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p),
+                                              m->tslot.p, m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p,
+                                              w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own);
+    else if (precision == MOF_PREC_MIXED)
         k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                             m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,
                                             w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own);

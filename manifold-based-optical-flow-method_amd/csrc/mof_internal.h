@@ -97,6 +97,10 @@ struct Pattern {
     // padding entries point at the all-zero triangle slot T = M.
     std::vector<int32_t> tsell_off;    // (nslices+1), in entries
     std::vector<int32_t> tinc;         // (4 * tsell_nb)
+    // per incidence entry: SELL slots (in row i) of the blocks (i, v_{a+1})
+    // and (i, v_{a+2}), packed s1 | s2 << 8 (row-wise assembly)
+    std::vector<int32_t> tslot;        // (tsell_nb)
+    int32_t max_w = 0;                 // widest SELL row (blocks)
     int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
     int64_t tsell_nb() const { return tsell_off.empty() ? 0 : tsell_off.back(); }
     int32_t nblocks() const { return (int32_t)vcol.size(); }
@@ -173,7 +177,7 @@ struct mof_mesh {
     mof::DevArray<int32_t> icol;      // (N) internal vertex -> its column of the caller's I
     // device mesh data (internal order)
     mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row,
-        diag_pos, tsell_off, tinc;
+        diag_pos, tsell_off, tinc, tslot;
     mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4] (unscaled, bit-exact)
     // operator copies: lambda*a2 (cached per lambda) and A_T/12 with a zero slot M
     mof::DevArray<double> a2s64, w12_64;

@@ -146,16 +146,27 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat, const
         }
     }
     std::vector<int32_t> tfill(N, 0);
+    pat.tslot.assign((size_t)tnb, 0);
+    // SELL slot of block (i, j) in row i (diagonal first, sell_slot)
+    auto slot_of = [&](int32_t i, int32_t j) {
+        const auto b = pat.vcol.begin() + pat.vptr[i], e = pat.vcol.begin() + pat.vptr[i + 1];
+        const int32_t t = (int32_t)(std::lower_bound(b, e, j) - b), td = (int32_t)(std::lower_bound(b, e, i) - b);
+        return sell_slot(t, td);
+    };
     for (int32_t q = 0; q < M; ++q) {
         const int32_t T = torder ? torder[q] : q;  // caller's triangle order
         const int32_t *v = tri + 3 * (int64_t)T;
         for (int a = 0; a < 3; ++a) {
             const int32_t i = v[a];
             const int32_t t = tfill[i]++;
-            int32_t *ent = &pat.tinc[4 * ((int64_t)pat.tsell_off[i / kSlice] + (int64_t)t * kSlice + (i % kSlice))];
+            const int64_t e = (int64_t)pat.tsell_off[i / kSlice] + (int64_t)t * kSlice + (i % kSlice);
+            int32_t *ent = &pat.tinc[4 * e];
             ent[0] = T; ent[1] = a; ent[2] = v[(a + 1) % 3]; ent[3] = v[(a + 2) % 3];
+            pat.tslot[e] = slot_of(i, ent[2]) | (slot_of(i, ent[3]) << 8);
         }
     }
+    pat.max_w = 0;
+    for (int32_t s = 0; s < pat.nslices; ++s) pat.max_w = std::max(pat.max_w, (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice);
 }
 
 // Reverse Cuthill-McKee order of the vertex graph in `pat` (adjacency

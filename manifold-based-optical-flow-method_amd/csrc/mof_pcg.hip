@@ -37,6 +37,8 @@
 // residual refreshes r64 = f - A x64 between inner solves (iterative
 // refinement).
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 
@@ -112,6 +114,9 @@ __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd
     block_sum<NV>(out, lds);
 }
 
+#ifndef MOF_RES_U
+#define MOF_RES_U 4
+#endif
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
 // U slots / incident triangles at a time as in spmv_row.
@@ -119,7 +124,7 @@ template <typename V>
 __device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int32_t i,
                                              const V *__restrict__ x, double &y0, double &y1) {
     using V2 = typename VT<V>::V2;
-    constexpr int U = 4;
+    constexpr int U = MOF_RES_U;
     const int32_t s = i >> 6, l = i & 63;
     V a0 = 0, a1 = 0;
     // lambda a2 x
@@ -809,9 +814,11 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     }
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
-    int64_t iters = 0;
+    int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
     const OpArgs<double> o64 = op64(m);
+    // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
+    static const bool verbose = std::getenv("MOF_SOLVE_VERBOSE") != nullptr;
     for (; o < sp.max_outer; ++o) {
         const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
         if (sp.precision == MOF_PREC_MIXED) {
@@ -835,6 +842,17 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         fetch_flags(m, B, s);
         bool any = false;
         for (int32_t b = 0; b < B; ++b) any |= m->h_sysi[b * kSysStride + SI_ACTIVE] != 0;
+        if (verbose) {
+            double worst = 0.0;
+            int32_t act = 0;
+            for (int32_t b = 0; b < B; ++b) {
+                worst = std::max(worst, m->h_sysd[b * kSysStride + SD_REL]);
+                act += m->h_sysi[b * kSysStride + SI_ACTIVE] != 0;
+            }
+            std::fprintf(stderr, "[mof solve] B=%d outer %d: %lld inner its (sum), max rel residual %.3e, %d still active\n",
+                         B, o, (long long)(iters - iters_before), worst, act);
+            iters_before = iters;
+        }
         if (!any) {
             ++o;
             break;
