@@ -463,6 +463,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         // one that stops improving, or hits max_iter, has a bad preconditioner
         sp.stall = sp.amg ? env_int("MOF_PCG_STALL", 64) : 0;
         sp.fail_at_max_iter = sp.amg;
+        sp.adaptive_inner = env_int("MOF_FIXED_INNER_RTOL", 0) == 0;
         const bool recovery = !(o.flags & MOF_NO_RECOVERY);
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
         if (!I2) I2 = I;

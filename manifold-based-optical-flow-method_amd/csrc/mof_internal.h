@@ -269,6 +269,9 @@ struct SolveParams {
     // an inner solve that ends at max_iter unconverged fails the system
     // (instead of handing the partial correction to the next refinement step)
     bool fail_at_max_iter = false;
+    // refinement steps after the first: per-system inner tolerance from the
+    // outer residual still missing (k_pcg_tol); MOF_FIXED_INNER_RTOL=1: off
+    bool adaptive_inner = true;
 };
 // Solve the B assembled systems in the workspace; fills sysd/sysi.
 // Returns total inner iterations; sets *outer to the refinement steps used.

@@ -231,8 +231,13 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
 }
 
 // One workgroup per system: tolerance from |rhs|^2, reset the convergence word.
+// outer_rtol > 0 (refinement steps after the first): each system's inner
+// tolerance is what its own outer residual still needs, 0.3 rtol |f| / |r64|,
+// kept within [rtol, 0.5] -- a system 3x above the outer target (R3 after two
+// steps: the fp32 operator's rounding limits a step to ~3e-4 there) takes a
+// short inner solve, not a full 1e-4 one.
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol) {
+__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, double outer_rtol) {
     __shared__ double lds[8];
     const int32_t b = blockIdx.x;
     int32_t *si = a.sysi + b * kSysStride;
@@ -243,7 +248,12 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol) {
     double v[2];
     reduce_sys<2>(a.part_rzrr, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) {
-        a.sysd[b * kSysStride + SD_TOL2] = rtol * rtol * v[1];
+        double t = rtol;
+        if (outer_rtol > 0.0) {
+            const double ff = a.sysd[b * kSysStride + SD_FF], rr = a.sysd[b * kSysStride + SD_RR];
+            if (ff > 0.0 && rr > 0.0) t = fmax(rtol, fmin(0.5, 0.3 * outer_rtol * sqrt(ff / rr)));
+        }
+        a.sysd[b * kSysStride + SD_TOL2] = t * t * v[1];
         a.sysd[b * kSysStride + SD_RR0] = v[1];
         a.sysd[b * kSysStride + SD_BEST] = v[1];
         si[SI_BEST_IT] = 0;
@@ -601,7 +611,7 @@ void charge_chunk(const mof_mesh *m, int32_t B, const std::vector<int32_t> &runn
 template <typename V>
 int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
             double rtol, const SolveParams &sp, hipStream_t s, int32_t *max_iters, SpmvTiming *timing,
-            int32_t *hint, bool amg) {
+            int32_t *hint, bool amg, double outer_rtol = 0.0) {
     const int32_t max_iter = sp.max_iter;
     PcgArgs<V> a = make_args<V>(m, B, mat, dinv);
     a.ext = amg ? 1 : 0;
@@ -622,7 +632,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B, kGrpSpmv));
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
-    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol);
+    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol);
     if (amg) precond(0);
     MOF_HIP(hipGetLastError());
     // systems active at the start of this solve: the host mirror is current
@@ -824,13 +834,14 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         if (sp.precision == MOF_PREC_MIXED) {
             // hints per (precision, preconditioner, refinement step)
             iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol, sp, s,
-                                max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg);
+                                max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg,
+                                o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
             k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
                                                     w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
-                                 &m->iter_hint[std::min(o, 15)], false);
+                                 &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
@@ -926,7 +937,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
     dd_sync_partials(d, d->part_rzrr.p, 2 * rec, s);
     // the tolerance step resets the convergence word the cycle's kernels
     // check, so it runs before the first cycle
-    for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol);
+    for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol, 0.0);
     if (amg) precond(0);
     MOF_HIP(hipGetLastError());
     std::vector<int32_t> was_active(B);
