@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--inner-rtol", type=float, default=0.0,
                     help="mixed precision: inner PCG tolerance per refinement step (0: the library's 1e-4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 64,
+    ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 4,
                     help="fraction of the triangle loop the CPU baseline times")
     ap.add_argument("--lambda_", type=float, default=0.01)
     ap.add_argument("--fixed-timesteps", type=int, default=0,
