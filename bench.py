@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=256, help="timesteps per step")
+    ap.add_argument("--batch", type=int, default=512, help="timesteps per step")
     ap.add_argument("--config", default="C3", choices=sorted(CONFIG_NAMES))
     ap.add_argument("--precision", default=None, choices=["mixed", "f64"])
     ap.add_argument("--precond", default=None, choices=["jacobi", "amg"],

@@ -85,7 +85,7 @@ typedef struct mof_opts {
     uint32_t precision;    /* MOF_PREC_* */
     uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI | MOF_TIME_SPMV | MOF_PRECOND_AMG */
     int32_t batch;         /* timesteps solved together per launch (0: auto =
-                              256, fewer if device memory is short) */
+                              512, fewer if device memory is short) */
     int32_t max_iter;      /* PCG iterations per inner solve (0: 10000; 1000
                               with MOF_PRECOND_AMG, whose inner solves take
                               tens: more means a bad preconditioner, and
