@@ -694,15 +694,17 @@ __global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t 
         if (i >= N) break;
         float y0, y1;
         float2 xi;
+        uint2 dg;  // the row's diagonal block (slot 0), kept from the SpMV
         if constexpr (MOF_X0_BF16 == 2) {
-            spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1);
+            spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1, &dg);
             xi = reinterpret_cast<const float2 *>(xv)[vb + i];
         } else {
-            spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1);
+            spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1, &dg);
             xi = ld_x0(xv, vb + i);
         }
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-        const float2 ds = bf16_mat2(Dh[vb + i], ri.x - y0, ri.y - y1);
+        const float2 ds = MOF_DINV_FROM_A ? bf16_diag_solve(dg, ri.x - y0, ri.y - y1)
+                                          : bf16_mat2(Dh[vb + i], ri.x - y0, ri.y - y1);
         const float z0 = xi.x + omega * ds.x;
         const float z1 = xi.y + omega * ds.y;
         reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
@@ -852,6 +854,9 @@ AmgFine amg_fine(mof_mesh *m) {
     AmgDevice &G = *m->amg;
     AmgFine f;
     f.D0h = G.D0h.p;
+    f.A0h = G.A0h.p;
+    f.sell_nb = m->pat.sell_nb();
+    f.sell_off = m->sell_off.p;
     f.x0 = G.lv[0].x.p;
     f.omega = G.omega;
     return f;

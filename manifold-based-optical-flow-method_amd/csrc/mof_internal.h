@@ -296,6 +296,9 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_s
 // level-0 smoother data the PCG update / init write the pre-smoothing with
 struct AmgFine {
     const void *D0h;  // bf16 2x2 D^-1 [B][N] (uint2 each)
+    const void *A0h;  // bf16 level-0 operator [B][sell_nb] (its diagonal blocks: MOF_DINV_FROM_A)
+    int64_t sell_nb;
+    const int32_t *sell_off;
     float *x0;        // smoother x
     float omega;
 };

@@ -81,6 +81,9 @@ struct PcgArgs {
     V *x0;                 // ext: pre-smoothed x0 = omega D^-1 r for the V-cycle
     V omega;
     const uint2 *dh;       // ext (multigrid, fp32): the smoother's 2x2 D^-1, 4 bf16 [B][N]
+    const uint2 *dA;       // ext, MOF_DINV_FROM_A: the smoother's bf16 operator (diagonal blocks)
+    int64_t dA_nb;
+    const int32_t *dA_off;
     RedArgs red;           // partial-record layout; rows >= red.nown (ghosts) are not summed
     int32_t stall;         // stagnation window in iterations (0: off)
 };
@@ -216,7 +219,8 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
             if (i < a.red.nown) rz += (double)r0 * z0 + (double)r1 * z1;  // ghost rows: never summed
         } else if constexpr (sizeof(V) == 4) {
             // the smoother's D^-1 (bf16), as in every later sweep
-            const float2 d = bf16_mat2(a.dh[vi], r0, r1);
+            const float2 d = MOF_DINV_FROM_A ? bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), r0, r1)
+                                             : bf16_mat2(a.dh[vi], r0, r1);
             st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
         }
         if (i < a.red.nown) rr += (double)r0 * r0 + (double)r1 * r1;
@@ -380,7 +384,9 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
             if (i < a.red.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
         } else if constexpr (sizeof(V) == 4) {
             // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
-            const float2 d = bf16_mat2(a.dh[vi], ri.x, ri.y);
+            const float2 d = MOF_DINV_FROM_A
+                                 ? bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), ri.x, ri.y)
+                                 : bf16_mat2(a.dh[vi], ri.x, ri.y);
             st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
         }
         if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
@@ -559,6 +565,9 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.x0 = nullptr;
     a.omega = (V)0;
     a.dh = nullptr;
+    a.dA = nullptr;
+    a.dA_nb = 0;
+    a.dA_off = nullptr;
     a.stall = 0;
     return a;
 }
@@ -622,6 +631,9 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             a.x0 = f.x0;
             a.omega = f.omega;
             a.dh = static_cast<const uint2 *>(f.D0h);
+            a.dA = static_cast<const uint2 *>(f.A0h);
+            a.dA_nb = f.sell_nb;
+            a.dA_off = f.sell_off;
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
@@ -903,6 +915,9 @@ std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, bool amg) {
                 a.x0 = f.x0;
                 a.omega = f.omega;
                 a.dh = static_cast<const uint2 *>(f.D0h);
+                a.dA = static_cast<const uint2 *>(f.A0h);
+                a.dA_nb = f.sell_nb;
+                a.dA_off = f.sell_off;
             }
         }
         args.push_back(a);

@@ -216,10 +216,11 @@ struct MatH {
 };
 
 // spmv_row on the bf16 blocks; the operand of column j comes from
-// xload(j) (a plain gather, or a value formed on the fly)
+// xload(j) (a plain gather, or a value formed on the fly); *diag (if given)
+// receives the row's slot 0, the diagonal block
 template <int U = 8, typename XL>
 __device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
-                                            float &y1) {
+                                            float &y1, uint2 *diag = nullptr) {
     const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
@@ -233,6 +234,7 @@ __device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i
         for (int u = 0; u < U; ++u) j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
 #pragma unroll
         for (int u = 0; u < U; ++u) blk[u] = A[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+        if (diag && t0 == 0) *diag = blk[0];
 #pragma unroll
         for (int u = 0; u < U; ++u) xj[u] = xload(j[u]);
 #pragma unroll
@@ -247,8 +249,8 @@ __device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i
 }
 
 __device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i, const float *__restrict__ x,
-                                           float &y0, float &y1) {
-    spmv_row_hx(mt, b, i, [x](int32_t j) { return reinterpret_cast<const float2 *>(x)[j]; }, y0, y1);
+                                           float &y0, float &y1, uint2 *diag = nullptr) {
+    spmv_row_hx(mt, b, i, [x](int32_t j) { return reinterpret_cast<const float2 *>(x)[j]; }, y0, y1, diag);
 }
 
 // The V-cycle's level-0 iterate: the pre-smoothed x0 = w D^-1 r (written by
@@ -280,6 +282,24 @@ __device__ __forceinline__ void st_x0(float *x, int64_t vi, float a, float b) {
 // 2x2 block stored as 4 bf16: y = D v
 __device__ __forceinline__ float2 bf16_mat2(uint2 d, float v0, float v1) {
     return make_float2(bf16_lo(d.x) * v0 + bf16_hi(d.x) * v1, bf16_lo(d.y) * v0 + bf16_hi(d.y) * v1);
+}
+
+// The level-0 smoother's D^-1 v from the diagonal block of the bf16 operator
+// itself (slot 0 of the row: diagonal first), solved in fp32: no separate
+// D^-1 array to stream (MOF_DINV_FROM_A; the pre- and post-smoothing use the
+// same D, so the cycle stays symmetric).
+#ifndef MOF_DINV_FROM_A
+#define MOF_DINV_FROM_A 1
+#endif
+__device__ __forceinline__ float2 bf16_diag_solve(uint2 a, float v0, float v1) {
+    const float a00 = bf16_lo(a.x), a01 = bf16_hi(a.x), a10 = bf16_lo(a.y), a11 = bf16_hi(a.y);
+    const float id = 1.f / (a00 * a11 - a01 * a10);
+    return make_float2((a11 * v0 - a01 * v1) * id, (a00 * v1 - a10 * v0) * id);
+}
+// slot 0 (the diagonal block) of row i of system b in a SELL-64 bf16 operator
+__device__ __forceinline__ uint2 bf16_diag_block(const uint2 *A, int64_t sell_nb, const int32_t *sell_off,
+                                                 int32_t b, int32_t i) {
+    return A[(int64_t)b * sell_nb + sell_off[i >> 6] + (i & 63)];
 }
 
 }  // namespace
