@@ -312,19 +312,23 @@ def main():
     kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
     traffic, traffic_src = pmc_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), kname)
     sv = 4 if precision == "mixed" else 8
-    per_sys = info["nblocks"] * 4 * sv + N * 2 * sv * 5
+    # fp32 operator: diagonal + upper blocks (the lower ones are read as their
+    # transposes through the shared mirror table); fp64: every block
+    nread = info.get("blocks_read", info["nblocks"]) if precision == "mixed" else info["nblocks"]
+    shared = info["nblocks"] * 4 * (2 if nread < info["nblocks"] else 1)  # column indices (+ mirror table)
+    per_sys = nread * 4 * sv + N * 2 * sv * 5
     nl = max(1, agg["spmv_launches"])
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": traffic_src, "kernel": kname,
                 "bytes_per_launch": round(agg["spmv_bytes"] / nl),
-                "bytes_per_system": per_sys, "shared_bytes_per_launch": info["nblocks"] * 4,
+                "bytes_per_system": per_sys, "shared_bytes_per_launch": shared,
                 "systems_per_launch": round(agg["spmv_systems"] / nl, 2),
                 "us_per_launch": round(1e3 * agg["ms_spmv"] / nl, 2),
                 "launches": agg["spmv_launches"],
                 "full_launches": agg["spmv_full_launches"],
                 "us_per_full_launch": round(1e3 * agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]), 2),
-                "full_launch_frac": round((B * per_sys + info["nblocks"] * 4)
+                "full_launch_frac": round((B * per_sys + shared)
                                           / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3)
                                           / 1e9 / HBM_PEAK_GBS, 4) if agg["ms_spmv_full"] > 0 else None}
 

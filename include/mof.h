@@ -130,6 +130,10 @@ typedef struct mof_mesh_info {
     int64_t sell_blocks;       /* blocks incl. SELL-64 padding */
     double ms_geometry;        /* one-time device geometry + a2 build */
     double ms_pattern;         /* one-time host pattern build */
+    int64_t blocks_read;       /* distinct blocks one fp32 / bf16 operator pass
+                                  reads per system: the diagonal and upper
+                                  blocks (lower ones are read as transposes),
+                                  = nblocks in a build without symmetric reads */
 } mof_mesh_info;
 
 /* Library / device queries. */

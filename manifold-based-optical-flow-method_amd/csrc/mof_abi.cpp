@@ -166,6 +166,21 @@ int mof_io_guard(const std::function<void()> &f) { return guarded(f); }
 
 namespace mof {
 
+void mesh_set_own(mof_mesh *m, int32_t nown) {
+    MOF_HIP(hipSetDevice(m->device));
+    m->n_own = nown;
+    // MOF_SYM_READS: 1 / 0 force the symmetric / plain reads, unset: per mesh
+    const char *env = std::getenv("MOF_SYM_READS");
+    const int sym = !MOF_SYM_A ? 0 : env && *env ? (std::atoi(env) != 0) : -1;
+    const std::vector<int32_t> mir = sell_mirror(m->pat, nown, sym, &m->sym_reads);
+    m->sell_mir.alloc(mir.size());
+    m->sell_mir.upload(mir.data(), mir.size(), m->stream);
+    int64_t own = 0;  // positions read at their own place: diagonal + upper blocks
+    for (int32_t v : mir) own += v >= 0 && !(v & kMirT);
+    m->blocks_read = own;
+    MOF_HIP(hipStreamSynchronize(m->stream));
+}
+
 void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t *tri,
                 const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
                 const int32_t *perm_in, const int32_t *tri_ids) {
@@ -255,6 +270,7 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
     put(m->tsell_off, P.tsell_off);
     put(m->tinc, P.tinc);
     put(m->tslot, P.tslot);
+    mesh_set_own(m, N);
     mof::DevArray<double> dxyz, dnrm;
     dxyz.alloc(3 * (size_t)N);
     dxyz.upload(xyz_new.data(), 3 * (size_t)N, s);
@@ -352,6 +368,7 @@ int mof_mesh_get_info(const mof_mesh *m, mof_mesh_info *info) {
         info->sell_blocks = m->pat.sell_nb();
         info->ms_geometry = m->ms_geometry;
         info->ms_pattern = m->ms_pattern;
+        info->blocks_read = m->blocks_read;
     });
 }
 

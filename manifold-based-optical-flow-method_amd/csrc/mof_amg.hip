@@ -723,6 +723,7 @@ MatH level0_mat(mof_mesh *m) {
     mt.sell_nb = m->pat.sell_nb();
     mt.sell_off = m->sell_off.p;
     mt.sell_col = m->sell_col.p;
+    mt.sell_mir = m->sym_reads ? m->sell_mir.p : nullptr;
     mt.A = reinterpret_cast<const uint2 *>(m->amg->A0h.p);
     return mt;
 }

@@ -56,6 +56,9 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
                 const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
                 const int32_t *perm, const int32_t *tri_ids);
 
+// rows >= nown are a part's ghost rows; re-uploads the SELL mirror table
+void mesh_set_own(mof_mesh *m, int32_t nown);
+
 struct RcclApi;  // mof_dd.hip
 
 }  // namespace mof

@@ -462,7 +462,7 @@ void dd_setup(mof_dd *d, const double *xyz, const double *nrm, const int32_t *tr
         // the folds; I is gathered by the caller's (global) vertex ids
         mesh_build(m, lx.data(), ln.data(), lt.data(), la.data(), nl, ml, d->device, d->flags, ident.data(),
                    gt.data());
-        m->n_own = D.n_own;  // ghost rows: decoupled in the part's multigrid cycle
+        mesh_set_own(m, D.n_own);  // ghost rows: decoupled in the part's multigrid cycle
         d->own_off.push_back((int64_t)own.size());
         own.insert(own.end(), D.l2g.begin(), D.l2g.begin() + D.n_own);
     }

@@ -81,6 +81,15 @@ __host__ __device__ inline int32_t sell_block(int32_t slot, int32_t td) {
     return slot == 0 ? td : (slot <= td ? slot - 1 : slot);
 }
 
+// Symmetric reads of the fp32 / bf16 operators through the mirror table
+// (mof_rowkern.h spmv_row); 0 reads every block at its own position.
+#ifndef MOF_SYM_A
+#define MOF_SYM_A 1
+#endif
+// sell_mirror entries: position | kMirT = read the block transposed
+constexpr int32_t kMirT = 1 << 30;
+constexpr int32_t kMirPos = kMirT - 1;
+
 // Host-side sparsity structures, built once per mesh (mof_pattern.cpp).
 struct Pattern {
     int32_t N = 0, M = 0;
@@ -112,6 +121,7 @@ struct Pattern {
 void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat,
                    const int32_t *torder = nullptr);
 std::vector<int32_t> rcm_order(const Pattern &pat);
+std::vector<int32_t> sell_mirror(const Pattern &pat, int32_t nown, int sym, bool *used);
 
 // Per-batch device workspace (capacity B systems).
 struct Workspace {
@@ -178,6 +188,9 @@ struct mof_mesh {
     // device mesh data (internal order)
     mof::DevArray<int32_t> tri, vptr, vcol, cptr, clist, sell_off, sell_col, sell_blk, blk_row,
         diag_pos, tsell_off, tinc, tslot;
+    mof::DevArray<int32_t> sell_mir;  // sell_mirror(pat, n_own): (re)uploaded by mesh_set_own
+    int64_t blocks_read = 0;          // blocks an fp32 / bf16 operator pass reads per system
+    bool sym_reads = false;           // the mirror table transposes lower blocks
     mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4] (unscaled, bit-exact)
     // operator copies: lambda*a2 (cached per lambda) and A_T/12 with a zero slot M
     mof::DevArray<double> a2s64, w12_64;

@@ -169,6 +169,73 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat, const
     for (int32_t s = 0; s < pat.nslices; ++s) pat.max_w = std::max(pat.max_w, (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice);
 }
 
+// Mirror table of the SELL-64 layout (per position, shared by all systems):
+// the fp32 / bf16 operators are symmetric (A(j,i) = A(i,j)^T up to the
+// rounding of the fold), so row i reads a block (i, j) of the lower triangle
+// (j < i) as the transpose of block (j, i), which row j reads anyway: only
+// the diagonal and upper blocks ever leave HBM. Entry: the position to read
+// (| kMirT if transposed), or -1 for padding (read as the row's diagonal,
+// masked: padding lines never leave HBM either). Rows >= nown (ghost rows of
+// a part) and blocks coupling to them read their own position.
+// The mirrored reads of a wave are coalesced only as far as neighbouring rows
+// have their neighbours in the same slots (regular meshes): `sym` = 1 uses
+// them, 0 keeps every block at its own position (identity table), -1 decides
+// per mesh from the 128-B lines a wave instruction touches (fp32 blocks):
+// symmetric reads when own + mirrored lines stay within 1.25x the lines of
+// the plain layout (C3: 1.09x, irregular hull R3: 2.5x).
+std::vector<int32_t> sell_mirror(const Pattern &pat, int32_t nown, int sym, bool *used) {
+    const int64_t snb = pat.sell_off[pat.nslices];
+    MOF_REQUIRE(snb < kMirT, "SELL layout too large for the mirror table");
+    std::vector<int32_t> mir((size_t)snb, -1);
+    auto slot_of = [&](int32_t i, int32_t j) {
+        const auto b = pat.vcol.begin() + pat.vptr[i], e = pat.vcol.begin() + pat.vptr[i + 1];
+        const int32_t t = (int32_t)(std::lower_bound(b, e, j) - b), td = (int32_t)(std::lower_bound(b, e, i) - b);
+        return sell_slot(t, td);
+    };
+    for (int32_t s = 0; s < pat.nslices; ++s) {
+        const int32_t w = (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice;
+        for (int32_t l = 0; l < kSlice; ++l) {
+            const int32_t i = s * kSlice + l;
+            if (i >= pat.N) break;
+            for (int32_t t = 0; t < w; ++t) {
+                const int64_t pos = pat.sell_off[s] + (int64_t)t * kSlice + l;
+                if (pat.sell_blk[pos] < 0) continue;  // padding
+                const int32_t j = pat.sell_col[pos];
+                if (sym != 0 && j < i && i < nown)
+                    mir[pos] = (int32_t)(pat.sell_off[j / kSlice] + (int64_t)slot_of(j, i) * kSlice + j % kSlice) | kMirT;
+                else
+                    mir[pos] = (int32_t)pos;
+            }
+        }
+    }
+    if (sym < 0) {  // lines (128 B = 8 fp32 blocks) per wave instruction, summed
+        int64_t plain = 0, mirrored = 0;
+        std::vector<int64_t> ln;
+        for (int32_t s = 0; s < pat.nslices; ++s) {
+            const int32_t w = (pat.sell_off[s + 1] - pat.sell_off[s]) / kSlice;
+            for (int32_t t = 0; t < w; ++t) {
+                const int64_t base = pat.sell_off[s] + (int64_t)t * kSlice;
+                ln.clear();
+                int64_t last = -1;
+                for (int32_t l = 0; l < kSlice; ++l) {
+                    const int32_t v = mir[base + l];
+                    if (v < 0) continue;
+                    if (((base + l) >> 3) != last) ++plain, last = (base + l) >> 3;
+                    ln.push_back((int64_t)(v & kMirPos) >> 3);
+                }
+                std::sort(ln.begin(), ln.end());
+                mirrored += std::unique(ln.begin(), ln.end()) - ln.begin();
+            }
+        }
+        sym = mirrored * 4 <= plain * 5 ? 1 : 0;
+        if (!sym)
+            for (int64_t q = 0; q < snb; ++q)
+                if (mir[q] >= 0) mir[q] = (int32_t)q;
+    }
+    if (used) *used = sym != 0;
+    return mir;
+}
+
 // Reverse Cuthill-McKee order of the vertex graph in `pat` (adjacency
 // only). Returns perm with perm[old] = new. BFS from a pseudo-peripheral
 // vertex of every connected component, neighbours in increasing degree,

@@ -538,6 +538,7 @@ MatArgs<V> make_mat(mof_mesh *m, const V *A) {
     mt.sell_nb = m->pat.sell_nb();
     mt.sell_off = m->sell_off.p;
     mt.sell_col = m->sell_col.p;
+    mt.sell_mir = m->sym_reads ? m->sell_mir.p : nullptr;
     mt.A = A;
     return mt;
 }
@@ -736,11 +737,14 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
 }  // namespace
 
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
-    // per system: the 2x2 block values, z gathered once, q and p read and
-    // written; shared by all systems of the launch: the column indices.
-    const double N = m->N, nb = m->pat.nblocks();
-    const double sv = precision == MOF_PREC_MIXED ? 4.0 : 8.0;
-    return active * (nb * 4 * sv + N * 2 * sv * 5) + nb * 4.0;
+    // per system: the 2x2 block values (fp32: the diagonal and upper blocks,
+    // read once each with the symmetric reads), z gathered once, q and p read
+    // and written; shared by all systems of the launch: the column indices
+    // (and the mirror table).
+    const bool f32 = precision == MOF_PREC_MIXED;
+    const double N = m->N, nb = m->pat.nblocks(), nr = f32 ? (double)m->blocks_read : nb;
+    const double sv = f32 ? 4.0 : 8.0;
+    return active * (nr * 4 * sv + N * 2 * sv * 5) + nb * 4.0 * (f32 && m->sym_reads ? 2 : 1);
 }
 
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {

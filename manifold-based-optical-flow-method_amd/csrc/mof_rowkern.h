@@ -90,8 +90,17 @@ template <typename V>
 struct MatArgs {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;
+    const int32_t *sell_mir;  // mirror table (fp32 operator, MOF_SYM_A)
     const V *A;  // [B][sell_nb][4]
 };
+
+// Symmetric reads (MOF_SYM_A): the fp32 and bf16 operators read a lower
+// block (i, j), j < i, as the transpose of block (j, i) through the mirror
+// table (sell_mirror), so only the diagonal and upper blocks move from HBM;
+// row j of the same or a recent row block has just read them, and the
+// mirrored reads of 64 neighbouring rows fall on about as few cache lines as
+// their own reads would. Padding slots read the row's diagonal, masked.
+__device__ __forceinline__ int64_t mir_pos(int32_t m, int64_t diag) { return m < 0 ? diag : (int64_t)(m & kMirPos); }
 
 template <typename V>
 __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
@@ -104,9 +113,9 @@ __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
 // a row costs two memory round trips instead of two per slot. Slots past
 // the slice width re-load the last valid slot and are masked out, keeping
 // every load unconditional.
-template <typename V>
-__device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
-                                         const V *__restrict__ x, V &y0, V &y1) {
+template <bool sym, typename V>
+__device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int32_t i,
+                                           const V *__restrict__ x, V &y0, V &y1) {
     using V2 = typename VT<V>::V2;
     constexpr int U = 8;  // fp64 too: 525 vs 536 us per C2 launch with 4
     const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
@@ -115,30 +124,52 @@ __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_
     const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
     V a0 = 0, a1 = 0;
     for (int32_t t0 = 0; t0 < w; t0 += U) {
-        int32_t j[U];
+        int32_t j[U], mr[U];
         V blk[U][4];
         V2 xj[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int32_t t = min(t0 + u, w - 1);
             j[u] = mt.sell_col[(int64_t)o + t * kSlice + l];
+            if constexpr (sym) mr[u] = mt.sell_mir[(int64_t)o + t * kSlice + l];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int32_t t = min(t0 + u, w - 1);
-            ld_blk(A, (int64_t)o + t * kSlice + l, blk[u]);
+            if constexpr (sym)
+                ld_blk(A, mir_pos(mr[u], (int64_t)o + l), blk[u]);
+            else
+                ld_blk(A, (int64_t)o + t * kSlice + l, blk[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) xj[u] = ld2(x + 2 * (int64_t)j[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool on = t0 + u < w;
-            a0 += on ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : (V)0;
-            a1 += on ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : (V)0;
+            if constexpr (sym) {
+                const bool on = t0 + u < w && mr[u] >= 0;
+                const bool tr = (mr[u] & kMirT) != 0;
+                const V b1 = tr ? blk[u][2] : blk[u][1], b2 = tr ? blk[u][1] : blk[u][2];
+                a0 += on ? blk[u][0] * xj[u].x + b1 * xj[u].y : (V)0;
+                a1 += on ? b2 * xj[u].x + blk[u][3] * xj[u].y : (V)0;
+            } else {
+                const bool on = t0 + u < w;
+                a0 += on ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : (V)0;
+                a1 += on ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : (V)0;
+            }
         }
     }
     y0 = a0;
     y1 = a1;
+}
+// sell_mir == nullptr (a mesh without symmetric reads, and fp64): every block
+// at its own position, no table reads
+template <typename V>
+__device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
+                                         const V *__restrict__ x, V &y0, V &y1) {
+    if (MOF_SYM_A && sizeof(V) == 4 && mt.sell_mir)
+        spmv_row_t<MOF_SYM_A && sizeof(V) == 4>(mt, b, i, x, y0, y1);
+    else
+        spmv_row_t<false>(mt, b, i, x, y0, y1);
 }
 
 // XCD-aware workgroup -> (row block, system): workgroups w and w+8 share an
@@ -212,40 +243,62 @@ __device__ __forceinline__ uint2 bf16x4(float a, float b, float c, float d) {
 struct MatH {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;
+    const int32_t *sell_mir;  // mirror table (MOF_SYM_A)
     const uint2 *A;  // [B][sell_nb] 4 bf16 per block
 };
 
 // spmv_row on the bf16 blocks; the operand of column j comes from
 // xload(j) (a plain gather, or a value formed on the fly); *diag (if given)
 // receives the row's slot 0, the diagonal block
-template <int U = 8, typename XL>
-__device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
-                                            float &y1, uint2 *diag = nullptr) {
+template <bool sym, int U = 8, typename XL>
+__device__ __forceinline__ void spmv_row_hx_t(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
+                                              float &y1, uint2 *diag) {
     const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
     const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
     float a0 = 0.f, a1 = 0.f;
     for (int32_t t0 = 0; t0 < w; t0 += U) {
-        int32_t j[U];
+        int32_t j[U], mr[U];
         uint2 blk[U];
         float2 xj[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+        for (int u = 0; u < U; ++u) {
+            j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+            if constexpr (sym) mr[u] = mt.sell_mir[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+        }
 #pragma unroll
-        for (int u = 0; u < U; ++u) blk[u] = A[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+        for (int u = 0; u < U; ++u)
+            blk[u] = A[sym ? mir_pos(mr[u], (int64_t)o + l) : (int64_t)o + min(t0 + u, w - 1) * kSlice + l];
         if (diag && t0 == 0) *diag = blk[0];
 #pragma unroll
         for (int u = 0; u < U; ++u) xj[u] = xload(j[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool on = t0 + u < w;
-            a0 += on ? bf16_lo(blk[u].x) * xj[u].x + bf16_hi(blk[u].x) * xj[u].y : 0.f;
-            a1 += on ? bf16_lo(blk[u].y) * xj[u].x + bf16_hi(blk[u].y) * xj[u].y : 0.f;
+            bool on = t0 + u < w;
+            uint32_t bx = blk[u].x, by = blk[u].y;
+            if constexpr (sym) {
+                on = on && mr[u] >= 0;
+                const bool tr = (mr[u] & kMirT) != 0;  // transpose: swap the off-diagonal halves
+                const uint32_t tx = (bx & 0xFFFFu) | (by << 16), ty = (bx >> 16) | (by & 0xFFFF0000u);
+                bx = tr ? tx : bx;
+                by = tr ? ty : by;
+            }
+            a0 += on ? bf16_lo(bx) * xj[u].x + bf16_hi(bx) * xj[u].y : 0.f;
+            a1 += on ? bf16_lo(by) * xj[u].x + bf16_hi(by) * xj[u].y : 0.f;
         }
     }
     y0 = a0;
     y1 = a1;
+}
+
+template <typename XL>
+__device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
+                                            float &y1, uint2 *diag = nullptr) {
+    if (MOF_SYM_A && mt.sell_mir)
+        spmv_row_hx_t<(bool)MOF_SYM_A>(mt, b, i, xload, y0, y1, diag);
+    else
+        spmv_row_hx_t<false>(mt, b, i, xload, y0, y1, diag);
 }
 
 __device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i, const float *__restrict__ x,

@@ -96,7 +96,7 @@ class MofMeshInfo(ctypes.Structure):
         ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("device", ctypes.c_int32),
         ("nblocks", ctypes.c_int32), ("nnz_struct", ctypes.c_int64),
         ("sell_blocks", ctypes.c_int64), ("ms_geometry", ctypes.c_double),
-        ("ms_pattern", ctypes.c_double),
+        ("ms_pattern", ctypes.c_double), ("blocks_read", ctypes.c_int64),
     ]
 
 

@@ -48,7 +48,7 @@ def test_struct_layouts():
     # mirror of the C structs in include/mof.h (x86-64 SysV layout)
     assert ctypes.sizeof(L.MofOpts) == 48
     assert ctypes.sizeof(L.MofStats) == 112
-    assert ctypes.sizeof(L.MofMeshInfo) == 48
+    assert ctypes.sizeof(L.MofMeshInfo) == 56
 
 
 def test_struct_offsets_match_header(tmp_path):

@@ -82,10 +82,14 @@ def test_recovery_reaches_fp64(precond):
     assert np.abs(V - g["V_k"][:6]).max() < VTOL
 
 
+@pytest.mark.parametrize("sym", ["0", "1"])
 @pytest.mark.parametrize("precision,precond", [("mixed", "amg"), ("mixed", "jacobi"), ("f64", "jacobi")])
-def test_spmv_accounting_systems_equal_iterations(precision, precond):
+def test_spmv_accounting_systems_equal_iterations(precision, precond, sym, monkeypatch):
     """Every timed SpMV launch is charged with the systems that worked in it:
-    summed over launches that is exactly the PCG iteration count."""
+    summed over launches that is exactly the PCG iteration count. With the
+    symmetric reads (MOF_SYM_READS=1) the fp32 operator's bytes are the
+    diagonal and upper blocks."""
+    monkeypatch.setenv("MOF_SYM_READS", sym)  # read when the mesh is built
     g = load_golden("G1_ico642")
     T = 40
     I = synth.travelling_wave(g["coordinates"], T)
@@ -100,10 +104,30 @@ def test_spmv_accounting_systems_equal_iterations(precision, precond):
     N = len(g["coordinates"])
     info = m.info()
     sv = 4 if precision == "mixed" else 8
-    per_sys = info["nblocks"] * 4 * sv + N * 2 * sv * 5
-    shared = info["nblocks"] * 4
+    # the fp32 operator reads each symmetric pair of blocks once (diagonal + upper)
+    nread = info["blocks_read"] if precision == "mixed" else info["nblocks"]
+    if precision == "mixed":
+        assert nread == ((info["nblocks"] + N) // 2 if sym == "1" else info["nblocks"])
+    per_sys = nread * 4 * sv + N * 2 * sv * 5
+    shared = info["nblocks"] * 4 * (2 if precision == "mixed" and sym == "1" else 1)
     lo = st["spmv_systems"] * per_sys
     assert lo <= st["spmv_bytes"] <= lo + st["spmv_launches"] * shared
+
+
+@pytest.mark.parametrize("sym", ["0", "1"])
+@pytest.mark.parametrize("precond", ["jacobi", "amg"])
+def test_symmetric_reads_match_spsolve(precond, sym, monkeypatch):
+    """The fp32 / bf16 operators read through the mirror table both ways
+    (lower blocks as transposes of upper ones, or every block in place; the
+    library picks per mesh, forced here): V meets the 1e-6 bar either way."""
+    monkeypatch.setenv("MOF_SYM_READS", sym)
+    g = load_golden("G1_ico642")
+    m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+    info = m.info()
+    assert info["blocks_read"] == ((info["nblocks"] + info["N"]) // 2 if sym == "1" else info["nblocks"])
+    V, st = m.solve_range(g["I"], g["t_k"], 0, 6, float(g["lambda_"]), precision="mixed", precond=precond)
+    assert st["failed"] == 0 and st["recovered"] == 0 and st["max_rel_residual"] <= 1e-8
+    assert np.abs(V - g["V_k"][:6]).max() < VTOL
 
 
 @pytest.mark.parametrize("same_I2", [True, False])
