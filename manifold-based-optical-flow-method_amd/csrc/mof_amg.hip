@@ -379,7 +379,7 @@ __device__ __forceinline__ void ld_dh(const Lvl &L, int32_t b, int32_t i, float 
 
 // Level 0: r1 = r - A x0 (x0 = w D^-1 r from the PCG update), stored at the
 // member position of each vertex. PCG row layout, XCD-aware grid.
-__global__ __launch_bounds__(kWG) void k_res0(int32_t N, int32_t nblk, int32_t B, MatH mat,
+__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                               const float *__restrict__ rv, const float *__restrict__ xv,
                                               const int32_t *__restrict__ apos,
                                               const int32_t *__restrict__ sysi, float *__restrict__ r1) {
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 
 // Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
 // of the row block's record). PCG row layout, XCD-aware grid.
-__global__ __launch_bounds__(kWG) void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
+__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                const uint2 *__restrict__ Dh,
                                                const float *__restrict__ rv,
                                                const float *__restrict__ xv, float omega,

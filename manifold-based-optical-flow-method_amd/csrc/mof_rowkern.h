@@ -113,11 +113,27 @@ __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
 // a row costs two memory round trips instead of two per slot. Slots past
 // the slice width re-load the last valid slot and are masked out, keeping
 // every load unconditional.
+// occupancy / unroll knobs of the fine-level operator passes (A/B builds)
+#ifndef MOF_ROW_WAVES
+#define MOF_ROW_WAVES 5
+#endif
+#if MOF_ROW_WAVES > 0
+#define MOF_ROW_OCC __attribute__((amdgpu_waves_per_eu(MOF_ROW_WAVES, 8)))
+#else
+#define MOF_ROW_OCC
+#endif
+#ifndef MOF_SPMV_U
+#define MOF_SPMV_U 8
+#endif
+#ifndef MOF_SWEEP_U
+#define MOF_SWEEP_U 8
+#endif
+
 template <bool sym, typename V>
 __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int32_t i,
                                            const V *__restrict__ x, V &y0, V &y1) {
     using V2 = typename VT<V>::V2;
-    constexpr int U = 8;  // fp64 too: 525 vs 536 us per C2 launch with 4
+    constexpr int U = sizeof(V) == 4 ? MOF_SPMV_U : 8;  // fp64: 525 vs 536 us per C2 launch with 4
     const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
@@ -250,7 +266,7 @@ struct MatH {
 // spmv_row on the bf16 blocks; the operand of column j comes from
 // xload(j) (a plain gather, or a value formed on the fly); *diag (if given)
 // receives the row's slot 0, the diagonal block
-template <bool sym, int U = 8, typename XL>
+template <bool sym, int U = MOF_SWEEP_U, typename XL>
 __device__ __forceinline__ void spmv_row_hx_t(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
                                               float &y1, uint2 *diag) {
     const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
