@@ -114,20 +114,28 @@ def test_spmv_accounting_systems_equal_iterations(precision, precond, sym, monke
     assert lo <= st["spmv_bytes"] <= lo + st["spmv_launches"] * shared
 
 
-@pytest.mark.parametrize("sym", ["0", "1"])
 @pytest.mark.parametrize("precond", ["jacobi", "amg"])
-def test_symmetric_reads_match_spsolve(precond, sym, monkeypatch):
-    """The fp32 / bf16 operators read through the mirror table both ways
-    (lower blocks as transposes of upper ones, or every block in place; the
-    library picks per mesh, forced here): V meets the 1e-6 bar either way."""
-    monkeypatch.setenv("MOF_SYM_READS", sym)
+def test_symmetric_reads_match_spsolve(precond, monkeypatch):
+    """The fp32 / bf16 operators read through the mirror table (lower blocks
+    as transposes of upper ones) or every block in place; the library picks
+    per mesh, forced here. The fp32 fold builds each block from its own row's
+    incident triangles, so a lower block and its transposed upper twin differ
+    at fp32 rounding (the fp64 A is bit-symmetric, like the reference's
+    mirrored assignment); V agrees far inside the 1e-6 bar either way."""
     g = load_golden("G1_ico642")
-    m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
-    info = m.info()
-    assert info["blocks_read"] == ((info["nblocks"] + info["N"]) // 2 if sym == "1" else info["nblocks"])
-    V, st = m.solve_range(g["I"], g["t_k"], 0, 6, float(g["lambda_"]), precision="mixed", precond=precond)
-    assert st["failed"] == 0 and st["recovered"] == 0 and st["max_rel_residual"] <= 1e-8
-    assert np.abs(V - g["V_k"][:6]).max() < VTOL
+    out = {}
+    for sym in ("0", "1"):
+        monkeypatch.setenv("MOF_SYM_READS", sym)
+        m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+        info = m.info()
+        assert info["blocks_read"] == ((info["nblocks"] + info["N"]) // 2 if sym == "1" else info["nblocks"])
+        V, st = m.solve_range(g["I"], g["t_k"], 0, 6, float(g["lambda_"]), precision="mixed", precond=precond)
+        assert st["failed"] == 0 and st["recovered"] == 0 and st["max_rel_residual"] <= 1e-8
+        assert np.abs(V - g["V_k"][:6]).max() < VTOL
+        out[sym] = (V, st["iterations"])
+        m.close()
+    assert abs(out["0"][1] - out["1"][1]) <= 0.02 * out["0"][1]
+    assert np.abs(out["0"][0] - out["1"][0]).max() < 1e-8 * np.abs(out["0"][0]).max()
 
 
 @pytest.mark.parametrize("same_I2", [True, False])

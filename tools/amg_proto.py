@@ -1,0 +1,311 @@
+"""CPU prototype of the inner solve's multigrid preconditioner (research tool).
+
+    python tools/amg_proto.py CONFIG [variant ...]
+
+Builds one timestep's system with the oracle (fp64, caller order), renumbers
+it by reverse Cuthill-McKee like the library, and counts the PCG iterations
+(fp64) to a 1e-4 relative residual -- the first refinement step of the
+mixed solve -- for aggregation-multigrid variants:
+
+  base        the library's cycle: greedy aggregation on the block graph,
+              tentative prolongator from the tangent-frame near-null space,
+              V(1,1) damped block Jacobi (omega 0.85 / 1.05), dense coarsest
+  theta=X     level-0 aggregation on strong couplings only
+              (||A_ij||_F >= X sqrt(||A_ii||_F ||A_jj||_F))
+  theta2=X    the same with the strength measured on lambda*a2 (per mesh)
+  om=X,Y      smoother damping (fine, coarse)
+  l1          l1 block-Jacobi smoother (D + sum_j ||A_ij|| I), undamped
+  sa=X        smoothed prolongator P = (I - X D^-1 A) P_tent at level 0,
+              with the system's own A (per timestep)
+  sa2=X       the same with lambda*a2 only (a per-mesh, timestep-free P)
+  w2          two coarse-grid visits per level-1 cycle (W-cycle at level 1)
+
+The oracle is test infrastructure; this script is a design tool, never part
+of the product path.
+"""
+import sys
+import os
+
+import numpy as np
+import scipy.sparse as sp
+import scipy.linalg as sla
+from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(REPO, "manifold-based-optical-flow-method_amd"))
+import oracle  # noqa: E402
+from mofhip import synth  # noqa: E402
+
+
+def system(cfg, k=0):
+    if cfg.startswith("ico"):
+        p, t = synth.icosphere(int(cfg[3:]), 0.005)
+        n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    else:
+        p, t, n, a = synth.mesh_for_config(cfg)
+    I = synth.travelling_wave(p, k + 2)
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    A, f = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
+    N = len(p)
+    lam_a2 = 0.01 * a2
+    # planar [V0, V1] -> interleaved (vertex-major) dofs, vertices in RCM order
+    r = np.concatenate([t[:, 0], t[:, 1], t[:, 2], t[:, 1], t[:, 2], t[:, 0]])
+    c = np.concatenate([t[:, 1], t[:, 2], t[:, 0], t[:, 0], t[:, 1], t[:, 2]])
+    G = sp.csr_matrix((np.ones(len(r)), (r, c)), shape=(N, N))
+    order = reverse_cuthill_mckee(G.tocsr(), symmetric_mode=True)  # new -> old
+    dof = np.empty(2 * N, dtype=np.int64)
+    dof[0::2] = order
+    dof[1::2] = order + N
+    A = sp.csr_matrix(A)[dof][:, dof].tocsr()
+    a2m = sp.csr_matrix(lam_a2)[dof][:, dof].tocsr()
+    f = f[dof]
+    e = e[order]  # (N, 2, 3)
+    return A, a2m, f, e, N
+
+
+def block_diag_inv(A, bs):
+    n = A.shape[0] // bs
+    D = np.zeros((n, bs, bs))
+    Acoo = A.tocoo()
+    m = (Acoo.row // bs) == (Acoo.col // bs)
+    D[Acoo.row[m] // bs, Acoo.row[m] % bs, Acoo.col[m] % bs] += Acoo.data[m]
+    return D, np.linalg.inv(D)
+
+
+def bsr_apply(Dinv, v, bs):
+    return np.einsum("nij,nj->ni", Dinv, v.reshape(-1, bs)).ravel()
+
+
+def block_graph(A, bs):
+    n = A.shape[0] // bs
+    Acoo = A.tocoo()
+    Bg = sp.csr_matrix((np.abs(Acoo.data), (Acoo.row // bs, Acoo.col // bs)), shape=(n, n))
+    Bg.sum_duplicates()
+    return Bg
+
+
+def aggregate(G):
+    """The library's greedy aggregation (mof_amg_host.cpp aggregate) on CSR
+    adjacency with self loops."""
+    n = G.shape[0]
+    ptr, col = G.indptr, G.indices
+    agg = -np.ones(n, dtype=np.int64)
+    na = 0
+    for i in range(n):
+        nb = col[ptr[i]:ptr[i + 1]]
+        if (agg[nb] < 0).all():
+            agg[nb] = na
+            na += 1
+    for i in range(n):
+        if agg[i] >= 0:
+            continue
+        nb = agg[col[ptr[i]:ptr[i + 1]]]
+        nb = nb[nb >= 0]
+        if len(nb) == 0:
+            agg[i] = na
+            na += 1
+            continue
+        vals, cnt = np.unique(nb, return_counts=True)
+        agg[i] = vals[np.argmax(cnt)]
+    return agg, na
+
+
+def strength_graph(A, bs, theta):
+    Acoo = A.tocoo()
+    n = A.shape[0] // bs
+    F = sp.csr_matrix((Acoo.data ** 2, (Acoo.row // bs, Acoo.col // bs)), shape=(n, n))
+    F.sum_duplicates()
+    F.data = np.sqrt(F.data)
+    d = F.diagonal()
+    Fc = F.tocoo()
+    keep = (Fc.row == Fc.col) | (Fc.data >= theta * np.sqrt(d[Fc.row] * d[Fc.col]))
+    return sp.csr_matrix((np.ones(keep.sum()), (Fc.row[keep], Fc.col[keep])), shape=(n, n))
+
+
+def tentative(agg, na, Bnull, bs):
+    """Per aggregate QR of the stacked near-null space (MGS twice, dead
+    columns dropped) -> P (n*bs x 3*na), coarse near-null (na, 3, 3)."""
+    n = len(agg)
+    order = np.argsort(agg, kind="stable")
+    bounds = np.searchsorted(agg[order], np.arange(na + 1))
+    rows, cols, vals = [], [], []
+    Bc = np.zeros((na, 3, 3))
+    for I in range(na):
+        mem = order[bounds[I]:bounds[I + 1]]
+        Bm = Bnull[mem].reshape(-1, 3)
+        Q = Bm.copy()
+        R = np.zeros((3, 3))
+        cmax = np.sqrt((Bm ** 2).sum(0)).max()
+        dead = [False] * 3
+        for c in range(3):
+            for _ in range(2):
+                for pp in range(c):
+                    if dead[pp]:
+                        continue
+                    d = Q[:, pp] @ Q[:, c]
+                    R[pp, c] += d
+                    Q[:, c] -= d * Q[:, pp]
+            s = np.sqrt(Q[:, c] @ Q[:, c])
+            dead[c] = not (s > 1e-6 * cmax) or Bm.shape[0] < c + 1
+            if dead[c]:
+                Q[:, c] = 0
+                R[:, c] = 0
+                continue
+            R[c, c] = s
+            Q[:, c] /= s
+        Bc[I] = R
+        dofs = (mem[:, None] * bs + np.arange(bs)).ravel()
+        for c in range(3):
+            if dead[c]:
+                continue
+            rows.append(dofs)
+            cols.append(np.full(len(dofs), 3 * I + c))
+            vals.append(Q[:, c])
+    P = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(n * bs, 3 * na))
+    return P, Bc
+
+
+class Level:
+    pass
+
+
+def build(A, a2m, e, opts):
+    levels = []
+    bs = 2
+    Bnull = e.reshape(-1, bs, 3)
+    Acur = A
+    lvl = 0
+    while True:
+        L = Level()
+        L.A, L.bs = Acur, bs
+        L.D, L.Dinv = block_diag_inv(Acur, bs)
+        if opts.get("l1"):
+            G = block_graph(Acur, bs)  # |entries| summed per block
+            Fr = sp.csr_matrix((Acur.tocoo().data ** 2, (Acur.tocoo().row // bs, Acur.tocoo().col // bs)),
+                               shape=G.shape)
+            Fr.sum_duplicates()
+            Fr.data = np.sqrt(Fr.data)
+            off = np.asarray(Fr.sum(1)).ravel() - Fr.diagonal()
+            L.Dinv = np.linalg.inv(L.D + off[:, None, None] * np.eye(bs)[None])
+            L.om = 1.0
+        else:
+            L.om = opts.get("om", (0.85, 1.05))[0 if lvl == 0 else 1]
+        levels.append(L)
+        n = Acur.shape[0] // bs
+        if n * bs <= 128 or n * 3 <= 128:
+            L.coarse = np.linalg.inv(Acur.toarray() + np.diag((np.abs(Acur).sum(1).A1 == 0) * 1.0))
+            break
+        G = block_graph(Acur, bs)
+        if lvl == 0 and "theta" in opts:
+            G = strength_graph(Acur, bs, opts["theta"])
+        if lvl == 0 and "theta2" in opts:  # strength from lambda*a2 (per mesh)
+            G = strength_graph(a2m, bs, opts["theta2"])
+        G = (G + sp.eye(G.shape[0])).tocsr()
+        G.sort_indices()
+        agg, na = aggregate(G)
+        if na >= n:
+            L.coarse = np.linalg.inv(Acur.toarray())
+            break
+        P, Bc = tentative(agg, na, Bnull, bs)
+        if lvl == 0 and ("sa" in opts or "sa2" in opts):
+            Asm = Acur if "sa" in opts else a2m
+            w = opts.get("sa", opts.get("sa2"))
+            _, Dinv_s = block_diag_inv(Asm, bs)
+            Dbsr = sp.block_diag([Dinv_s[i] for i in range(n)], format="csr")
+            P = (P - w * (Dbsr @ (Asm @ P))).tocsr()
+            if "trunc" in opts:  # drop the 2x3 blocks of P below trunc x the row's largest
+                Pb = P.tobsr(blocksize=(2, 3))
+                nb = np.sqrt((Pb.data ** 2).sum(axis=(1, 2)))
+                rowmax = np.zeros(Pb.shape[0] // 2)
+                rows = np.repeat(np.arange(Pb.shape[0] // 2), np.diff(Pb.indptr))
+                np.maximum.at(rowmax, rows, nb)
+                keep = nb >= opts["trunc"] * rowmax[rows]
+                Pb.data[~keep] = 0
+                P = Pb.tocsr()
+                P.eliminate_zeros()
+        Pb = P.tobsr(blocksize=(bs, 3))
+        L.p_blocks = Pb.nnz / (bs * 3) / (P.shape[0] / bs)
+        L.P = P
+        Ab = Acur.tobsr(blocksize=(bs, bs))
+        # Galerkin terms: sum over fine blocks (i, j) of |P_i| |P_j| (blocks)
+        pc = np.diff(Pb.indptr)
+        rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
+        L.gal_terms = int((pc[rows] * pc[Ab.indices]).sum())
+        Ac = (P.T @ Acur @ P).tocsr()
+        dead = np.abs(Ac).sum(1).A1 == 0
+        Ac = (Ac + sp.diags(dead * 1.0)).tocsr()
+        Acur, bs, Bnull = Ac, 3, Bc
+        lvl += 1
+    return levels
+
+
+def vcycle(levels, l, b, opts):
+    L = levels[l]
+    if hasattr(L, "coarse"):
+        return L.coarse @ b
+    x = L.om * bsr_apply(L.Dinv, b, L.bs)
+    cyc = 2 if (opts.get("w2") and l == 1) else 1
+    for _ in range(cyc):
+        r = b - L.A @ x
+        y = vcycle(levels, l + 1, L.P.T @ r, opts)
+        x = x + L.P @ y
+        x = x + L.om * bsr_apply(L.Dinv, b - L.A @ x, L.bs)
+    return x
+
+
+def pcg(A, f, M, tol=1e-4, maxit=2000):
+    x = np.zeros_like(f)
+    r = f.copy()
+    z = M(r)
+    p = z.copy()
+    rz = r @ z
+    nf = np.linalg.norm(f)
+    for it in range(1, maxit + 1):
+        q = A @ p
+        a = rz / (p @ q)
+        x += a * p
+        r -= a * q
+        if np.linalg.norm(r) <= tol * nf:
+            return it
+        z = M(r)
+        rz2 = r @ z
+        p = z + (rz2 / rz) * p
+        rz = rz2
+    return maxit
+
+
+def parse(args):
+    opts = {}
+    for a in args:
+        if a == "base":
+            continue
+        if a in ("l1", "w2"):
+            opts[a] = True
+        elif a.startswith("om="):
+            opts["om"] = tuple(float(v) for v in a[3:].split(","))
+        else:
+            k, v = a.split("=")
+            opts[k] = float(v)
+    return opts
+
+
+def main():
+    cfg = sys.argv[1]
+    A, a2m, f, e, N = system(cfg)
+    for spec in sys.argv[2:] or ["base"]:
+        opts = parse(spec.split("+"))
+        levels = build(A, a2m, e, opts)
+        sizes = [lv.A.shape[0] // lv.bs for lv in levels]
+        nnz = sum(lv.A.nnz for lv in levels)
+        its = pcg(A, f, lambda r: vcycle(levels, 0, r, opts))
+        blk = [round(lv.A.nnz / lv.bs ** 2 / (lv.A.shape[0] / lv.bs), 1) for lv in levels]
+        pb = [round(lv.p_blocks, 2) for lv in levels if hasattr(lv, "p_blocks")]
+        gal = [getattr(lv, "gal_terms", 0) for lv in levels]
+        print("%s %-24s its(1e-4) %4d  levels %s  op complexity %.2f  blocks/row %s  P blocks/row %s  "
+              "Galerkin terms %s" % (cfg, spec, its, sizes, nnz / A.nnz, blk, pb, gal), flush=True)
+
+
+if __name__ == "__main__":
+    main()
