@@ -20,6 +20,16 @@ struct AmgParams {
     // use an identity block on their diagonal and zero for every coupling
     // that touches them (the Dirichlet problem of the owned rows); -1: none
     int32_t nown = -1;
+    // smoothed aggregation at level 0: P = (I - w D^-1 a2) P_tent with the
+    // mesh's a2 (per mesh: D^-1 (lambda a2) does not depend on lambda, and
+    // the per-timestep a1 is left out). 1 on, 0 off, -1 auto: on for
+    // irregular meshes (vertex valence standard deviation > 0.5: the random
+    // hull R3 1.33, icospheres <= 0.14). CPU prototype (tools/amg_proto.py,
+    // PCG its to 1e-4): R3 40 -> 18, C3 8 -> 6 for 7.5x the level-0 Galerkin
+    // terms and a level-1 operator with 2x the blocks per row.
+    int32_t smooth = -1;
+    float smooth_omega = 0.66f;
+    const double *a2 = nullptr;  // [sell_nb][4] level-0 a2 in the fine SELL layout (smoothing)
 };
 
 // One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser
@@ -38,7 +48,13 @@ struct AmgLevel {
     std::vector<float> Q;                          // (n, bs, 3) tentative prolongator rows
     std::vector<float> Qm;                         // the same rows in member (mlist) order
     std::vector<int32_t> gptr;                     // (next sell_nb + 1) Galerkin gather ranges
-    std::vector<int32_t> gent;                     // triples {fine SELL pos, i, j}
+    std::vector<int32_t> gent;                     // triples {fine SELL pos, P block of i, P block of j}
+    // smoothed prolongator (level 0 with AmgParams::smooth): P rows as blocks
+    // (bs x 3 floats each, in Q) with CSR pptr / pcol over the fine nodes, and
+    // the restriction lists per coarse node: pairs {fine node, P block}. The
+    // tentative prolongator is the special case pptr = 0..n, pcol = agg.
+    bool smoothed = false;
+    std::vector<int32_t> pptr, pcol, rptr, rent;
     int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
 };
 
@@ -49,6 +65,8 @@ struct AmgHierarchy {
 
 void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,
                AmgHierarchy &H);
+// deterministic per-mesh choice of AmgParams::smooth = -1
+bool amg_auto_smooth(const Pattern &fine);
 
 // Device copy of a level. Level 0 borrows the mesh's SELL arrays and the
 // inner solver's A32 / dinv32 / r / z; it owns only its smoother scratch.
@@ -59,6 +77,8 @@ struct AmgDevLevel {
     DevArray<uint8_t> dead;                          // level >= 1
     DevArray<int32_t> agg, mptr, apos, gptr, gent;  // transition to level + 1
     DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
+    bool smoothed = false;                          // level 0: smoothed prolongator
+    DevArray<int32_t> pptr, pcol, rptr, rent;
     int32_t ngrp = 0;
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap

@@ -262,6 +262,105 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
                         Dh22, Ah, Ah22, Afh);
 }
 
+// Level 0's Galerkin product with kNS systems per thread: the gather entry
+// (fine position, P blocks of i and j) and both P blocks are loaded once and
+// applied to the fine blocks of every system (level 0 has 7.5x the entries
+// with a smoothed prolongator). Fine blocks from the smoother's bf16 copy
+// (Afh) or the fp32 A (Af); same fold order per system as galerkin_block.
+#ifndef MOF_GAL_NS
+#define MOF_GAL_NS 1
+#endif
+constexpr int kGalNS = 4;
+__global__ __launch_bounds__(kWG) void k_galerkin0_ns(
+    int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
+    const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
+    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
+    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
+    const uint2 *__restrict__ Afh) {
+    // no fp contraction: every system slot of the unrolled loops rounds alike
+    // (a system's bits must not depend on its slot, i.e. on the batch split)
+#pragma clang fp contract(off)
+    int32_t tile, bq;
+    const int32_t nq = (B + kGalNS - 1) / kGalNS;
+    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), nq, tile, bq, kGrpGal)) return;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
+    if (pos >= c_sell_nb) return;
+    const int32_t I = c_sell_row[pos];
+    if (I >= nC) return;
+    const int32_t b0 = bq * kGalNS;
+    float Cm[kGalNS][3][3] = {};
+    const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
+    constexpr int U = 2;
+    for (int32_t t0 = g0; t0 < g1; t0 += U) {
+        int32_t fp[U], ii[U], jj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = min(t0 + u, g1 - 1);
+            fp[u] = gent[3 * g];
+            ii[u] = gent[3 * g + 1];
+            jj[u] = gent[3 * g + 2];
+        }
+        float qi[U][6], qj[U][6], a[U][kGalNS][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                qi[u][k] = Q[(int64_t)ii[u] * 6 + k];
+                qj[u][k] = Q[(int64_t)jj[u] * 6 + k];
+            }
+#pragma unroll
+            for (int t = 0; t < kGalNS; ++t) {
+                const int64_t bb = min(b0 + t, B - 1);
+                if (Afh) {
+                    const uint2 h = Afh[bb * f_sell_nb + max(fp[u], 0)];
+                    a[u][t][0] = bf16_lo(h.x); a[u][t][1] = bf16_hi(h.x);
+                    a[u][t][2] = bf16_lo(h.y); a[u][t][3] = bf16_hi(h.y);
+                } else {
+                    const float4 v = reinterpret_cast<const float4 *>(Af)[bb * f_sell_nb + max(fp[u], 0)];
+                    a[u][t][0] = v.x; a[u][t][1] = v.y; a[u][t][2] = v.z; a[u][t][3] = v.w;
+                }
+                if (fp[u] < 0) {  // a decomposed part's ghost block: identity / zero
+                    const float d = fp[u] == -1 ? 1.f : 0.f;
+                    a[u][t][0] = d; a[u][t][1] = 0.f; a[u][t][2] = 0.f; a[u][t][3] = d;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float on = t0 + u < g1 ? 1.f : 0.f;
+#pragma unroll
+            for (int t = 0; t < kGalNS; ++t) {
+                float T[2][3];  // A Q_j
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+                        T[r][c] = on * (a[u][t][2 * r] * qj[u][c] + a[u][t][2 * r + 1] * qj[u][3 + c]);
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) Cm[t][r][c] += qi[u][r] * T[0][c] + qi[u][3 + r] * T[1][c];
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kGalNS; ++t) {
+        const int32_t b = b0 + t;
+        if (b >= B) continue;
+        if (pos == c_diag[I]) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                if (c_dead[3 * (int64_t)I + d]) Cm[t][d][d] += 1.f;
+            float D[3][3];
+            inv3(Cm[t], D);
+            st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
+        }
+        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm[t]);
+        if (Ah) st_h9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm[t]);
+    }
+}
+
 constexpr int kMaxCoarse = 128;
 constexpr int kInvWG = 1024;
 constexpr int kSweepRows = kMaxCoarse * kMaxCoarse / kInvWG;  // 16 matrix rows per thread
@@ -356,7 +455,9 @@ struct Lvl {
     const uint16_t *Ah22;                // [B][sell_nb] entry (2,2)
     float *b, *x, *r, *y;                // [B][n][4] (level 0: x [B][n][2], r bf16 [B][n][2])
     const int32_t *agg, *mptr, *apos;    // transition to level + 1
-    const float *Q, *Qm;
+    const float *Q, *Qm;                 // tentative rows (node order / member order), or P blocks
+    const int32_t *pptr, *pcol;          // smoothed P: row blocks of each fine node
+    const int32_t *rptr, *rent;          // smoothed P: {fine node, P block} per coarse node
 };
 
 // 3x3 bf16 block stored as 8 entries in 16 B + entry (2,2) in 2 B
@@ -581,6 +682,138 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
     }
 }
 
+// Level 0 with a smoothed prolongator: b_C[I] = sum over I's restriction
+// list (fine node order) of P^T r (r in node order). As k_restrict: a
+// workgroup takes whole coarse nodes with at most kRGS list entries in
+// total and kNS systems; one thread per entry loads the entry and its P block
+// once and forms P_e^T r_i of every system into LDS, then one thread per
+// coarse node sums its entries in list order (per system); with smooth also
+// x_C[I] = w D_C^-1 b_C[I].
+constexpr int kNS = 4;     // systems per workgroup / thread in the smoothed-P kernels
+constexpr int kRGS = 512;  // list entries per restriction group (smoothed P)
+__global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
+                                                      int32_t B, int32_t smooth, float omega,
+                                                      const int32_t *__restrict__ sysi) {
+    // no fp contraction: every system slot of the unrolled loops rounds alike
+    // (a system's bits must not depend on its slot, i.e. on the batch split)
+#pragma clang fp contract(off)
+    __shared__ float con[kNS][3][kRGS];
+    int32_t g, bq;
+    const int32_t nq = (B + kNS - 1) / kNS;
+    if (!xcd_map(ngrp, nq, g, bq, kGrpRestr)) return;
+    const int32_t b0 = bq * kNS;
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < kNS; ++t) any |= b0 + t < B && !retired(sysi, b0 + t);
+    if (!any) return;
+    const int32_t I0 = grp[g], I1 = grp[g + 1];
+    const int32_t e0 = F.rptr[I0], e1 = F.rptr[I1];
+    const bool big = e1 - e0 > kRGS;  // one coarse node with an oversized list: summed from memory
+    auto contrib = [&](int32_t e, float (&c3)[kNS][3]) {
+        const int32_t i = F.rent[2 * (int64_t)e];
+        const float *p = F.Q + (int64_t)F.rent[2 * (int64_t)e + 1] * 6;
+        float pm[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) pm[k] = p[k];
+        float ri[kNS][2];
+#pragma unroll
+        for (int t = 0; t < kNS; ++t) ldr<2>(F.r, min(b0 + t, B - 1), F.n, i, ri[t]);
+#pragma unroll
+        for (int t = 0; t < kNS; ++t)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) c3[t][c] = pm[c] * ri[t][0] + pm[3 + c] * ri[t][1];
+    };
+    for (int32_t e = e0 + threadIdx.x; e < e1 && !big; e += kWG) {
+        float c3[kNS][3];
+        contrib(e, c3);
+#pragma unroll
+        for (int t = 0; t < kNS; ++t)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) con[t][c][e - e0] = c3[t][c];
+    }
+    __syncthreads();
+    for (int32_t I = I0 + threadIdx.x; I < I1; I += kWG) {
+        float acc[kNS][3] = {};
+        for (int32_t e = F.rptr[I]; e < F.rptr[I + 1]; ++e) {
+            float c3[kNS][3];
+            if (big) {
+                contrib(e, c3);
+            } else {
+#pragma unroll
+                for (int t = 0; t < kNS; ++t)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) c3[t][c] = con[t][c][e - e0];
+            }
+#pragma unroll
+            for (int t = 0; t < kNS; ++t)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[t][c] += c3[t][c];
+        }
+#pragma unroll
+        for (int t = 0; t < kNS; ++t) {
+            const int32_t b = b0 + t;
+            if (b >= B || retired(sysi, b)) continue;
+            const int64_t vo = (int64_t)b * C.n * 4;
+            stv<3>(C.b + vo, I, acc[t]);
+            if (smooth) {
+                float d[3][3], x[3];
+                ld_dh(C, b, I, d);
+                matvec<3>(d, acc[t], x);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) x[c] *= omega;
+                stv<3>(C.x + vo, I, x);
+            }
+        }
+    }
+}
+
+// Level 0 with a smoothed prolongator: x_i = x0_i + sum_k P_ik y_C[pcol k],
+// kNS systems per thread (the row's P blocks and columns loaded once)
+__global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk, int32_t B,
+                                                     const int32_t *__restrict__ sysi) {
+    // no fp contraction: every system slot of the unrolled loops rounds alike
+    // (a system's bits must not depend on its slot, i.e. on the batch split)
+#pragma clang fp contract(off)
+    int32_t rb, bq;
+    const int32_t nq = (B + kNS - 1) / kNS;
+    if (!xcd_map(nblk, nq, rb, bq, kGrpProl)) return;
+    const int32_t b0 = bq * kNS;
+    const int32_t i = rb * kWG + threadIdx.x;
+    if (i >= F.n) return;
+    float x[kNS][2];
+#pragma unroll
+    for (int t = 0; t < kNS; ++t) {
+        const float2 v = ld_x0(F.x, (int64_t)min(b0 + t, B - 1) * F.n + i);
+        x[t][0] = v.x;
+        x[t][1] = v.y;
+    }
+    const int32_t k0 = F.pptr[i], k1 = F.pptr[i + 1];
+    for (int32_t k = k0; k < k1; ++k) {
+        const int32_t K = F.pcol[k];
+        const float *q = F.Q + (int64_t)k * 6;
+        float qm[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) qm[c] = q[c];
+        float y[kNS][3];
+#pragma unroll
+        for (int t = 0; t < kNS; ++t) ldv<3>(C.y + (int64_t)min(b0 + t, B - 1) * C.n * 4, K, y[t]);
+#pragma unroll
+        for (int t = 0; t < kNS; ++t) {
+            x[t][0] += qm[0] * y[t][0] + qm[1] * y[t][1] + qm[2] * y[t][2];
+            x[t][1] += qm[3] * y[t][0] + qm[4] * y[t][1] + qm[5] * y[t][2];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kNS; ++t) {
+        const int32_t b = b0 + t;
+        if (b >= B || retired(sysi, b)) continue;
+        if constexpr (MOF_X0_BF16 == 2)  // full-precision x for the post-smoothing
+            reinterpret_cast<float2 *>(F.y)[(int64_t)b * F.n + i] = make_float2(x[t][0], x[t][1]);
+        else
+            st_x0(F.x, (int64_t)b * F.n + i, x[t][0], x[t][1]);
+    }
+}
+
 template <int BSF>
 __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__restrict__ sysi) {
     const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
@@ -736,6 +969,7 @@ bool amg_build(mof_mesh *m) {
     AmgParams prm;
     if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
     if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
+    if (const char *v = std::getenv("MOF_AMG_SMOOTH")) prm.smooth = std::atoi(v);  // 1 / 0 force, unset auto
     if (m->n_own < m->N) prm.nown = m->n_own;
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
@@ -744,6 +978,14 @@ bool amg_build(mof_mesh *m) {
     std::vector<double> e(6 * (size_t)m->N);
     MOF_HIP(hipMemcpyAsync(e.data(), m->e.p, e.size() * sizeof(double), hipMemcpyDeviceToHost, s));
     MOF_HIP(hipStreamSynchronize(s));
+    // the mesh's a2 (unscaled, fine SELL layout) for the smoothed prolongator
+    std::vector<double> a2;
+    if (prm.nown < 0 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) {
+        a2.resize(4 * (size_t)m->pat.sell_nb());
+        MOF_HIP(hipMemcpyAsync(a2.data(), m->a2.p, a2.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        MOF_HIP(hipStreamSynchronize(s));
+        prm.a2 = a2.data();
+    }
     AmgHierarchy H;
     build_amg(m->pat, e.data(), prm, H);
     G.omega = prm.omega;
@@ -785,12 +1027,21 @@ bool amg_build(mof_mesh *m) {
             put_i(D.gent, L.gent);
             put_f(D.Q, L.Q);
             put_f(D.Qm, L.Qm);
-            // restriction groups: whole aggregates, <= kRG members each
+            D.smoothed = L.smoothed;
+            if (L.smoothed) {
+                put_i(D.pptr, L.pptr);
+                put_i(D.pcol, L.pcol);
+                put_i(D.rptr, L.rptr);
+                put_i(D.rent, L.rent);
+            }
+            // restriction groups: whole aggregates, <= kRG members (smoothed P:
+            // restriction list entries) each
             std::vector<int32_t> grp{0};
-            const int32_t na = (int32_t)L.mptr.size() - 1;
+            const std::vector<int32_t> &gp = L.smoothed ? L.rptr : L.mptr;
+            const int32_t na = (int32_t)gp.size() - 1;
             for (int32_t I = 0; I < na; ++I) {
                 const int32_t g0 = grp.back();
-                if (I > g0 && L.mptr[I + 1] - L.mptr[g0] > kRG) grp.push_back(I);
+                if (I > g0 && gp[I + 1] - gp[g0] > (L.smoothed ? kRGS : kRG)) grp.push_back(I);
             }
             grp.push_back(na);
             D.ngrp = (int32_t)grp.size() - 1;
@@ -801,8 +1052,9 @@ bool amg_build(mof_mesh *m) {
     G.cap = 0;
     if (std::getenv("MOF_AMG_VERBOSE")) {
         for (size_t l = 0; l < H.levels.size(); ++l)
-            std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld\n", l, H.levels[l].n,
-                         H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb());
+            std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld%s\n", l, H.levels[l].n,
+                         H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb(),
+                         H.levels[l].smoothed ? " (smoothed P)" : "");
     }
     MOF_HIP(hipStreamSynchronize(s));
     return true;
@@ -882,12 +1134,24 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     G.bf16_fresh = false;
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
-        if (l == 0)
+        if (l == 0 && MOF_GAL_NS)
+            k_galerkin0_ns<<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGalNS - 1) / kGalNS,
+                                           kGrpGal)),
+                             kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p,
+                                          F.Q.p, w.A32.p, m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
+                                          F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
+                                              ? nullptr
+                                              : reinterpret_cast<const uint2 *>(G.A0h.p));
+        else if (l == 0)
             k_galerkin<2><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
                                                               m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p,
                                                               ah(C), ah22(C),
-                                                              reinterpret_cast<const uint2 *>(G.A0h.p));
+                                                              // a smoothed P's product cancels far more (its
+                                                              // columns are A-smooth): fp32 blocks
+                                                              F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
+                                                                  ? nullptr
+                                                                  : reinterpret_cast<const uint2 *>(G.A0h.p));
         else
             k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
@@ -920,6 +1184,10 @@ Lvl level_view(const AmgDevLevel &D) {
     v.apos = D.apos.p;
     v.Q = D.Q.p;
     v.Qm = D.Qm.p;
+    v.pptr = D.pptr.p;
+    v.pcol = D.pcol.p;
+    v.rptr = D.rptr.p;
+    v.rent = D.rent.p;
     return v;
 }
 
@@ -943,8 +1211,13 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
             k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x, v[0].apos, sysi, v[0].r);
-            k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
-                v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
+            if (G.lv[0].smoothed) {
+                k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNS - 1) / kNS, kGrpRestr)), kWG, 0, s>>>(
+                    v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
+            } else {
+                k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
+                    v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
+            }
         } else {
             k_res3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], sysi);
             k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
@@ -963,7 +1236,11 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = S - 1; l >= 0; --l) {
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
-            k_prolong0<<<dim3(xcd_grid(nb0, B, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+            if (G.lv[0].smoothed)
+                k_prolong0_sa<<<dim3(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B,
+                                                                                             sysi);
+            else
+                k_prolong0<<<dim3(xcd_grid(nb0, B, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
             k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, reinterpret_cast<const uint2 *>(G.D0h.p), r0,
                                        MOF_X0_BF16 == 2 ? v[0].y : v[0].x, om, sysi, z0, part_slot, rd);
         } else {

@@ -136,7 +136,83 @@ void sell_layout(AmgLevel &L) {
     }
 }
 
+// P = (I - w D^-1 a2) Q at level 0 (bs = 2): row i gets its own tentative
+// block and -w D_i^-1 a2_ij Q_j for every neighbour j (itself included), in
+// the row's block order, merged per aggregate; rows sorted by aggregate.
+void smooth_prolongator(const Pattern &fine, const AmgParams &prm, const std::vector<int32_t> &agg,
+                        const std::vector<float> &Q, std::vector<int32_t> &pptr, std::vector<int32_t> &pcol,
+                        std::vector<float> &P) {
+    const int32_t n = fine.N;
+    std::vector<double> ab(4 * fine.vcol.size(), 0.0);  // a2 per adjacency block
+    for (size_t pos = 0; pos < fine.sell_blk.size(); ++pos)
+        if (fine.sell_blk[pos] >= 0)
+            for (int k = 0; k < 4; ++k) ab[4 * (size_t)fine.sell_blk[pos] + k] = prm.a2[4 * pos + k];
+    const double w = prm.smooth_omega;
+    pptr.assign(n + 1, 0);
+    pcol.clear();
+    P.clear();
+    std::vector<int32_t> rk;
+    std::vector<double> rv;
+    for (int32_t i = 0; i < n; ++i) {
+        rk.clear();
+        rv.clear();
+        auto add = [&](int32_t K, const double (&t)[6]) {
+            size_t e = 0;
+            while (e < rk.size() && rk[e] != K) ++e;
+            if (e == rk.size()) {
+                rk.push_back(K);
+                rv.insert(rv.end(), 6, 0.0);
+            }
+            for (int c = 0; c < 6; ++c) rv[6 * e + c] += t[c];
+        };
+        double own[6];
+        for (int c = 0; c < 6; ++c) own[c] = Q[6 * (size_t)i + c];
+        add(agg[i], own);
+        int32_t qd = -1;
+        for (int32_t q = fine.vptr[i]; q < fine.vptr[i + 1]; ++q)
+            if (fine.vcol[q] == i) qd = q;
+        const double *d = qd >= 0 ? &ab[4 * (size_t)qd] : nullptr;
+        const double det = d ? d[0] * d[3] - d[1] * d[2] : 0.0;
+        if (d && det != 0.0 && std::isfinite(det)) {
+            const double di[4] = {d[3] / det, -d[1] / det, -d[2] / det, d[0] / det};
+            for (int32_t q = fine.vptr[i]; q < fine.vptr[i + 1]; ++q) {
+                const int32_t j = fine.vcol[q];
+                const double *a = &ab[4 * (size_t)q];
+                const double m[4] = {di[0] * a[0] + di[1] * a[2], di[0] * a[1] + di[1] * a[3],
+                                     di[2] * a[0] + di[3] * a[2], di[2] * a[1] + di[3] * a[3]};
+                double t[6];
+                for (int r = 0; r < 2; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        t[3 * r + c] = -w * (m[2 * r] * Q[6 * (size_t)j + c] + m[2 * r + 1] * Q[6 * (size_t)j + 3 + c]);
+                add(agg[j], t);
+            }
+        }
+        std::vector<size_t> ord(rk.size());
+        for (size_t e = 0; e < ord.size(); ++e) ord[e] = e;
+        std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return rk[x] < rk[y]; });
+        for (size_t e : ord) {
+            pcol.push_back(rk[e]);
+            for (int c = 0; c < 6; ++c) P.push_back((float)rv[6 * e + c]);
+        }
+        pptr[i + 1] = (int32_t)pcol.size();
+    }
+}
+
 }  // namespace
+
+bool amg_auto_smooth(const Pattern &fine) {
+    // vertex valence = adjacency row length minus the diagonal
+    const int32_t n = fine.N;
+    if (n <= 0) return false;
+    double s = 0.0, s2 = 0.0;
+    for (int32_t i = 0; i < n; ++i) {
+        const double v = fine.vptr[i + 1] - fine.vptr[i] - 1;
+        s += v;
+        s2 += v * v;
+    }
+    const double mean = s / n, var = std::max(0.0, s2 / n - mean * mean);
+    return std::sqrt(var) > 0.5;
+}
 
 void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,
                AmgHierarchy &H) {
@@ -205,7 +281,36 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         F.Qm.assign(F.Q.size(), 0.f);
         for (int32_t q = 0; q < F.n; ++q)
             std::copy_n(F.Q.begin() + (size_t)F.mlist[q] * bs * 3, bs * 3, F.Qm.begin() + (size_t)q * bs * 3);
-        // coarse pattern: (agg(i), agg(j)) of every fine block, sorted
+        // prolongator rows: the tentative Q (one block per node), or smoothed
+        const bool smooth = H.levels.size() == 1 && prm.nown < 0 && prm.a2 &&
+                            (prm.smooth > 0 || (prm.smooth < 0 && amg_auto_smooth(fine)));
+        if (smooth) {
+            std::vector<float> P;
+            smooth_prolongator(fine, prm, agg, F.Q, F.pptr, F.pcol, P);
+            F.Q.swap(P);  // P blocks, indexed by the gather lists and the prolongation
+            F.smoothed = true;
+            for (int32_t i = 0; i < F.n; ++i) F.apos[i] = i;  // restriction gathers by node
+        } else {
+            F.pptr.resize(F.n + 1);
+            for (int32_t i = 0; i <= F.n; ++i) F.pptr[i] = i;
+            F.pcol = agg;
+        }
+        // restriction lists: coarse node -> {fine node, P block}, fine node order
+        F.rptr.assign(nc + 1, 0);
+        for (int32_t k = 0; k < F.pptr[F.n]; ++k) F.rptr[F.pcol[k] + 1]++;
+        for (int32_t I = 0; I < nc; ++I) F.rptr[I + 1] += F.rptr[I];
+        F.rent.assign(2 * (size_t)F.pptr[F.n], 0);
+        {
+            std::vector<int32_t> fill(F.rptr.begin(), F.rptr.end() - 1);
+            for (int32_t i = 0; i < F.n; ++i)
+                for (int32_t k = F.pptr[i]; k < F.pptr[i + 1]; ++k) {
+                    const int32_t e = fill[F.pcol[k]]++;
+                    F.rent[2 * (size_t)e] = i;
+                    F.rent[2 * (size_t)e + 1] = k;
+                }
+        }
+        // coarse pattern: (K, L) for every fine block (i, j), K of a P block of
+        // row i and L of one of row j
         AmgLevel C;
         C.n = nc;
         C.bs = 3;
@@ -213,7 +318,11 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         {
             std::vector<std::vector<int32_t>> rows(nc);
             for (int32_t i = 0; i < F.n; ++i)
-                for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) rows[agg[i]].push_back(agg[F.vcol[q]]);
+                for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) {
+                    const int32_t j = F.vcol[q];
+                    for (int32_t ka = F.pptr[i]; ka < F.pptr[i + 1]; ++ka)
+                        for (int32_t kb = F.pptr[j]; kb < F.pptr[j + 1]; ++kb) rows[F.pcol[ka]].push_back(F.pcol[kb]);
+                }
             C.vptr.assign(nc + 1, 0);
             for (int32_t I = 0; I < nc; ++I) {
                 auto &r = rows[I];
@@ -221,21 +330,28 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
                 r.erase(std::unique(r.begin(), r.end()), r.end());
                 C.vcol.insert(C.vcol.end(), r.begin(), r.end());
                 C.vptr[I + 1] = (int32_t)C.vcol.size();
+                std::vector<int32_t>().swap(r);
             }
         }
         sell_layout(C);
-        // Galerkin gather lists: coarse block -> fine blocks (in fine block order)
+        // Galerkin gather lists: coarse block -> terms P_iK^T A_ij P_jL, in fine
+        // block order (then P block order)
         const int32_t cnb = (int32_t)C.vcol.size();
-        std::vector<int32_t> cblk_of_fine(F.vcol.size());
+        std::vector<int32_t> term_cb;
         std::vector<int32_t> cnt(cnb + 1, 0);
         for (int32_t i = 0; i < F.n; ++i)
             for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) {
-                const int32_t I = agg[i], J = agg[F.vcol[q]];
-                const int32_t p = (int32_t)(std::lower_bound(C.vcol.begin() + C.vptr[I],
-                                                             C.vcol.begin() + C.vptr[I + 1], J) -
-                                            C.vcol.begin());
-                cblk_of_fine[q] = p;
-                cnt[p + 1]++;
+                const int32_t j = F.vcol[q];
+                for (int32_t ka = F.pptr[i]; ka < F.pptr[i + 1]; ++ka) {
+                    const int32_t I = F.pcol[ka];
+                    for (int32_t kb = F.pptr[j]; kb < F.pptr[j + 1]; ++kb) {
+                        const int32_t p = (int32_t)(std::lower_bound(C.vcol.begin() + C.vptr[I],
+                                                                     C.vcol.begin() + C.vptr[I + 1], F.pcol[kb]) -
+                                                    C.vcol.begin());
+                        term_cb.push_back(p);
+                        cnt[p + 1]++;
+                    }
+                }
             }
         for (int32_t p = 0; p < cnb; ++p) cnt[p + 1] += cnt[p];
         // gather ranges indexed by coarse SELL position
@@ -243,18 +359,22 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         for (int64_t pos = 0; pos < (int64_t)F.sell_blk.size(); ++pos)
             if (F.sell_blk[pos] >= 0) fine_pos[F.sell_blk[pos]] = (int32_t)pos;
         F.gptr.assign(C.sell_blk.size() + 1, 0);
-        std::vector<int32_t> by_block(cnt.back() * 3);
+        std::vector<int32_t> by_block((size_t)cnt.back() * 3);
         {
             std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+            size_t t = 0;
             for (int32_t i = 0; i < F.n; ++i)
                 for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) {
-                    const int32_t p = cblk_of_fine[q];
-                    const int32_t k = fill[p]++;
-                    const bool ghost = H.levels.size() == 1 && prm.nown >= 0 &&
-                                       (i >= prm.nown || F.vcol[q] >= prm.nown);
-                    by_block[3 * k + 0] = ghost ? (F.vcol[q] == i ? -1 : -2) : fine_pos[q];
-                    by_block[3 * k + 1] = i;
-                    by_block[3 * k + 2] = F.vcol[q];
+                    const int32_t j = F.vcol[q];
+                    // a decomposed part's ghost couplings (tentative P only)
+                    const bool ghost = H.levels.size() == 1 && prm.nown >= 0 && (i >= prm.nown || j >= prm.nown);
+                    for (int32_t ka = F.pptr[i]; ka < F.pptr[i + 1]; ++ka)
+                        for (int32_t kb = F.pptr[j]; kb < F.pptr[j + 1]; ++kb) {
+                            const size_t k = (size_t)fill[term_cb[t++]]++;
+                            by_block[3 * k + 0] = ghost ? (j == i ? -1 : -2) : fine_pos[q];
+                            by_block[3 * k + 1] = ka;
+                            by_block[3 * k + 2] = kb;
+                        }
                 }
         }
         F.gent.clear();
@@ -262,7 +382,7 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         for (int64_t pos = 0; pos < (int64_t)C.sell_blk.size(); ++pos) {
             const int32_t p = C.sell_blk[pos];
             if (p >= 0)
-                F.gent.insert(F.gent.end(), by_block.begin() + 3 * cnt[p], by_block.begin() + 3 * cnt[p + 1]);
+                F.gent.insert(F.gent.end(), by_block.begin() + 3 * (size_t)cnt[p], by_block.begin() + 3 * (size_t)cnt[p + 1]);
             F.gptr[pos + 1] = (int32_t)(F.gent.size() / 3);
         }
         B.swap(Bc);
