@@ -99,22 +99,22 @@ __device__ __forceinline__ int64_t red_rec(const RedArgs &rd, int32_t B, int32_t
 
 // Sum over all parts' partial records of system b, in one fixed order (part,
 // then workgroup), so every part of a decomposed solve gets the same bits.
-template <int NV>
+template <int NV, int NT = kWG>
 __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd, int32_t B, int32_t b,
                                            double (&out)[NV], double *lds) {
     if (rd.P == 1) {
-        reduce_partials<NV>(slot + (int64_t)NV * b * rd.nmax, rd.nmax, out, lds);
+        reduce_partials<NV, NT>(slot + (int64_t)NV * b * rd.nmax, rd.nmax, out, lds);
         return;
     }
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = 0.0;
     for (int32_t q = 0; q < rd.P; ++q) {
         const double *p = slot + (int64_t)NV * ((int64_t)q * B + b) * rd.nmax;
-        for (int32_t w = threadIdx.x; w < rd.nmax; w += kWG)
+        for (int32_t w = threadIdx.x < kWG ? (int32_t)threadIdx.x : rd.nmax; w < rd.nmax; w += kWG)
 #pragma unroll
             for (int k = 0; k < NV; ++k) out[k] += p[(int64_t)w * NV + k];
     }
-    block_sum<NV>(out, lds);
+    block_sum<NV, NT>(out, lds);
 }
 
 #ifndef MOF_RES_U
@@ -265,9 +265,20 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, doub
     }
 }
 
-template <typename V, bool FIRST>
+// fp32 SpMV workgroup: kRowsPerWG rows as kSpmvRows rows per thread (4: 256
+// threads, the other row kernels' shape; 1: 1024 threads, all rows of the
+// row block at once, so the neighbouring row blocks of a system run in step
+// and the transposed reads of the symmetric layout meet their lines in L2)
+#ifndef MOF_SPMV_ROWS
+#define MOF_SPMV_ROWS 4
+#endif
+constexpr int kSpmvRows = MOF_SPMV_ROWS;
+constexpr int kSpmvWG = kRowsPerWG / kSpmvRows;
+
+template <typename V, bool FIRST, int NT = kWG>
 __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
-    __shared__ double lds[8];
+    constexpr int RPT = kRowsPerWG / NT;  // rows per thread
+    __shared__ double lds[2 * (NT / 64)];
     int32_t rb, b;
     if (!xcd_map(a.nblk, a.B, rb, b, kGrpSpmv)) return;
     const bool force = flags & kForce;
@@ -277,7 +288,7 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
         return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;  // slot stride
     double cur[2];
-    reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
+    reduce_sys<2, NT>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
     if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
         if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
             a.sysi[b * kSysStride + SI_CONV] = it;
@@ -292,15 +303,15 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     V beta = 0;
     if (!FIRST) {
         double old[2];
-        reduce_sys<2>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
+        reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
         beta = (V)(cur[0] / old[0]);
     }
     using V2 = typename VT<V>::V2;
     const int64_t vb = (int64_t)b * a.N;
     double pq = 0.0;
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+    for (int r = 0; r < RPT; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
         if (i >= a.N) break;
         V y0, y1;
         spmv_row<V>(a.mat, b, i, a.z + 2 * vb, y0, y1);
@@ -321,7 +332,7 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
         if (i < a.red.nown) pq += (double)pi.x * qi.x + (double)pi.y * qi.y;
     }
     double v[1] = {pq};
-    block_sum<1>(v, lds);
+    block_sum<1, NT>(v, lds);
     if (threadIdx.x == 0) a.part_pq[red_rec(a.red, a.B, b, rb)] = v[0];
 }
 
@@ -332,15 +343,18 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
     pcg_spmv_body<V, FIRST>(a, it, flags);
 }
 template <>
-__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_pcg_spmv<float, true>(PcgArgs<float> a, int32_t it,
-                                                                             int32_t flags) {
-    pcg_spmv_body<float, true>(a, it, flags);
+__global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, true>(PcgArgs<float> a, int32_t it,
+                                                                                 int32_t flags) {
+    pcg_spmv_body<float, true, kSpmvWG>(a, it, flags);
 }
 template <>
-__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_pcg_spmv<float, false>(PcgArgs<float> a, int32_t it,
-                                                                              int32_t flags) {
-    pcg_spmv_body<float, false>(a, it, flags);
+__global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, false>(PcgArgs<float> a, int32_t it,
+                                                                                  int32_t flags) {
+    pcg_spmv_body<float, false, kSpmvWG>(a, it, flags);
 }
+// workgroup size of an SpMV launch
+template <typename V>
+constexpr int spmv_wg() { return sizeof(V) == 4 ? kSpmvWG : kWG; }
 
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
@@ -697,15 +711,15 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 // and end of its execution, as rocprof's kernel trace), not
                 // separate marker packets around it
                 if (it == 0)
-                    hipExtLaunchKernelGGL(k_pcg_spmv<V, true>, gx, dim3(kWG), 0, s, ev[2 * c], ev[2 * c + 1], 0, a,
+                    hipExtLaunchKernelGGL(k_pcg_spmv<V, true>, gx, dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0, a,
                                           it, 0);
                 else
-                    hipExtLaunchKernelGGL(k_pcg_spmv<V, false>, gx, dim3(kWG), 0, s, ev[2 * c], ev[2 * c + 1], 0,
+                    hipExtLaunchKernelGGL(k_pcg_spmv<V, false>, gx, dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0,
                                           a, it, 0);
             } else if (it == 0) {
-                k_pcg_spmv<V, true><<<gx, kWG, 0, s>>>(a, it, 0);
+                k_pcg_spmv<V, true><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
             } else {
-                k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(a, it, 0);
+                k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
             }
             k_pcg_update<V><<<g, kWG, 0, s>>>(a, it);
             if (amg) precond((it + 1) & 1);
@@ -727,7 +741,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     }
     if (!done) {
         // one more check launch so SI_CONV records systems converged at max_iter
-        k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(a, it, 0);
+        k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
         if (sp.fail_at_max_iter) k_fail_running<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, it, a.sysi);
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -986,9 +1000,9 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
         for (size_t l = 0; l < L; ++l) {
             const dim3 gx(xcd_grid(d->parts[l]->ws.nblk, B, kGrpSpmv));
             if (first)
-                k_pcg_spmv<V, true><<<gx, kWG, 0, s>>>(args[l], it_, 0);
+                k_pcg_spmv<V, true><<<gx, spmv_wg<V>(), 0, s>>>(args[l], it_, 0);
             else
-                k_pcg_spmv<V, false><<<gx, kWG, 0, s>>>(args[l], it_, 0);
+                k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(args[l], it_, 0);
         }
         dd_sync_partials(d, d->part_pq.p, rec, s);
     };
@@ -1120,10 +1134,10 @@ double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipS
     auto launch = [&]() {
         if (precision == MOF_PREC_MIXED) {
             PcgArgs<float> a = make_args<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p);
-            k_pcg_spmv<float, false><<<gx, kWG, 0, s>>>(a, 1, kForce);
+            k_pcg_spmv<float, false><<<gx, spmv_wg<float>(), 0, s>>>(a, 1, kForce);
         } else {
             PcgArgs<double> a = make_args<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p);
-            k_pcg_spmv<double, false><<<gx, kWG, 0, s>>>(a, 1, kForce);
+            k_pcg_spmv<double, false><<<gx, spmv_wg<double>(), 0, s>>>(a, 1, kForce);
         }
     };
     for (int r = 0; r < 3; ++r) launch();

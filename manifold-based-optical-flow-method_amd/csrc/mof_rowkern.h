@@ -44,8 +44,10 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;  // valid in lane 0
 }
 
-// Deterministic workgroup sum of NV values; every thread gets the result.
-template <int NV>
+// Deterministic workgroup sum of NV values over NT threads (lds: NT / 64 * NV
+// doubles), waves summed in order; every thread gets the result. Waves that
+// contribute 0 leave the bits of the 256-thread sum unchanged.
+template <int NV, int NT = kWG>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
@@ -56,17 +58,23 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = ((lds[k] + lds[NV + k]) + lds[2 * NV + k]) + lds[3 * NV + k];
+    for (int k = 0; k < NV; ++k) {
+        double s = ((lds[k] + lds[NV + k]) + lds[2 * NV + k]) + lds[3 * NV + k];
+#pragma unroll
+        for (int q = 4; q < NT / 64; ++q) s += lds[q * NV + k];
+        v[k] = s;
+    }
     __syncthreads();
 }
 
-// Sum n partials of NV values each (record stride NV) in a fixed order.
-template <int NV>
+// Sum n partials of NV values each (record stride NV) in a fixed order: the
+// first kWG threads load, so any workgroup size NT gets the same bits.
+template <int NV, int NT = kWG>
 __device__ __forceinline__ void reduce_partials(const double *part, int n, double (&out)[NV],
                                                 double *lds) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = 0.0;
-    int q = threadIdx.x;
+    int q = threadIdx.x < kWG ? (int)threadIdx.x : n;
     for (; q + 3 * kWG < n; q += 4 * kWG) {  // four independent loads in flight
         double v[4][NV];
 #pragma unroll
@@ -82,7 +90,7 @@ __device__ __forceinline__ void reduce_partials(const double *part, int n, doubl
 #pragma unroll
         for (int k = 0; k < NV; ++k) out[k] += part[(int64_t)q * NV + k];
     }
-    block_sum<NV>(out, lds);
+    block_sum<NV, NT>(out, lds);
 }
 
 // Materialised A of B systems (inner PCG operator).
