@@ -330,7 +330,15 @@ def main():
                 "us_per_full_launch": round(1e3 * agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]), 2),
                 "full_launch_frac": round((B * per_sys + shared)
                                           / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3)
-                                          / 1e9 / HBM_PEAK_GBS, 4) if agg["ms_spmv_full"] > 0 else None}
+                                          / 1e9 / HBM_PEAK_GBS, 4) if agg["ms_spmv_full"] > 0 else None,
+                "symmetric_reads": nread < info["nblocks"]}
+    if nread < info["nblocks"] and agg["ms_spmv_full"] > 0:
+        # context only: the plain layout's bytes (every block read at its own
+        # position, no mirror table) over this kernel's full-launch time, i.e.
+        # the rate the plain kernel would need to match it
+        plain = B * (info["nblocks"] * 4 * sv + N * 2 * sv * 5) + info["nblocks"] * 4
+        roofline["plain_layout_equiv_frac"] = round(
+            plain / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and not dry:

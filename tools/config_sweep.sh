@@ -14,4 +14,5 @@ $S 400 $o/C4_strong_n1.json python3 bench.py --fixed-timesteps 5000 --steps 2 --
 MOF_BENCH_REHEARSE=1 $S 400 $o/C3_rehearse_n2.json python3 bench.py --gpus 2 --steps 6 --warmup 1 --no-cpu-baseline || exit 99
 $S 400 $o/dd_c5_p8.json python3 bench_dd.py --parts 8 --config C5 --batch 64 --steps 3 --warmup 1 || exit 99
 $S 400 $o/dd_c5_p8_amg.json python3 bench_dd.py --parts 8 --config C5 --batch 64 --steps 3 --warmup 1 --precond amg || exit 99
+$S 400 $o/R3.json python3 bench.py --config R3 --batch 256 --steps 6 --warmup 1 --no-cpu-baseline || exit 99
 $S 600 $o/rows.jsonl python3 bench_rows.py || exit 99
