@@ -30,6 +30,10 @@ struct AmgParams {
     int32_t smooth = -1;
     float smooth_omega = 0.66f;
     const double *a2 = nullptr;  // [sell_nb][4] level-0 a2 in the fine SELL layout (smoothing)
+    // the fine level's mirror table when its operators are read symmetrically
+    // (sell_mirror): level-0 gather entries of lower blocks then point at the
+    // transposed upper block (| kMirT), which is all the assembly writes
+    const int32_t *mirror = nullptr;
 };
 
 // One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser
@@ -48,7 +52,7 @@ struct AmgLevel {
     std::vector<float> Q;                          // (n, bs, 3) tentative prolongator rows
     std::vector<float> Qm;                         // the same rows in member (mlist) order
     std::vector<int32_t> gptr;                     // (next sell_nb + 1) Galerkin gather ranges
-    std::vector<int32_t> gent;                     // triples {fine SELL pos, P block of i, P block of j}
+    std::vector<int32_t> gent;                     // triples {fine SELL pos (| kMirT: transposed), P block of i, P block of j}
     // smoothed prolongator (level 0 with AmgParams::smooth): P rows as blocks
     // (bs x 3 floats each, in Q) with CSR pptr / pcol over the fine nodes, and
     // the restriction lists per coarse node: pairs {fine node, P block}. The

@@ -176,17 +176,25 @@ __device__ __forceinline__ void galerkin_block(
         for (int u = 0; u < U; ++u) {
             // fp -1 / -2: a decomposed part's ghost block, identity / zero
             if constexpr (BSF == 2) {
+                // level 0 (symmetric layout: a lower block is the transpose of
+                // the upper block the entry points at)
+                const int32_t fq = fp[u] < 0 ? 0 : fp[u] & kMirPos;
                 if (Afh) {
                     // level 0: the smoother's bf16 blocks (8 B per block; the
                     // product's scattered gathers touch half the cache lines
                     // of the fp32 A: 5.35 vs 6.78 ms per 256 systems, same
                     // iteration counts) -- the coarse operator is then the
                     // Galerkin product of the operator the smoother sweeps
-                    const uint2 t = Afh[(int64_t)b * f_sell_nb + max(fp[u], 0)];
+                    const uint2 t = Afh[(int64_t)b * f_sell_nb + fq];
                     a[u][0][0] = bf16_lo(t.x); a[u][0][1] = bf16_hi(t.x);
                     a[u][1][0] = bf16_lo(t.y); a[u][1][1] = bf16_hi(t.y);
                 } else {
-                    ldm<BSF>(A, max(fp[u], 0), a[u]);
+                    ldm<BSF>(A, fq, a[u]);
+                }
+                if (fp[u] >= 0 && (fp[u] & kMirT)) {
+                    const float t01 = a[u][0][1];
+                    a[u][0][1] = a[u][1][0];
+                    a[u][1][0] = t01;
                 }
             } else {
                 // level >= 1: the fp32 operator (its bf16 sweep copy: 620 vs
@@ -309,16 +317,23 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
                 qi[u][k] = Q[(int64_t)ii[u] * 6 + k];
                 qj[u][k] = Q[(int64_t)jj[u] * 6 + k];
             }
+            const int32_t fq = fp[u] < 0 ? 0 : fp[u] & kMirPos;
+            const bool tr = fp[u] >= 0 && (fp[u] & kMirT);  // transposed upper block
 #pragma unroll
             for (int t = 0; t < kGalNS; ++t) {
                 const int64_t bb = min(b0 + t, B - 1);
                 if (Afh) {
-                    const uint2 h = Afh[bb * f_sell_nb + max(fp[u], 0)];
+                    const uint2 h = Afh[bb * f_sell_nb + fq];
                     a[u][t][0] = bf16_lo(h.x); a[u][t][1] = bf16_hi(h.x);
                     a[u][t][2] = bf16_lo(h.y); a[u][t][3] = bf16_hi(h.y);
                 } else {
-                    const float4 v = reinterpret_cast<const float4 *>(Af)[bb * f_sell_nb + max(fp[u], 0)];
+                    const float4 v = reinterpret_cast<const float4 *>(Af)[bb * f_sell_nb + fq];
                     a[u][t][0] = v.x; a[u][t][1] = v.y; a[u][t][2] = v.z; a[u][t][3] = v.w;
+                }
+                if (tr) {
+                    const float t01 = a[u][t][1];
+                    a[u][t][1] = a[u][t][2];
+                    a[u][t][2] = t01;
                 }
                 if (fp[u] < 0) {  // a decomposed part's ghost block: identity / zero
                     const float d = fp[u] == -1 ? 1.f : 0.f;
@@ -985,6 +1000,11 @@ bool amg_build(mof_mesh *m) {
         MOF_HIP(hipMemcpyAsync(a2.data(), m->a2.p, a2.size() * sizeof(double), hipMemcpyDeviceToHost, s));
         MOF_HIP(hipStreamSynchronize(s));
         prm.a2 = a2.data();
+    }
+    std::vector<int32_t> mir;
+    if (m->sym_reads && MOF_SKIP_LOWER) {
+        mir = sell_mirror(m->pat, m->n_own, 1, nullptr);
+        prm.mirror = mir.data();
     }
     AmgHierarchy H;
     build_amg(m->pat, e.data(), prm, H);

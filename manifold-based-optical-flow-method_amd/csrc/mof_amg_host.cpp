@@ -371,7 +371,9 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
                     for (int32_t ka = F.pptr[i]; ka < F.pptr[i + 1]; ++ka)
                         for (int32_t kb = F.pptr[j]; kb < F.pptr[j + 1]; ++kb) {
                             const size_t k = (size_t)fill[term_cb[t++]]++;
-                            by_block[3 * k + 0] = ghost ? (j == i ? -1 : -2) : fine_pos[q];
+                            by_block[3 * k + 0] = ghost ? (j == i ? -1 : -2)
+                                                  : H.levels.size() == 1 && prm.mirror ? prm.mirror[fine_pos[q]]
+                                                                                       : fine_pos[q];
                             by_block[3 * k + 1] = ka;
                             by_block[3 * k + 2] = kb;
                         }

@@ -464,7 +464,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows(
     const int4 *__restrict__ tinc, const int32_t *__restrict__ tslot, const float *__restrict__ w12,
     const float *__restrict__ a2s, const float *__restrict__ u, const double *__restrict__ fc, int block_jacobi,
     float *__restrict__ A, float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
-    uint2 *__restrict__ Dh, int32_t nown) {
+    uint2 *__restrict__ Dh, int32_t nown, const int32_t *__restrict__ mir) {
     int32_t rb, b;
     if (!xcd_map(nblk, B, rb, b, kGrpAsm)) return;
     const float *ub = u + 6 * (int64_t)b * (M + 1);
@@ -540,6 +540,9 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows(
         for (int z = 0; z < WMAX; ++z) {
             if (z >= deg) continue;
             const int64_t pos = o + (int64_t)z * kSlice + l;
+            // symmetric layout: lower blocks are read as transposed upper
+            // ones and never leave the registers
+            if (mir && (mir[pos] & kMirT)) continue;
             const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
             const float Av[4] = {acc[z][0] + s4.x, acc[z][1] + s4.y, acc[z][2] + s4.z, acc[z][3] + s4.w};
             const int64_t qq = (int64_t)b * sell_nb + pos;
@@ -827,12 +830,13 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
         k_assemble_rows<8><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p,
                                              m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p,
                                              m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p, w.dinv32.p,
-                                             w.rhs.p, bf.A0h, bf.D0h, m->n_own);
+                                             w.rhs.p, bf.A0h, bf.D0h, m->n_own, m->sym_reads && MOF_SKIP_LOWER ? m->sell_mir.p : nullptr);
     else if (precision == MOF_PREC_MIXED && rows_env && W <= 16)
         k_assemble_rows<16><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p,
                                               m->vptr.p, m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p),
                                               m->tslot.p, m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p,
-                                              w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own);
+                                              w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own,
+                                              m->sym_reads && MOF_SKIP_LOWER ? m->sell_mir.p : nullptr);
     else if (precision == MOF_PREC_MIXED)
         k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                             m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,

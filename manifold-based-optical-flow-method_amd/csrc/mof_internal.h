@@ -86,6 +86,11 @@ __host__ __device__ inline int32_t sell_block(int32_t slot, int32_t td) {
 #ifndef MOF_SYM_A
 #define MOF_SYM_A 1
 #endif
+// with symmetric reads, the assembly stores no lower blocks and the level-0
+// Galerkin lists read them as transposed upper ones (0: store everything)
+#ifndef MOF_SKIP_LOWER
+#define MOF_SKIP_LOWER 1
+#endif
 // sell_mirror entries: position | kMirT = read the block transposed
 constexpr int32_t kMirT = 1 << 30;
 constexpr int32_t kMirPos = kMirT - 1;
