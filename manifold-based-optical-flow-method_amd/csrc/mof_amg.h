@@ -79,7 +79,7 @@ struct AmgDevLevel {
     int64_t sell_nb = 0;
     DevArray<int32_t> sell_off, sell_col, sell_row, diag_pos;  // level >= 1
     DevArray<uint8_t> dead;                          // level >= 1
-    DevArray<int32_t> agg, mptr, apos, gptr, gent;  // transition to level + 1
+    DevArray<int32_t> agg, mptr, mlist, apos, gptr, gent;  // transition to level + 1
     DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
     bool smoothed = false;                          // level 0: smoothed prolongator
     DevArray<int32_t> pptr, pcol, rptr, rent;

@@ -470,6 +470,7 @@ struct Lvl {
     const uint16_t *Ah22;                // [B][sell_nb] entry (2,2)
     float *b, *x, *r, *y;                // [B][n][4] (level 0: x [B][n][2], r bf16 [B][n][2])
     const int32_t *agg, *mptr, *apos;    // transition to level + 1
+    const int32_t *mlist;                // aggregate members (level 0: r1 gathered in member order)
     const float *Q, *Qm;                 // tentative rows (node order / member order), or P blocks
     const int32_t *pptr, *pcol;          // smoothed P: row blocks of each fine node
     const int32_t *rptr, *rent;          // smoothed P: {fine node, P block} per coarse node
@@ -509,7 +510,8 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0(int32_t N, int32_t nbl
         float y0, y1;
         spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1);
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-        reinterpret_cast<uint32_t *>(r1)[vb + apos[i]] = bf16_bits(ri.x - y0) | (bf16_bits(ri.y - y1) << 16);
+        reinterpret_cast<uint32_t *>(r1)[vb + (apos ? apos[i] : i)] =
+            bf16_bits(ri.x - y0) | (bf16_bits(ri.y - y1) << 16);
     }
 }
 
@@ -560,6 +562,19 @@ __device__ __forceinline__ void res3_node(const Lvl &L, int32_t b, int32_t i) {
     stv<3>(L.r + vo, L.apos[i], ri);
 }
 
+// MOF_R1_NATURAL = 1 stores level 0's restricted residual r1 in node order
+// (k_res0's stores coalesced instead of scattered into member order: 1053
+// -> 961 us) and lets the restriction gather member q's value at mlist[q]
+// (233 -> 361 us): a net loss, so r1 stays in member order (C3, B = 512).
+#ifndef MOF_R1_NATURAL
+#define MOF_R1_NATURAL 0
+#endif
+template <int BSF>
+__device__ __forceinline__ int32_t r_at(const Lvl &F, int32_t q) {
+    if constexpr (BSF == 2 && MOF_R1_NATURAL) return F.mlist[q];
+    return q;
+}
+
 // b_C[I] = sum over the members of aggregate I of Q^T r (member order,
 // contiguous, U at a time); with smooth also x_C[I] = w D_C^-1 b_C[I].
 template <int BSF>
@@ -571,7 +586,7 @@ __device__ __forceinline__ void restrict_node(const Lvl &F, const Lvl &C, int32_
     for (int32_t t0 = q0; t0 < q1; t0 += U) {
         float ri[U][BSF], qm[U][BSF * 3];
 #pragma unroll
-        for (int u = 0; u < U; ++u) ldr<BSF>(F.r, b, F.n, min(t0 + u, q1 - 1), ri[u]);
+        for (int u = 0; u < U; ++u) ldr<BSF>(F.r, b, F.n, r_at<BSF>(F, min(t0 + u, q1 - 1)), ri[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float *p = F.Qm + (int64_t)min(t0 + u, q1 - 1) * BSF * 3;
@@ -668,7 +683,7 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
     }
     for (int32_t q = q0 + threadIdx.x; q < q1; q += kWG) {
         float ri[BSF];
-        ldr<BSF>(F.r, b, F.n, q, ri);
+        ldr<BSF>(F.r, b, F.n, r_at<BSF>(F, q), ri);
         const float *qm = F.Qm + (int64_t)q * BSF * 3;
         float c3[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -1042,6 +1057,7 @@ bool amg_build(mof_mesh *m) {
         if (l + 1 < H.levels.size()) {
             put_i(D.agg, L.agg);
             put_i(D.mptr, L.mptr);
+            put_i(D.mlist, L.mlist);
             put_i(D.apos, L.apos);
             put_i(D.gptr, L.gptr);
             put_i(D.gent, L.gent);
@@ -1201,6 +1217,7 @@ Lvl level_view(const AmgDevLevel &D) {
     v.y = D.y.p;
     v.agg = D.agg.p;
     v.mptr = D.mptr.p;
+    v.mlist = D.mlist.p;
     v.apos = D.apos.p;
     v.Q = D.Q.p;
     v.Qm = D.Qm.p;
@@ -1230,7 +1247,8 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = 0; l < S; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
-            k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x, v[0].apos, sysi, v[0].r);
+            k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
+                                      MOF_R1_NATURAL || G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
             if (G.lv[0].smoothed) {
                 k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNS - 1) / kNS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
