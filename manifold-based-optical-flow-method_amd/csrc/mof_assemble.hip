@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
         }
 #pragma unroll
         for (int q = 0; q < 6; q += 2) {
-            *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
+            if (u) *reinterpret_cast<double2 *>(u + base + q) = make_double2(uo[q], uo[q + 1]);
             *reinterpret_cast<double2 *>(fc + base + q) = make_double2(fo[q], fo[q + 1]);
             if (u32) *reinterpret_cast<float2 *>(u32 + base + q) = make_float2((float)uo[q], (float)uo[q + 1]);
         }
@@ -809,8 +809,15 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     }
     const double *J0 = w.Iint.p, *J1 = w.Iint.p + (I1 == I0 + ldI ? (int64_t)m->N : (int64_t)m->N * B);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
+    // the mixed path's residual re-forms u from the I rows: no u64 stores
+    const bool skip_u64 = MOF_RES_RECOMPUTE && precision == MOF_PREC_MIXED;
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
-                                  w.u64.p, w.fc.p, precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
+                                  skip_u64 ? nullptr : w.u64.p, w.fc.p,
+                                  precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
+    w.u64_stale = skip_u64;
+    w.J0 = J0;
+    w.J1 = J1;
+    w.JB = B;
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
@@ -861,6 +868,13 @@ void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStr
             m->N, snb, m->diag_pos.p, w.A32.p, w.dinv32.p);
     } else {
         MOF_REQUIRE(w.A64.n >= 4 * (size_t)snb * B, "recovery: fp64 A not allocated");
+        if (w.u64_stale) {  // the batch's u64 was never stored: form it from the same I rows
+            MOF_REQUIRE(w.J0 && w.J1 && w.JB >= B, "recovery: the batch's I rows are gone");
+            k_tri_step<<<dim3((unsigned)((m->M + kWG - 1) / kWG)), kWG, 0, s>>>(
+                m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, w.J0, w.J1, m->N, w.dt.p, w.u64.p, w.fc.p,
+                nullptr);
+            w.u64_stale = false;
+        }
         const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
         k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                                      m->cptr.p, m->clist.p, m->iw.p, m->a2s64.p, w.u64.p, w.fc.p,

@@ -150,7 +150,18 @@ struct Workspace {
     DevArray<double> Ibuf;             // [B][N] I0 rows + [B][N] I1 rows (host-staged)
     DevArray<double> Iint;             // the batch's I rows in internal vertex order ([B+1] or [2B] rows)
     DevArray<double> Vbuf;             // [B][2N] planar output staging
+    // MOF_RES_RECOMPUTE: the mixed path's k_tri_step leaves u64 unwritten
+    // (the fp64 residual re-forms u from the batch's I rows); the fp64
+    // recovery re-runs k_tri_step from the rows below when it needs u64
+    bool u64_stale = false;
+    const double *J0 = nullptr, *J1 = nullptr;  // the batch's I0 / I1 rows (in Iint), row stride N
+    int32_t JB = 0;                              // their systems
 };
+
+// the fp64 residual forms u from the I rows instead of reading u64
+#ifndef MOF_RES_RECOMPUTE
+#define MOF_RES_RECOMPUTE 1
+#endif
 
 // per-system scalar slots (Workspace::sysd / sysi)
 //  SD_RR0 / SD_BEST: |r|^2 at the start of the inner solve / smallest so far

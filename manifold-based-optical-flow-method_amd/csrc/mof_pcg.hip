@@ -64,7 +64,11 @@ struct OpArgs {
     const int32_t *tsell_off;            // vertex -> incident triangles, SELL-64
     const int4 *tinc;                    // {T, corner, vertex of corner+1, vertex of corner+2}
     const V *w12;                        // [M+1] A_T / 12 (slot M = 0)
-    const V *u;                          // [B][M+1][6] u_T per system (slot M = 0)
+    const V *u;                          // [B][M+1][6] u_T per system (slot M = 0), or null:
+    // u re-formed from the timestep's I row as k_tri_step forms it
+    const double *gw, *e;                // [M][9] hat gradients, [N][6] tangent bases
+    const double *I0;                    // [B][ldI] I_k rows (internal order)
+    int64_t ldI;
 };
 
 template <typename V>
@@ -189,6 +193,205 @@ __device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int
     }
     y0 = a0;
     y1 = a1;
+}
+
+// (a1_b x)_i with u re-formed per incident triangle from the system's I row
+// and the mesh geometry, in k_tri_step's exact arithmetic (grad I without
+// contraction, np.dot's fma chain), so r64 keeps its bits while the
+// 15.7 MB/system u64 array is neither written nor gathered three times
+// (once per incident row block); lambda a2 x as apply_row_mf.
+#ifndef MOF_RC_U
+#define MOF_RC_U 2
+#endif
+__device__ __forceinline__ double dot3_np(const double *x, const double *y) {
+    return fma(x[2], y[2], fma(x[1], y[1], __dmul_rn(x[0], y[0])));
+}
+__device__ __forceinline__ void apply_row_rc(const OpArgs<double> &op, int32_t b, int32_t i,
+                                             const double *__restrict__ x, double &y0, double &y1) {
+    constexpr int U = MOF_RC_U;
+    const int32_t s = i >> 6, l = i & 63;
+    double a0 = 0, a1 = 0;
+    {
+        const int32_t o = op.sell_off[s];
+        const int32_t w = (op.sell_off[s + 1] - o) >> 6;
+        for (int32_t t0 = 0; t0 < w; t0 += MOF_RES_U) {
+            int32_t j[MOF_RES_U];
+            double blk[MOF_RES_U][4];
+#pragma unroll
+            for (int u = 0; u < MOF_RES_U; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+            for (int u = 0; u < MOF_RES_U; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
+#pragma unroll
+            for (int u = 0; u < MOF_RES_U; ++u) {
+                const double2 xj = ld2(x + 2 * (int64_t)j[u]);
+                const bool on = t0 + u < w;
+                a0 += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : 0.0;
+                a1 += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : 0.0;
+            }
+        }
+    }
+    {
+        const double *Ib = op.I0 + (int64_t)b * op.ldI;
+        const double2 xi = ld2(x + 2 * (int64_t)i);
+        const double Ii = Ib[i];
+        double ei[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ei[q] = op.e[6 * (int64_t)i + q];
+        const int32_t o = op.tsell_off[s];
+        const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
+        for (int32_t t0 = 0; t0 < w; t0 += U) {
+            int4 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) q[u] = op.tinc[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+            double g[U][9], ej[U][6], ek[U][6], Ij[U], Ik[U], wt[U];
+            double2 xj[U], xk[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t T = min(q[u].x, op.M - 1);  // padding entries (T = M): any triangle, weight 0
+#pragma unroll
+                for (int k = 0; k < 9; ++k) g[u][k] = op.gw[9 * T + k];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    ej[u][k] = op.e[6 * (int64_t)q[u].z + k];
+                    ek[u][k] = op.e[6 * (int64_t)q[u].w + k];
+                }
+                Ij[u] = Ib[q[u].z];
+                Ik[u] = Ib[q[u].w];
+                xj[u] = ld2(x + 2 * (int64_t)q[u].z);
+                xk[u] = ld2(x + 2 * (int64_t)q[u].w);
+                wt[u] = op.w12[q[u].x];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = q[u].y;
+                // the triangle's corner values in its own corner order
+                const double c0 = c == 0 ? Ii : (c == 1 ? Ik[u] : Ij[u]);
+                const double c1 = c == 0 ? Ij[u] : (c == 1 ? Ii : Ik[u]);
+                const double c2 = c == 0 ? Ik[u] : (c == 1 ? Ij[u] : Ii);
+                double gI[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+                    gI[d] = __dadd_rn(__dadd_rn(__dmul_rn(c0, g[u][d]), __dmul_rn(c1, g[u][3 + d])),
+                                      __dmul_rn(c2, g[u][6 + d]));
+                const double2 ui = make_double2(dot3_np(gI, ei), dot3_np(gI, ei + 3));
+                const double2 uj = make_double2(dot3_np(gI, ej[u]), dot3_np(gI, ej[u] + 3));
+                const double2 uk = make_double2(dot3_np(gI, ek[u]), dot3_np(gI, ek[u] + 3));
+                const double si = ui.x * xi.x + ui.y * xi.y;
+                const double sj = uj.x * xj[u].x + uj.y * xj[u].y;
+                const double sk = uk.x * xk[u].x + uk.y * xk[u].y;
+                const double cc = (t0 + u < w) ? wt[u] * ((si + si) + sj + sk) : 0.0;
+                a0 += ui.x * cc;
+                a1 += ui.y * cc;
+            }
+        }
+    }
+    y0 = a0;
+    y1 = a1;
+}
+
+// apply_row_rc for two systems of the batch at once: every incident
+// triangle's geometry and every a2 block is loaded once for both (the
+// re-forming residual is bound by those shared gathers). No fp contraction,
+// so both system slots round alike (a system's bits must not depend on the
+// slot it lands in, i.e. on the batch split).
+__device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t b0, int32_t b1, int32_t i,
+                                              const double *__restrict__ x64, double (&y)[2][2]) {
+#pragma clang fp contract(off)
+    constexpr int U = MOF_RC_U;
+    const int32_t s = i >> 6, l = i & 63;
+    const int64_t vb[2] = {(int64_t)b0 * op.N, (int64_t)b1 * op.N};
+    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    {
+        const int32_t o = op.sell_off[s];
+        const int32_t w = (op.sell_off[s + 1] - o) >> 6;
+        for (int32_t t0 = 0; t0 < w; t0 += MOF_RES_U) {
+            int32_t j[MOF_RES_U];
+            double blk[MOF_RES_U][4];
+#pragma unroll
+            for (int u = 0; u < MOF_RES_U; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+            for (int u = 0; u < MOF_RES_U; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
+#pragma unroll
+            for (int u = 0; u < MOF_RES_U; ++u) {
+                const bool on = t0 + u < w;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const double2 xj = ld2(x64 + 2 * (vb[t] + j[u]));
+                    acc[t][0] += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : 0.0;
+                    acc[t][1] += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : 0.0;
+                }
+            }
+        }
+    }
+    {
+        const double *Ib[2] = {op.I0 + (int64_t)b0 * op.ldI, op.I0 + (int64_t)b1 * op.ldI};
+        double2 xi[2];
+        double Ii[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            xi[t] = ld2(x64 + 2 * (vb[t] + i));
+            Ii[t] = Ib[t][i];
+        }
+        double ei[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ei[q] = op.e[6 * (int64_t)i + q];
+        const int32_t o = op.tsell_off[s];
+        const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
+        for (int32_t t0 = 0; t0 < w; t0 += U) {
+            int4 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) q[u] = op.tinc[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+            double g[U][9], ej[U][6], ek[U][6], Ij[U][2], Ik[U][2], wt[U];
+            double2 xj[U][2], xk[U][2];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t T = min(q[u].x, op.M - 1);  // padding entries (T = M): weight 0
+#pragma unroll
+                for (int k = 0; k < 9; ++k) g[u][k] = op.gw[9 * T + k];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    ej[u][k] = op.e[6 * (int64_t)q[u].z + k];
+                    ek[u][k] = op.e[6 * (int64_t)q[u].w + k];
+                }
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    Ij[u][t] = Ib[t][q[u].z];
+                    Ik[u][t] = Ib[t][q[u].w];
+                    xj[u][t] = ld2(x64 + 2 * (vb[t] + q[u].z));
+                    xk[u][t] = ld2(x64 + 2 * (vb[t] + q[u].w));
+                }
+                wt[u] = op.w12[q[u].x];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = q[u].y;
+                const bool on = t0 + u < w;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const double c0 = c == 0 ? Ii[t] : (c == 1 ? Ik[u][t] : Ij[u][t]);
+                    const double c1 = c == 0 ? Ij[u][t] : (c == 1 ? Ii[t] : Ik[u][t]);
+                    const double c2 = c == 0 ? Ik[u][t] : (c == 1 ? Ij[u][t] : Ii[t]);
+                    double gI[3];
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[u][d] + c1 * g[u][3 + d]) + c2 * g[u][6 + d];
+                    const double2 ui = make_double2(dot3_np(gI, ei), dot3_np(gI, ei + 3));
+                    const double2 uj = make_double2(dot3_np(gI, ej[u]), dot3_np(gI, ej[u] + 3));
+                    const double2 uk = make_double2(dot3_np(gI, ek[u]), dot3_np(gI, ek[u] + 3));
+                    const double si = ui.x * xi[t].x + ui.y * xi[t].y;
+                    const double sj = uj.x * xj[u][t].x + uj.y * xj[u][t].y;
+                    const double sk = uk.x * xk[u][t].x + uk.y * xk[u][t].y;
+                    const double cc = on ? wt[u] * ((si + si) + sj + sk) : 0.0;
+                    acc[t][0] += ui.x * cc;
+                    acc[t][1] += ui.y * cc;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        y[t][0] = acc[t][0];
+        y[t][1] = acc[t][1];
+    }
 }
 
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
@@ -452,6 +655,7 @@ __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
 // partial |r|^2 and |f|^2.
+template <bool RC>
 __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                   const double *__restrict__ rhs,
                                                   const double *__restrict__ x64,
@@ -469,7 +673,10 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         double y0, y1;
-        apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
+        if constexpr (RC)
+            apply_row_rc(op, b, i, x64 + 2 * vb, y0, y1);
+        else
+            apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
         const double r0 = f.x - y0, r1 = f.y - y1;
         *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
@@ -484,6 +691,58 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
         double *o = part + 2 * red_rec(rd, B, b, rb);
         o[0] = v[0];
         o[1] = v[1];
+    }
+}
+
+// The re-forming residual, two systems per thread (apply_row_rc2): grid
+// over (row block, system pair) in the XCD-aware order; per-system partials
+// summed in the same tree as k_residual's.
+#ifndef MOF_RC_PAIR
+#define MOF_RC_PAIR 1
+#endif
+__global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
+                                                      const double *__restrict__ rhs,
+                                                      const double *__restrict__ x64,
+                                                      const int32_t *__restrict__ sysi,
+                                                      double *__restrict__ r64,
+                                                      double *__restrict__ part) {
+    __shared__ double lds[16];
+    int32_t rb, bp;
+    if (!xcd_map(nblk, (B + 1) / 2, rb, bp, kGrpRes)) return;
+    const int32_t b0 = 2 * bp, b1 = min(b0 + 1, B - 1);
+    const bool act[2] = {sysi[b0 * kSysStride + SI_ACTIVE] != 0,
+                         b0 + 1 < B && sysi[b1 * kSysStride + SI_ACTIVE] != 0};
+    if (!act[0] && !act[1]) return;
+    const int32_t N = op.N;
+    const int32_t bs[2] = {b0, b1};
+    double v[4] = {0.0, 0.0, 0.0, 0.0};  // rr, ff of each system
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= N) break;
+        double y[2][2];
+        apply_row_rc2(op, b0, b1, i, x64, y);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int64_t vi = (int64_t)bs[t] * N + i;
+            const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
+            const double r0 = f.x - y[t][0], r1 = f.y - y[t][1];
+            if (act[t]) *reinterpret_cast<double2 *>(r64 + 2 * vi) = make_double2(r0, r1);
+            if (i < rd.nown) {
+                v[2 * t] += r0 * r0 + r1 * r1;
+                v[2 * t + 1] += f.x * f.x + f.y * f.y;
+            }
+        }
+    }
+    block_sum<4>(v, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            if (!act[t]) continue;
+            double *o = part + 2 * red_rec(rd, B, bs[t], rb);
+            o[0] = v[2 * t];
+            o[1] = v[2 * t + 1];
+        }
     }
 }
 
@@ -558,10 +817,27 @@ OpArgs<V> make_op(mof_mesh *m, const V *a2s, const V *w12, const V *u) {
     op.tinc = reinterpret_cast<const int4 *>(m->tinc.p);
     op.w12 = w12;
     op.u = u;
+    op.gw = m->gw.p;
+    op.e = m->e.p;
+    op.I0 = m->ws.J0;
+    op.ldI = m->N;
     return op;
 }
 
-OpArgs<double> op64(mof_mesh *m) { return make_op<double>(m, m->a2s64.p, m->w12_64.p, m->ws.u64.p); }
+// u64 of the batch, or null when the mixed path left it unwritten (the
+// residual then re-forms u from the batch's I rows)
+OpArgs<double> op64(mof_mesh *m) {
+    return make_op<double>(m, m->a2s64.p, m->w12_64.p, m->ws.u64_stale ? nullptr : m->ws.u64.p);
+}
+template <typename... Args>
+void launch_residual(const OpArgs<double> &op, int32_t nblk, int32_t B, hipStream_t s, Args... args) {
+    if (op.u)
+        k_residual<false><<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
+    else if (MOF_RC_PAIR)
+        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
+    else
+        k_residual<true><<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
+}
 
 template <typename V>
 MatArgs<V> make_mat(mof_mesh *m, const V *A) {
@@ -892,7 +1168,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
-        k_residual<<<dim3(xcd_grid(w.nblk, B, kGrpRes)), kWG, 0, s>>>(o64, w.nblk, B, rd, w.rhs.p, w.x64.p, w.sysi.p,
+        launch_residual(o64, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
                                                               w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
@@ -1096,7 +1372,7 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
             mof_mesh *m = d->parts[l];
             Workspace &w = m->ws;
             const RedArgs rd{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
-            k_residual<<<dim3(xcd_grid(w.nblk, B, kGrpRes)), kWG, 0, s>>>(op64(m), w.nblk, B, rd, w.rhs.p, w.x64.p,
+            launch_residual(op64(m), w.nblk, B, s, rd, w.rhs.p, w.x64.p,
                                                                   w.sysi.p, w.r64.p, d->part_rr0.p);
         }
         dd_sync_partials(d, d->part_rr0.p, 2 * (int64_t)B * d->nmax, s);
