@@ -316,7 +316,7 @@ def main():
     # transposes through the shared mirror table); fp64: every block
     nread = info.get("blocks_read", info["nblocks"]) if precision == "mixed" else info["nblocks"]
     shared = info["nblocks"] * 4 * (2 if nread < info["nblocks"] else 1)  # column indices (+ mirror table)
-    per_sys = nread * 4 * sv + N * 2 * sv * 5
+    per_sys = nread * 4 * sv + N * 2 * sv * 7  # z, q, p, x (the deferred x += alpha p)
     nl = max(1, agg["spmv_launches"])
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -336,7 +336,7 @@ def main():
         # context only: the plain layout's bytes (every block read at its own
         # position, no mirror table) over this kernel's full-launch time, i.e.
         # the rate the plain kernel would need to match it
-        plain = B * (info["nblocks"] * 4 * sv + N * 2 * sv * 5) + info["nblocks"] * 4
+        plain = B * (info["nblocks"] * 4 * sv + N * 2 * sv * 7) + info["nblocks"] * 4
         roofline["plain_layout_equiv_frac"] = round(
             plain / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 

@@ -73,7 +73,7 @@ struct mof_dd {
     std::vector<int32_t> part_ids;   // global part id of each local part
     hipStream_t stream = nullptr;
     int32_t cap = 0, nmax = 0;       // systems / workgroups per part the partials hold
-    mof::DevArray<double> part_pq, part_rzrr, part_rr0;  // [P][B][nmax] (x2 slots, x NV)
+    mof::DevArray<double> part_pq, part_rzrr, part_rr0;  // [2][P][B][nmax] (x NV)
     // in-process halo: one entry per ghost row of every part
     // {dst part, dst row, src part, src row}
     mof::DevArray<int4> halo;

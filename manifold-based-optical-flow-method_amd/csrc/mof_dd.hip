@@ -385,7 +385,7 @@ void dd_ensure(mof_dd *d, int32_t B, uint32_t precision) {
         nmax = std::max(nmax, (int32_t)((D.n_loc() + kRowsPerWG - 1) / kRowsPerWG));
     d->nmax = nmax;
     const size_t rec = (size_t)d->P * B * nmax;
-    d->part_pq.alloc(rec);
+    d->part_pq.alloc(2 * rec);  // by iteration parity
     d->part_rzrr.alloc(4 * rec);
     d->part_rr0.alloc(2 * rec);
     if (staged(d)) {

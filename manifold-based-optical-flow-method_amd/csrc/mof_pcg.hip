@@ -77,7 +77,7 @@ struct PcgArgs {
     MatArgs<V> mat;
     const V *dinv;   // [B][N][4]
     V *x, *r, *z, *p, *q;  // [B][N][2]
-    double *part_pq;       // [P][B][nmax] (single domain: P = 1, nmax = nblk)
+    double *part_pq;       // [2][P][B][nmax] by iteration parity (single domain: P = 1, nmax = nblk)
     double *part_rzrr;     // [2][P][B][nmax][2]
     double *sysd;          // [B][8]
     int32_t *sysi;         // [B][8]
@@ -487,12 +487,43 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     const bool force = flags & kForce;
     // retired systems: inactive, or converged in an earlier iteration (the
     // word is sticky, so no later launch re-reads a stale partial slot)
-    if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || a.sysi[b * kSysStride + SI_CONV] >= 0))
-        return;
+    // (a system that converges in this launch still finishes it: the deferred
+    // x update below)
+    const int32_t conv = a.sysi[b * kSysStride + SI_CONV];
+    if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || (conv >= 0 && conv != it))) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;  // slot stride
+    const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;     // p.q slot stride
+    using V2 = typename VT<V>::V2;
+    const int64_t vb = (int64_t)b * a.N;
     double cur[2];
     reduce_sys<2, NT>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
+    // The previous iteration's x += alpha p, deferred to here: this launch
+    // reads p anyway (p = z + beta p), so the update kernel reads neither p
+    // nor x. alpha is the update's own value (same partials, same order).
+    V alpha_prev = 0;
+    double old[2] = {1.0, 1.0};  // the previous iteration's r.z, |r|^2
+    if (!FIRST) {
+        reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
+        if (!force) {
+            double pqp[1];
+            reduce_sys<1, NT>(a.part_pq + ((it + 1) & 1) * pqs, a.red, a.B, b, pqp, lds);
+            alpha_prev = (V)(old[0] / pqp[0]);
+        }
+    }
     if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
+        if (!FIRST) {
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
+                if (i >= a.N) break;
+                const int64_t vi = vb + i;
+                const V2 p0 = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
+                V2 xi = *reinterpret_cast<const V2 *>(a.x + 2 * vi);
+                xi.x += alpha_prev * p0.x;
+                xi.y += alpha_prev * p0.y;
+                *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
+            }
+        }
         if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
             a.sysi[b * kSysStride + SI_CONV] = it;
         return;
@@ -504,13 +535,7 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
         a.sysi[b * kSysStride + SI_BEST_IT] = it;
     }
     V beta = 0;
-    if (!FIRST) {
-        double old[2];
-        reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
-        beta = (V)(cur[0] / old[0]);
-    }
-    using V2 = typename VT<V>::V2;
-    const int64_t vb = (int64_t)b * a.N;
+    if (!FIRST) beta = (V)(cur[0] / old[0]);
     double pq = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
@@ -529,6 +554,12 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
             const V2 p0 = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
             qi = V2{y0 + beta * q0.x, y1 + beta * q0.y};
             pi = V2{zi.x + beta * p0.x, zi.y + beta * p0.y};
+            if (!force) {
+                V2 xi = *reinterpret_cast<const V2 *>(a.x + 2 * vi);
+                xi.x += alpha_prev * p0.x;
+                xi.y += alpha_prev * p0.y;
+                *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
+            }
         }
         *reinterpret_cast<V2 *>(a.q + 2 * vi) = qi;
         *reinterpret_cast<V2 *>(a.p + 2 * vi) = pi;
@@ -536,7 +567,7 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     }
     double v[1] = {pq};
     block_sum<1, NT>(v, lds);
-    if (threadIdx.x == 0) a.part_pq[red_rec(a.red, a.B, b, rb)] = v[0];
+    if (threadIdx.x == 0) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, b, rb)] = v[0];
 }
 
 // the fp32 instances run at >= 5 waves per SIMD (MOF_ROW_OCC: +1 % at C3);
@@ -570,7 +601,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
     if (cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) return;
     double pqv[1];
-    reduce_sys<1>(a.part_pq, a.red, a.B, b, pqv, lds);
+    reduce_sys<1>(a.part_pq + (it & 1) * ((int64_t)a.red.P * a.B * a.red.nmax), a.red, a.B, b, pqv, lds);
     // Every workgroup of the system reduces the same partials, so all take
     // the same decision: breakdown (p.q <= 0 or r.z <= 0: A or the
     // preconditioner is not SPD, e.g. an indefinite V-cycle; non-finite
@@ -600,15 +631,11 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
         const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= a.N) break;
         const int64_t vi = (int64_t)b * a.N + i;
-        const V2 pi = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
+        // x += alpha p happens in the next SpMV launch (it reads p anyway)
         const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
-        V2 xi = *reinterpret_cast<const V2 *>(a.x + 2 * vi);
         V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
-        xi.x += alpha * pi.x;
-        xi.y += alpha * pi.y;
         ri.x = i < a.red.nown ? ri.x - alpha * qi.x : (V)0;
         ri.y = i < a.red.nown ? ri.y - alpha * qi.y : (V)0;
-        *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
         *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
         if (!a.ext) {
             V d[4];
@@ -1046,12 +1073,13 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
     // per system: the 2x2 block values (fp32: the diagonal and upper blocks,
     // read once each with the symmetric reads), z gathered once, q and p read
-    // and written; shared by all systems of the launch: the column indices
+    // and written, x read and written (the previous iteration's deferred
+    // x += alpha p); shared by all systems of the launch: the column indices
     // (and the mirror table).
     const bool f32 = precision == MOF_PREC_MIXED;
     const double N = m->N, nb = m->pat.nblocks(), nr = f32 ? (double)m->blocks_read : nb;
     const double sv = f32 ? 4.0 : 8.0;
-    return active * (nr * 4 * sv + N * 2 * sv * 5) + nb * 4.0 * (f32 && m->sym_reads ? 2 : 1);
+    return active * (nr * 4 * sv + N * 2 * sv * 7) + nb * 4.0 * (f32 && m->sym_reads ? 2 : 1);
 }
 
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
@@ -1092,7 +1120,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.vz.alloc(2 * N * B);
     w.vp.alloc(2 * N * B);
     w.vq.alloc(2 * N * B);
-    w.part_pq.alloc((size_t)w.nblk * B);
+    w.part_pq.alloc(2 * (size_t)w.nblk * B);  // by iteration parity
     w.part_rzrr.alloc((size_t)4 * w.nblk * B);
     w.part_rr0.alloc((size_t)2 * w.nblk * B);
     w.sysd.alloc((size_t)kSysStride * B);
@@ -1280,7 +1308,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
             else
                 k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(args[l], it_, 0);
         }
-        dd_sync_partials(d, d->part_pq.p, rec, s);
+        dd_sync_partials(d, d->part_pq.p + (it_ & 1) * (int64_t)d->P * rec, rec, s);  // this parity's slot
     };
     while (!done && it < max_iter) {
         const int32_t n = std::min(chunk, max_iter - it);
