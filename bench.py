@@ -307,38 +307,48 @@ def main():
         rank_ranges = [[k_off, k_off + K_rank, agg["systems"]]]
 
     # roofline of the dominant kernel (k_pcg_spmv), live over the timed region:
-    # every timed launch is charged with the systems it processed
+    # every timed launch is charged with the systems it processed, in
+    # SURVEY.md 8(d)'s algorithmic bytes of a batched CSR SpMV
+    #   B nnz s_v + 4 nnz + 4 (R + 1) + B R (s_x + s_y)   (nnz = 4 nblocks, R = 2N)
     achieved = agg["spmv_bytes"] / (agg["ms_spmv"] * 1e-3) / 1e9 if agg["ms_spmv"] > 0 else 0.0
     kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
     traffic, traffic_src = pmc_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), kname)
     sv = 4 if precision == "mixed" else 8
-    # fp32 operator: diagonal + upper blocks (the lower ones are read as their
-    # transposes through the shared mirror table); fp64: every block
-    nread = info.get("blocks_read", info["nblocks"]) if precision == "mixed" else info["nblocks"]
-    shared = info["nblocks"] * 4 * (2 if nread < info["nblocks"] else 1)  # column indices (+ mirror table)
-    per_sys = nread * 4 * sv + N * 2 * sv * 7  # z, q, p, x (the deferred x += alpha p)
+    nnz, R = 4 * info["nblocks"], 2 * N
+    per_sys = nnz * sv + R * 2 * sv
+    shared = 4 * nnz + 4 * (R + 1)
     nl = max(1, agg["spmv_launches"])
+    nfull = max(1, agg["spmv_full_launches"])
+    t_full = agg["ms_spmv_full"] / nfull * 1e-3 if agg["ms_spmv_full"] > 0 else 0.0
+    # launches that did work (the shared bytes are charged once each)
+    n_work = round((agg["spmv_bytes"] - agg["spmv_systems"] * per_sys) / shared) if agg["spmv_bytes"] else 0
+    # the kernel's own traffic: the fp32 operator's diagonal + upper blocks
+    # (lower ones read as transposes through the shared mirror table), z
+    # gathered, q, p and x read and written; shared column indices (+ mirror)
+    nread = info.get("blocks_read", info["nblocks"]) if precision == "mixed" else info["nblocks"]
+    k_sys = nread * 4 * sv + N * 2 * sv * 7
+    k_shared = info["nblocks"] * 4 * (2 if nread < info["nblocks"] else 1)
+    k_bytes = agg["spmv_systems"] * k_sys + n_work * k_shared
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": traffic_src, "kernel": kname,
+                "bytes_formula": "SURVEY.md 8(d): B*nnz*s_v + 4*nnz + 4*(R+1) + B*R*(s_x+s_y)",
                 "bytes_per_launch": round(agg["spmv_bytes"] / nl),
                 "bytes_per_system": per_sys, "shared_bytes_per_launch": shared,
                 "systems_per_launch": round(agg["spmv_systems"] / nl, 2),
                 "us_per_launch": round(1e3 * agg["ms_spmv"] / nl, 2),
                 "launches": agg["spmv_launches"],
                 "full_launches": agg["spmv_full_launches"],
-                "us_per_full_launch": round(1e3 * agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]), 2),
-                "full_launch_frac": round((B * per_sys + shared)
-                                          / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3)
-                                          / 1e9 / HBM_PEAK_GBS, 4) if agg["ms_spmv_full"] > 0 else None,
-                "symmetric_reads": nread < info["nblocks"]}
-    if nread < info["nblocks"] and agg["ms_spmv_full"] > 0:
-        # context only: the plain layout's bytes (every block read at its own
-        # position, no mirror table) over this kernel's full-launch time, i.e.
-        # the rate the plain kernel would need to match it
-        plain = B * (info["nblocks"] * 4 * sv + N * 2 * sv * 7) + info["nblocks"] * 4
-        roofline["plain_layout_equiv_frac"] = round(
-            plain / (agg["ms_spmv_full"] / max(1, agg["spmv_full_launches"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                "us_per_full_launch": round(1e6 * t_full, 2),
+                "full_launch_frac": round((B * per_sys + shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
+                if t_full > 0 else None,
+                "symmetric_reads": nread < info["nblocks"],
+                # context: what this fused kernel itself must move
+                "kernel_bytes_per_system": k_sys, "kernel_shared_bytes_per_launch": k_shared,
+                "kernel_frac": round(k_bytes / (agg["ms_spmv"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                if agg["ms_spmv"] > 0 else None,
+                "kernel_full_launch_frac": round((B * k_sys + k_shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
+                if t_full > 0 else None}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and not dry:

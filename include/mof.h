@@ -109,8 +109,10 @@ typedef struct mof_stats {
     int64_t spmv_launches;    /* MOF_TIME_SPMV: PCG SpMV launches timed */
     double ms_spmv;           /* MOF_TIME_SPMV: summed SpMV launch time */
     double spmv_bytes;        /* MOF_TIME_SPMV: summed algorithmic bytes of
-                                 those launches, each charged with the systems
-                                 it processed */
+                                 those launches (the batched CSR
+                                 SpMV, B nnz s_v + 4 nnz + 4 (R+1) + B R (s_x+s_y)),
+                                 each charged with the systems it processed
+                                  */
     int64_t spmv_systems;     /* MOF_TIME_SPMV: systems processed, summed over
                                  the timed launches (a system that converged
                                  earlier in a chunk exits at once) */

@@ -1071,15 +1071,16 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
 }  // namespace
 
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
-    // per system: the 2x2 block values (fp32: the diagonal and upper blocks,
-    // read once each with the symmetric reads), z gathered once, q and p read
-    // and written, x read and written (the previous iteration's deferred
-    // x += alpha p); shared by all systems of the launch: the column indices
-    // (and the mirror table).
-    const bool f32 = precision == MOF_PREC_MIXED;
-    const double N = m->N, nb = m->pat.nblocks(), nr = f32 ? (double)m->blocks_read : nb;
-    const double sv = f32 ? 4.0 : 8.0;
-    return active * (nr * 4 * sv + N * 2 * sv * 7) + nb * 4.0 * (f32 && m->sym_reads ? 2 : 1);
+    // SURVEY.md 8(d)'s algorithmic bytes of a batched CSR SpMV: per system the
+    // nnz values, one read of x and one write of y (R = 2N rows); shared by
+    // the launch: the nnz column indices and the R + 1 row pointers,
+    //   B nnz s_v + 4 nnz + 4 (R + 1) + B R (s_x + s_y),  nnz = 4 nblocks.
+    // (The kernel's own traffic differs both ways: it reads only the diagonal
+    // and upper blocks with the symmetric reads, and it also updates q, p and
+    // x; bench.py reports that figure next to this one.)
+    const double nnz = 4.0 * m->pat.nblocks(), R = 2.0 * m->N;
+    const double sv = precision == MOF_PREC_MIXED ? 4.0 : 8.0;
+    return active * (nnz * sv + R * 2 * sv) + 4.0 * nnz + 4.0 * (R + 1);
 }
 
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {

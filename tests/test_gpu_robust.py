@@ -108,8 +108,10 @@ def test_spmv_accounting_systems_equal_iterations(precision, precond, sym, monke
     nread = info["blocks_read"] if precision == "mixed" else info["nblocks"]
     if precision == "mixed":
         assert nread == ((info["nblocks"] + N) // 2 if sym == "1" else info["nblocks"])
-    per_sys = nread * 4 * sv + N * 2 * sv * 7
-    shared = info["nblocks"] * 4 * (2 if precision == "mixed" and sym == "1" else 1)
+    # charged in SURVEY.md 8(d)'s batched CSR SpMV bytes
+    nnz, R = 4 * info["nblocks"], 2 * N
+    per_sys = nnz * sv + R * 2 * sv
+    shared = 4 * nnz + 4 * (R + 1)
     lo = st["spmv_systems"] * per_sys
     assert lo <= st["spmv_bytes"] <= lo + st["spmv_launches"] * shared
 
