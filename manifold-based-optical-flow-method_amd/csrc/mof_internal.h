@@ -144,6 +144,7 @@ struct Workspace {
     DevArray<double> part_pq;          // [B][nblk]
     DevArray<double> part_rzrr;        // [2][B][nblk][2]
     DevArray<double> part_rr0;         // [B][nblk][2]
+    DevArray<double> sc;               // pre-reduced PCG scalars: r.z, |r|^2 [2][B][2], p.q [2][B]
     DevArray<double> sysd;             // [B][8] per-system scalars
     DevArray<int32_t> sysi;            // [B][8] per-system flags
     DevArray<double> dt;               // [B]

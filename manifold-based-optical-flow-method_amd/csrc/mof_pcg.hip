@@ -90,7 +90,19 @@ struct PcgArgs {
     const int32_t *dA_off;
     RedArgs red;           // partial-record layout; rows >= red.nown (ghosts) are not summed
     int32_t stall;         // stagnation window in iterations (0: off)
+    double *sc;            // pre-reduced scalars (k_red_rzrr / k_red_pq), by iteration parity
 };
+
+// The per-system scalars every workgroup of the next launch needs, reduced
+// once by one workgroup per system (the same order as reduce_sys, so the
+// same bits) instead of by every workgroup from the partial records: r.z and
+// |r|^2 at sc[(slot B + b) 2 + k], p.q at sc[4 B + slot B + b].
+__device__ __forceinline__ double *sc_rzrr(double *sc, int32_t B, int32_t slot, int32_t b) {
+    return sc + 2 * ((int64_t)slot * B + b);
+}
+__device__ __forceinline__ double *sc_pq(double *sc, int32_t B, int32_t slot, int32_t b) {
+    return sc + 4 * (int64_t)B + (int64_t)slot * B + b;
+}
 
 // |r|^2 growth over the start of the inner solve taken as divergence (CG's
 // residual is not monotone, but 1e5 in norm is far past any transient)
@@ -437,6 +449,37 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
     }
 }
 
+// MOF_PRS: the scalars of the PCG recurrences are reduced once per system
+// (k_red_rzrr after the update / V-cycle, k_red_pq after the SpMV) and the
+// row kernels read two doubles instead of re-reducing every workgroup's
+// partial record -- which is what lets the row kernels use small
+// workgroups (MOF_KROWS).
+#ifndef MOF_PRS
+#define MOF_PRS 1
+#endif
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.x;
+    const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
+    double v[2];
+    reduce_sys<2>(a.part_rzrr + slot * ps, a.red, a.B, b, v, lds);
+    if (threadIdx.x == 0) {
+        double *o = sc_rzrr(a.sc, a.B, slot, b);
+        o[0] = v[0];
+        o[1] = v[1];
+    }
+}
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
+    __shared__ double lds[8];
+    const int32_t b = blockIdx.x;
+    const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;
+    double v[1];
+    reduce_sys<1>(a.part_pq + slot * pqs, a.red, a.B, b, v, lds);
+    if (threadIdx.x == 0) *sc_pq(a.sc, a.B, slot, b) = v[0];
+}
+
 // One workgroup per system: tolerance from |rhs|^2, reset the convergence word.
 // outer_rtol > 0 (refinement steps after the first): each system's inner
 // tolerance is what its own outer residual still needs, 0.3 rtol |f| / |r64|,
@@ -473,7 +516,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, doub
 // row block at once, so the neighbouring row blocks of a system run in step
 // and the transposed reads of the symmetric layout meet their lines in L2)
 #ifndef MOF_SPMV_ROWS
-#define MOF_SPMV_ROWS 4
+#define MOF_SPMV_ROWS MOF_KROWS
 #endif
 constexpr int kSpmvRows = MOF_SPMV_ROWS;
 constexpr int kSpmvWG = kRowsPerWG / kSpmvRows;
@@ -496,17 +539,32 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     using V2 = typename VT<V>::V2;
     const int64_t vb = (int64_t)b * a.N;
     double cur[2];
-    reduce_sys<2, NT>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
+    if (MOF_PRS) {
+        const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
+        cur[0] = c[0];
+        cur[1] = c[1];
+    } else {
+        reduce_sys<2, NT>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
+    }
     // The previous iteration's x += alpha p, deferred to here: this launch
     // reads p anyway (p = z + beta p), so the update kernel reads neither p
     // nor x. alpha is the update's own value (same partials, same order).
     V alpha_prev = 0;
     double old[2] = {1.0, 1.0};  // the previous iteration's r.z, |r|^2
     if (!FIRST) {
-        reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
+        if (MOF_PRS) {
+            const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
+            old[0] = o[0];
+            old[1] = o[1];
+        } else {
+            reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
+        }
         if (!force) {
             double pqp[1];
-            reduce_sys<1, NT>(a.part_pq + ((it + 1) & 1) * pqs, a.red, a.B, b, pqp, lds);
+            if (MOF_PRS)
+                pqp[0] = *sc_pq(a.sc, a.B, (it + 1) & 1, b);
+            else
+                reduce_sys<1, NT>(a.part_pq + ((it + 1) & 1) * pqs, a.red, a.B, b, pqp, lds);
             alpha_prev = (V)(old[0] / pqp[0]);
         }
     }
@@ -590,6 +648,9 @@ __global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, false>(
 template <typename V>
 constexpr int spmv_wg() { return sizeof(V) == 4 ? kSpmvWG : kWG; }
 
+constexpr int kUpdRB = kRows >= 4 ? 1 : 4 / kRows;  // row blocks per update workgroup
+inline unsigned upd_blocks(int32_t nblk) { return (unsigned)((nblk + kUpdRB - 1) / kUpdRB); }
+
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     __shared__ double lds[8];
@@ -597,11 +658,17 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
-    double cur[2];
-    reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
+    double cur[2], pqv[1];
+    if (MOF_PRS) {
+        const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
+        cur[0] = c[0];
+        cur[1] = c[1];
+        pqv[0] = *sc_pq(a.sc, a.B, it & 1, b);
+    } else {
+        reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
+        reduce_sys<1>(a.part_pq + (it & 1) * ((int64_t)a.red.P * a.B * a.red.nmax), a.red, a.B, b, pqv, lds);
+    }
     if (cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) return;
-    double pqv[1];
-    reduce_sys<1>(a.part_pq + (it & 1) * ((int64_t)a.red.P * a.B * a.red.nmax), a.red, a.B, b, pqv, lds);
     // Every workgroup of the system reduces the same partials, so all take
     // the same decision: breakdown (p.q <= 0 or r.z <= 0: A or the
     // preconditioner is not SPD, e.g. an indefinite V-cycle; non-finite
@@ -625,39 +692,46 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     }
     const V alpha = (V)(cur[0] / pqv[0]);
     using V2 = typename VT<V>::V2;
-    double rz = 0.0, rr = 0.0;
+    // kUpdRB row blocks per workgroup (one partial record each): the update
+    // has no gathers, so 1024 rows per workgroup amortise its fixed costs
+    // whatever the row kernels' block size
+    for (int32_t q = 0; q < kUpdRB; ++q) {
+        const int32_t rbk = blockIdx.x * kUpdRB + q;
+        if (rbk >= a.nblk) break;
+        double rz = 0.0, rr = 0.0;
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
-        if (i >= a.N) break;
-        const int64_t vi = (int64_t)b * a.N + i;
-        // x += alpha p happens in the next SpMV launch (it reads p anyway)
-        const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
-        V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
-        ri.x = i < a.red.nown ? ri.x - alpha * qi.x : (V)0;
-        ri.y = i < a.red.nown ? ri.y - alpha * qi.y : (V)0;
-        *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
-        if (!a.ext) {
-            V d[4];
-            ld_blk(a.dinv, vi, d);
-            const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
-            *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
-            if (i < a.red.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
-        } else if constexpr (sizeof(V) == 4) {
-            // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
-            const float2 d = MOF_DINV_FROM_A
-                                 ? bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), ri.x, ri.y)
-                                 : bf16_mat2(a.dh[vi], ri.x, ri.y);
-            st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
+        for (int r = 0; r < kRows; ++r) {
+            const int32_t i = rbk * kRowsPerWG + r * kWG + threadIdx.x;
+            if (i >= a.N) break;
+            const int64_t vi = (int64_t)b * a.N + i;
+            // x += alpha p happens in the next SpMV launch (it reads p anyway)
+            const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
+            V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
+            ri.x = i < a.red.nown ? ri.x - alpha * qi.x : (V)0;
+            ri.y = i < a.red.nown ? ri.y - alpha * qi.y : (V)0;
+            *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
+            if (!a.ext) {
+                V d[4];
+                ld_blk(a.dinv, vi, d);
+                const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
+                *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
+                if (i < a.red.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
+            } else if constexpr (sizeof(V) == 4) {
+                // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
+                const float2 d = MOF_DINV_FROM_A
+                                     ? bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), ri.x, ri.y)
+                                     : bf16_mat2(a.dh[vi], ri.x, ri.y);
+                st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
+            }
+            if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
         }
-        if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
-    }
-    double v[2] = {rz, rr};
-    block_sum<2>(v, lds);
-    if (threadIdx.x == 0) {
-        double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * red_rec(a.red, a.B, blockIdx.y, blockIdx.x);
-        o[0] = v[0];
-        o[1] = v[1];
+        double v[2] = {rz, rr};
+        block_sum<2>(v, lds);
+        if (threadIdx.x == 0) {
+            double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * red_rec(a.red, a.B, blockIdx.y, rbk);
+            o[0] = v[0];
+            o[1] = v[1];
+        }
     }
 }
 
@@ -904,6 +978,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.dA_nb = 0;
     a.dA_off = nullptr;
     a.stall = 0;
+    a.sc = w.sc.p;
     return a;
 }
 
@@ -981,6 +1056,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol);
     if (amg) precond(0);
+    if (MOF_PRS) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, 0);
     MOF_HIP(hipGetLastError());
     // systems active at the start of this solve: the host mirror is current
     // (reset by solve_batch, refreshed by every outer check)
@@ -1024,8 +1100,10 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             } else {
                 k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
             }
-            k_pcg_update<V><<<g, kWG, 0, s>>>(a, it);
+            if (MOF_PRS) k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it & 1);
+            k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), (unsigned)B), kWG, 0, s>>>(a, it);
             if (amg) precond((it + 1) & 1);
+            if (MOF_PRS) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, (it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -1123,6 +1201,8 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.vq.alloc(2 * N * B);
     w.part_pq.alloc(2 * (size_t)w.nblk * B);  // by iteration parity
     w.part_rzrr.alloc((size_t)4 * w.nblk * B);
+    w.sc.alloc((size_t)6 * B);
+    w.sc.zero(m->stream);
     w.part_rr0.alloc((size_t)2 * w.nblk * B);
     w.sysd.alloc((size_t)kSysStride * B);
     w.sysi.alloc((size_t)kSysStride * B);
@@ -1283,6 +1363,8 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
                                d->parts[l]->ws.nblk, args[l].red, s);
         }
         dd_sync_partials(d, d->part_rzrr.p + slot * ps, 2 * rec, s);
+        if (MOF_PRS)
+            for (size_t l = 0; l < L; ++l) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], slot);
     };
     for (size_t l = 0; l < L; ++l) {
         Workspace &w = d->parts[l]->ws;
@@ -1293,7 +1375,10 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
     // the tolerance step resets the convergence word the cycle's kernels
     // check, so it runs before the first cycle
     for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol, 0.0);
-    if (amg) precond(0);
+    if (amg)
+        precond(0);
+    else if (MOF_PRS)
+        for (size_t l = 0; l < L; ++l) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], 0);
     MOF_HIP(hipGetLastError());
     std::vector<int32_t> was_active(B);
     for (int32_t b = 0; b < B; ++b) was_active[b] = m0->h_sysi[b * kSysStride + SI_ACTIVE];
@@ -1310,13 +1395,15 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
                 k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(args[l], it_, 0);
         }
         dd_sync_partials(d, d->part_pq.p + (it_ & 1) * (int64_t)d->P * rec, rec, s);  // this parity's slot
+        if (MOF_PRS)
+            for (size_t l = 0; l < L; ++l) k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], it_ & 1);
     };
     while (!done && it < max_iter) {
         const int32_t n = std::min(chunk, max_iter - it);
         for (int32_t c = 0; c < n; ++c, ++it) {
             spmv(it == 0, it);
             for (size_t l = 0; l < L; ++l)
-                k_pcg_update<V><<<dim3((unsigned)d->parts[l]->ws.nblk, (unsigned)B), kWG, 0, s>>>(args[l], it);
+                k_pcg_update<V><<<dim3(upd_blocks(d->parts[l]->ws.nblk), (unsigned)B), kWG, 0, s>>>(args[l], it);
             precond((it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());

@@ -22,10 +22,17 @@ struct VT<double> {
 
 // Row kernels: a workgroup covers kRows groups of 256 consecutive vertex rows
 // (thread t takes rows base + 256 r + t, so every group stays 4 whole SELL
-// slices and every access stays coalesced). Fewer, larger workgroups keep the
-// per-workgroup partial sums short: each workgroup of the next launch re-reads
-// all nblk partials of its system, nblk = ceil(N / (256 kRows)).
-constexpr int kRows = 4;
+// slices and every access stays coalesced); nblk = ceil(N / (256 kRows))
+// partial records per system, reduced once per system into the PCG scalars
+// (MOF_PRS). kRows = 1: a workgroup lives one 256-row group long, so the
+// workgroups of neighbouring row blocks run side by side and the symmetric
+// layout's transposed reads find their lines in L2 (C3 SpMV fetch 11.9 ->
+// 8.9 GB per launch); 4 was the shape while every workgroup re-reduced the
+// previous launch's partials itself.
+#ifndef MOF_KROWS
+#define MOF_KROWS 1
+#endif
+constexpr int kRows = MOF_KROWS;
 constexpr int kRowsPerWG = kWG * kRows;
 
 __device__ __forceinline__ void ld_blk(const float *A, int64_t pos, float (&a)[4]) {
