@@ -614,8 +614,9 @@ __device__ __forceinline__ void restrict_node(const Lvl &F, const Lvl &C, int32_
     }
 }
 
-// x_i += Q_i y_C[agg(i)]
-template <int BSF>
+// x_i += Q_i y_C[agg(i)]; level 0's corrected iterate in the x0 format in
+// place (XM = 1) or as float2 in F.y (XM = 2), see AmgDevice::xm
+template <int BSF, int XM = 2>
 __device__ __forceinline__ void prolong_node(const Lvl &F, const Lvl &C, int32_t b, int32_t i) {
     float y[3], xi[BSF];
     ldv<3>(C.y + (int64_t)b * C.n * 4, F.agg[i], y);
@@ -630,7 +631,7 @@ __device__ __forceinline__ void prolong_node(const Lvl &F, const Lvl &C, int32_t
     const float *qi = F.Q + (int64_t)i * BSF * 3;
 #pragma unroll
     for (int k = 0; k < BSF; ++k) xi[k] += qi[3 * k] * y[0] + qi[3 * k + 1] * y[1] + qi[3 * k + 2] * y[2];
-    if constexpr (BSF == 2 && MOF_X0_BF16 == 2)  // full-precision x for the post-smoothing
+    if constexpr (BSF == 2 && XM == 2)  // full-precision x for the post-smoothing
         reinterpret_cast<float2 *>(F.y)[(int64_t)b * F.n + i] = make_float2(xi[0], xi[1]);
     else if constexpr (BSF == 2)
         st_x0(F.x, (int64_t)b * F.n + i, xi[0], xi[1]);
@@ -799,6 +800,7 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
 
 // Level 0 with a smoothed prolongator: x_i = x0_i + sum_k P_ik y_C[pcol k],
 // kNS systems per thread (the row's P blocks and columns loaded once)
+template <int XM>
 __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk, int32_t B,
                                                      const int32_t *__restrict__ sysi) {
     // no fp contraction: every system slot of the unrolled loops rounds alike
@@ -837,7 +839,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     for (int t = 0; t < kNS; ++t) {
         const int32_t b = b0 + t;
         if (b >= B || retired(sysi, b)) continue;
-        if constexpr (MOF_X0_BF16 == 2)  // full-precision x for the post-smoothing
+        if constexpr (XM == 2)  // full-precision x for the post-smoothing
             reinterpret_cast<float2 *>(F.y)[(int64_t)b * F.n + i] = make_float2(x[t][0], x[t][1]);
         else
             st_x0(F.x, (int64_t)b * F.n + i, x[t][0], x[t][1]);
@@ -855,13 +857,14 @@ __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__
 // node block run back to back on one XCD and share its Q rows in L2 instead
 // of re-reading Q per system (183 vs 261 us per 256-system launch with the
 // system-major grid; the coarse levels' kernels measured slower this way).
+template <int XM>
 __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, int32_t B,
                                                   const int32_t *__restrict__ sysi) {
     int32_t rb, b;
     if (!xcd_map(nblk, B, rb, b, kGrpProl) || retired(sysi, b)) return;
     const int32_t i = rb * kWG + threadIdx.x;
     if (i >= F.n) return;
-    prolong_node<2>(F, C, b, i);
+    prolong_node<2, XM>(F, C, b, i);
 }
 
 __global__ __launch_bounds__(kWG) void k_post3(Lvl L, float omega, const int32_t *__restrict__ sysi) {
@@ -939,6 +942,7 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 
 // Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
 // of the row block's record). PCG row layout, XCD-aware grid.
+template <int XM>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                const uint2 *__restrict__ Dh,
                                                const float *__restrict__ rv,
@@ -958,7 +962,7 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nb
         float y0, y1;
         float2 xi;
         uint2 dg;  // the row's diagonal block (slot 0), kept from the SpMV
-        if constexpr (MOF_X0_BF16 == 2) {
+        if constexpr (XM == 2) {
             spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1, &dg);
             xi = reinterpret_cast<const float2 *>(xv)[vb + i];
         } else {
@@ -1025,10 +1029,18 @@ bool amg_build(mof_mesh *m) {
     build_amg(m->pat, e.data(), prm, H);
     G.omega = prm.omega;
     G.omega1 = prm.omega1;
+    // level 0's corrected iterate x0 + Q y: bf16 in place on meshes with the
+    // tentative prolongator (C3 +3.8 %, C2 mixed +3.3 %, same iterations),
+    // fp32 with the smoothed one (R3: bf16 costs 54.5 vs 50 its, -5 %);
+    // MOF_X_BF16=0/1 forces either
+    G.xm = 2;
     G.lv.clear();
     G.built = true;
     // a mesh that does not coarsen (<= 42 vertices) keeps block Jacobi
     if (H.levels.size() < 2) return false;
+    G.xm = H.levels[0].smoothed ? 2 : 1;
+    if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
+    if (MOF_X0_BF16 == 0) G.xm = 1;  // all-fp32 build: x0 and x in place, both float2
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
@@ -1105,7 +1117,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
         const size_t n = D.n;
         if (l == 0) {
             D.x.alloc(2 * n * B);
-            if (MOF_X0_BF16 == 2) D.y.alloc(2 * n * B);
+            if (G.xm == 2) D.y.alloc(2 * n * B);
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
             G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
             G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
@@ -1274,13 +1286,21 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = S - 1; l >= 0; --l) {
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
-            if (G.lv[0].smoothed)
-                k_prolong0_sa<<<dim3(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B,
-                                                                                             sysi);
-            else
-                k_prolong0<<<dim3(xcd_grid(nb0, B, kGrpProl)), kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
-            k_post0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, reinterpret_cast<const uint2 *>(G.D0h.p), r0,
-                                       MOF_X0_BF16 == 2 ? v[0].y : v[0].x, om, sysi, z0, part_slot, rd);
+            const dim3 gsa(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), gp(xcd_grid(nb0, B, kGrpProl));
+            const uint2 *D0h = reinterpret_cast<const uint2 *>(G.D0h.p);
+            if (G.xm == 2) {
+                if (G.lv[0].smoothed)
+                    k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+                else
+                    k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+                k_post0<2><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot, rd);
+            } else {
+                if (G.lv[0].smoothed)
+                    k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+                else
+                    k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+                k_post0<1><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot, rd);
+            }
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
             k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om1, sysi);

@@ -340,8 +340,9 @@ __device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i,
 // The V-cycle's level-0 iterate: the pre-smoothed x0 = w D^-1 r (written by
 // the PCG update, gathered by k_res0, read by the prolongation) and the
 // corrected x = x0 + Q y (written by the prolongation, gathered by k_post0).
-// MOF_X0_BF16 = 0: both float2 in one buffer; 1: both bf16 pairs (4 B);
-// 2 (default): x0 as a bf16 pair, x as float2 in level 0's y buffer.
+// MOF_X0_BF16 >= 1 (default): x0 as a bf16 pair (4 B); 0: float2. The
+// corrected x is chosen per mesh (AmgDevice::xm): in the x0 format in place,
+// or float2 in level 0's y buffer. Round-1 build-time comparison:
 // PCG its/timestep and timesteps/s, C3 / R3 / C2 mixed: mode 0 18 / 101.9 /
 // 22.8 at 2357 / 374 / 9474; mode 1 18 / 115.8 / 22.8 at 2472 / 345 / 9943;
 // mode 2 18 / 103 / 22.8 at 2428 / 376 / 9676 (same box).
