@@ -942,7 +942,7 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 
 // Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
 // of the row block's record). PCG row layout, XCD-aware grid.
-template <int XM>
+template <int XM, bool ZH>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                const uint2 *__restrict__ Dh,
                                                const float *__restrict__ rv,
@@ -972,9 +972,16 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nb
         const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
         const float2 ds = MOF_DINV_FROM_A ? bf16_diag_solve(dg, ri.x - y0, ri.y - y1)
                                           : bf16_mat2(Dh[vb + i], ri.x - y0, ri.y - y1);
-        const float z0 = xi.x + omega * ds.x;
-        const float z1 = xi.y + omega * ds.y;
-        reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
+        float z0 = xi.x + omega * ds.x;
+        float z1 = xi.y + omega * ds.y;
+        if constexpr (ZH) {  // bf16 z: r.z of the rounded values the PCG uses
+            const uint32_t h = bf16_bits(z0) | (bf16_bits(z1) << 16);
+            reinterpret_cast<uint32_t *>(zv)[vb + i] = h;
+            z0 = bf16_lo(h);
+            z1 = bf16_hi(h);
+        } else {
+            reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
+        }
         if (i < rd.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
     }
     double v[1] = {rz};
@@ -1164,6 +1171,7 @@ AmgFine amg_fine(mof_mesh *m) {
     f.sell_off = m->sell_off.p;
     f.x0 = G.lv[0].x.p;
     f.omega = G.omega;
+    f.smoothed = G.lv[0].smoothed;
     return f;
 }
 
@@ -1245,7 +1253,7 @@ Lvl level_view(const AmgDevLevel &D) {
 }
 
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part_slot, int32_t nblk,
-                const RedArgs &rd, hipStream_t s) {
+                const RedArgs &rd, hipStream_t s, bool zh) {
     AmgDevice &G = *m->amg;
     Workspace &w = m->ws;
     const int32_t L = (int32_t)G.lv.size();
@@ -1297,13 +1305,23 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
-                k_post0<2><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot, rd);
+                if (zh)
+                    k_post0<2, true><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot,
+                                                        rd);
+                else
+                    k_post0<2, false><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0,
+                                                         part_slot, rd);
             } else {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
-                k_post0<1><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot, rd);
+                if (zh)
+                    k_post0<1, true><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot,
+                                                        rd);
+                else
+                    k_post0<1, false><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0,
+                                                         part_slot, rd);
             }
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);

@@ -321,8 +321,9 @@ void amg_ensure(mof_mesh *m, int32_t B);            // per-system storage
 void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s);  // Galerkin + coarse inverse
 // z = V-cycle(r) on the fp32 inner vectors; writes partial r.z (component 0)
 // into the part_rzrr slot `part_slot`
+// zh: write z as a bf16 pair per vertex (uint32) instead of float2
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_slot, int32_t nblk,
-                const RedArgs &rd, hipStream_t s);
+                const RedArgs &rd, hipStream_t s, bool zh);
 // level-0 smoother data the PCG update / init write the pre-smoothing with
 struct AmgFine {
     const void *D0h;  // bf16 2x2 D^-1 [B][N] (uint2 each)
@@ -331,6 +332,7 @@ struct AmgFine {
     const int32_t *sell_off;
     float *x0;        // smoother x
     float omega;
+    bool smoothed;    // level 0 has the smoothed prolongator (irregular mesh)
 };
 AmgFine amg_fine(mof_mesh *m);
 // bf16 level-0 A / D^-1 of the next batch, written by the assembly (marks

@@ -91,6 +91,7 @@ struct PcgArgs {
     RedArgs red;           // partial-record layout; rows >= red.nown (ghosts) are not summed
     int32_t stall;         // stagnation window in iterations (0: off)
     double *sc;            // pre-reduced scalars (k_red_rzrr / k_red_pq), by iteration parity
+    int32_t zh;            // z stored as bf16 pairs (the multigrid cycle's output, MOF_Z_BF16)
 };
 
 // The per-system scalars every workgroup of the next launch needs, reduced
@@ -408,6 +409,12 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
 
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
 
+// The multigrid cycle's output z stored as a bf16 pair per vertex (single
+// domain; the decomposed path's halo exchange moves float2 z)
+#ifndef MOF_Z_BF16
+#define MOF_Z_BF16 1
+#endif
+
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__restrict__ rhs) {
     __shared__ double lds[8];
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, doub
 constexpr int kSpmvRows = MOF_SPMV_ROWS;
 constexpr int kSpmvWG = kRowsPerWG / kSpmvRows;
 
-template <typename V, bool FIRST, int NT = kWG>
+template <typename V, bool FIRST, int NT = kWG, bool ZH = false>
 __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
     constexpr int RPT = kRowsPerWG / NT;  // rows per thread
     __shared__ double lds[2 * (NT / 64)];
@@ -600,9 +607,17 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
         const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
         if (i >= a.N) break;
         V y0, y1;
-        spmv_row<V>(a.mat, b, i, a.z + 2 * vb, y0, y1);
         const int64_t vi = vb + i;
-        const V2 zi = *reinterpret_cast<const V2 *>(a.z + 2 * vi);
+        V2 zi;
+        if constexpr (ZH) {
+            spmv_row<V, true>(a.mat, b, i, reinterpret_cast<const V *>(reinterpret_cast<const uint32_t *>(a.z) + vb),
+                              y0, y1);
+            const uint32_t h = reinterpret_cast<const uint32_t *>(a.z)[vi];
+            zi = V2{bf16_lo(h), bf16_hi(h)};
+        } else {
+            spmv_row<V>(a.mat, b, i, a.z + 2 * vb, y0, y1);
+            zi = *reinterpret_cast<const V2 *>(a.z + 2 * vi);
+        }
         V2 qi, pi;
         if (FIRST) {
             qi = V2{y0, y1};
@@ -630,23 +645,34 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
 
 // the fp32 instances run at >= 5 waves per SIMD (MOF_ROW_OCC: +1 % at C3);
 // the fp64 ones keep the compiler's choice (the hint costs C2 fp64 2.7 %)
-template <typename V, bool FIRST>
+template <typename V, bool FIRST, bool ZH = false>
 __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int32_t flags) {
     pcg_spmv_body<V, FIRST>(a, it, flags);
 }
-template <>
-__global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, true>(PcgArgs<float> a, int32_t it,
-                                                                                 int32_t flags) {
-    pcg_spmv_body<float, true, kSpmvWG>(a, it, flags);
-}
-template <>
-__global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, false>(PcgArgs<float> a, int32_t it,
-                                                                                  int32_t flags) {
-    pcg_spmv_body<float, false, kSpmvWG>(a, it, flags);
-}
+#define MOF_SPMV_F32(FIRST, ZH)                                                                              \
+    template <>                                                                                              \
+    __global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, FIRST, ZH>(PcgArgs<float> a,   \
+                                                                                       int32_t it,          \
+                                                                                       int32_t flags) {     \
+        pcg_spmv_body<float, FIRST, kSpmvWG, ZH>(a, it, flags);                                              \
+    }
+MOF_SPMV_F32(true, false)
+MOF_SPMV_F32(false, false)
+MOF_SPMV_F32(true, true)
+MOF_SPMV_F32(false, true)
+#undef MOF_SPMV_F32
 // workgroup size of an SpMV launch
 template <typename V>
 constexpr int spmv_wg() { return sizeof(V) == 4 ? kSpmvWG : kWG; }
+template <typename V>
+void launch_spmv(const PcgArgs<V> &a, bool first, dim3 g, hipStream_t s, int32_t it, int32_t flags) {
+    if (first)
+        a.zh ? k_pcg_spmv<V, true, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags)
+             : k_pcg_spmv<V, true, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+    else
+        a.zh ? k_pcg_spmv<V, false, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags)
+             : k_pcg_spmv<V, false, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+}
 
 constexpr int kUpdRB = kRows >= 4 ? 1 : 4 / kRows;  // row blocks per update workgroup
 inline unsigned upd_blocks(int32_t nblk) { return (unsigned)((nblk + kUpdRB - 1) / kUpdRB); }
@@ -979,6 +1005,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.dA_off = nullptr;
     a.stall = 0;
     a.sc = w.sc.p;
+    a.zh = 0;
     return a;
 }
 
@@ -1044,12 +1071,15 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             a.dA = static_cast<const uint2 *>(f.A0h);
             a.dA_nb = f.sell_nb;
             a.dA_off = f.sell_off;
+            // bf16 z with the tentative prolongator (C3 +1 %, C2 mixed +2 %,
+            // same iterations); R3 on the smoothed one: 63 vs 50 its
+            a.zh = MOF_Z_BF16 && !f.smoothed;
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
     // z = M^-1 r for the external preconditioner, r.z into slot `slot`
     auto precond = [&](int32_t slot) {
-        if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s);
+        if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s, a.zh != 0);
     };
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B, kGrpSpmv));
@@ -1089,16 +1119,11 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 // events stamped by the kernel's own dispatch packet (start
                 // and end of its execution, as rocprof's kernel trace), not
                 // separate marker packets around it
-                if (it == 0)
-                    hipExtLaunchKernelGGL(k_pcg_spmv<V, true>, gx, dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0, a,
-                                          it, 0);
-                else
-                    hipExtLaunchKernelGGL(k_pcg_spmv<V, false>, gx, dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0,
-                                          a, it, 0);
-            } else if (it == 0) {
-                k_pcg_spmv<V, true><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
+                auto kf = it == 0 ? (a.zh ? k_pcg_spmv<V, true, true> : k_pcg_spmv<V, true, false>)
+                                  : (a.zh ? k_pcg_spmv<V, false, true> : k_pcg_spmv<V, false, false>);
+                hipExtLaunchKernelGGL(kf, gx, dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0, a, it, 0);
             } else {
-                k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
+                launch_spmv(a, it == 0, gx, s, it, 0);
             }
             if (MOF_PRS) k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it & 1);
             k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), (unsigned)B), kWG, 0, s>>>(a, it);
@@ -1122,7 +1147,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     }
     if (!done) {
         // one more check launch so SI_CONV records systems converged at max_iter
-        k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(a, it, 0);
+        launch_spmv(a, false, gx, s, it, 0);
         if (sp.fail_at_max_iter) k_fail_running<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, it, a.sysi);
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -1360,7 +1385,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
             if (amg)
                 for (size_t l = 0; l < L; ++l)
                     amg_vcycle(d->parts[l], B, args[l].r, args[l].z, d->part_rzrr.p + slot * ps,
-                               d->parts[l]->ws.nblk, args[l].red, s);
+                               d->parts[l]->ws.nblk, args[l].red, s, false);
         }
         dd_sync_partials(d, d->part_rzrr.p + slot * ps, 2 * rec, s);
         if (MOF_PRS)
@@ -1389,10 +1414,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
         dd_halo(d, B, sizeof(V) == 4, 0, s);
         for (size_t l = 0; l < L; ++l) {
             const dim3 gx(xcd_grid(d->parts[l]->ws.nblk, B, kGrpSpmv));
-            if (first)
-                k_pcg_spmv<V, true><<<gx, spmv_wg<V>(), 0, s>>>(args[l], it_, 0);
-            else
-                k_pcg_spmv<V, false><<<gx, spmv_wg<V>(), 0, s>>>(args[l], it_, 0);
+            launch_spmv(args[l], first, gx, s, it_, 0);
         }
         dd_sync_partials(d, d->part_pq.p + (it_ & 1) * (int64_t)d->P * rec, rec, s);  // this parity's slot
         if (MOF_PRS)

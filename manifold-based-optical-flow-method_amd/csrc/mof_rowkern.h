@@ -45,6 +45,19 @@ __device__ __forceinline__ void ld_blk(const double *A, int64_t pos, double (&a)
     a[0] = v0.x; a[1] = v0.y; a[2] = v1.x; a[3] = v1.y;
 }
 
+// bf16 copies of the level-0 operator for the multigrid smoother sweeps (the
+// preconditioner only needs an SPD approximation of A; rounding the blocks
+// (i,j) and (j,i)^T alike keeps it symmetric) -- half the bytes of A32.
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;  // round to nearest even
+}
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+__device__ __forceinline__ uint2 bf16x4(float a, float b, float c, float d) {
+    return make_uint2(bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16));
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -144,7 +157,9 @@ __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
 #define MOF_SWEEP_U 8
 #endif
 
-template <bool sym, typename V>
+// ZH: the operand is a bf16 pair per row (uint32 each; x points at the
+// system's first one) instead of V2
+template <bool sym, typename V, bool ZH = false>
 __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int32_t i,
                                            const V *__restrict__ x, V &y0, V &y1) {
     using V2 = typename VT<V>::V2;
@@ -173,7 +188,14 @@ __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int3
                 ld_blk(A, (int64_t)o + t * kSlice + l, blk[u]);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) xj[u] = ld2(x + 2 * (int64_t)j[u]);
+        for (int u = 0; u < U; ++u) {
+            if constexpr (ZH) {
+                const uint32_t h = reinterpret_cast<const uint32_t *>(x)[j[u]];
+                xj[u] = V2{bf16_lo(h), bf16_hi(h)};
+            } else {
+                xj[u] = ld2(x + 2 * (int64_t)j[u]);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if constexpr (sym) {
@@ -194,13 +216,13 @@ __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int3
 }
 // sell_mir == nullptr (a mesh without symmetric reads, and fp64): every block
 // at its own position, no table reads
-template <typename V>
+template <typename V, bool ZH = false>
 __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
                                          const V *__restrict__ x, V &y0, V &y1) {
     if (MOF_SYM_A && sizeof(V) == 4 && mt.sell_mir)
-        spmv_row_t<MOF_SYM_A && sizeof(V) == 4>(mt, b, i, x, y0, y1);
+        spmv_row_t<MOF_SYM_A && sizeof(V) == 4, V, ZH>(mt, b, i, x, y0, y1);
     else
-        spmv_row_t<false>(mt, b, i, x, y0, y1);
+        spmv_row_t<false, V, ZH>(mt, b, i, x, y0, y1);
 }
 
 // XCD-aware workgroup -> (row block, system): workgroups w and w+8 share an
@@ -257,19 +279,6 @@ inline unsigned xcd_grid(int32_t nblk, int32_t B, int32_t grp_sz) {
     return (unsigned)(8 * G * ((B + G - 1) / G) * ((nblk + 7) / 8));
 }
 
-
-// bf16 copies of the level-0 operator for the multigrid smoother sweeps (the
-// preconditioner only needs an SPD approximation of A; rounding the blocks
-// (i,j) and (j,i)^T alike keeps it symmetric) -- half the bytes of A32.
-__device__ __forceinline__ uint32_t bf16_bits(float f) {
-    const uint32_t u = __float_as_uint(f);
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;  // round to nearest even
-}
-__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
-__device__ __forceinline__ uint2 bf16x4(float a, float b, float c, float d) {
-    return make_uint2(bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16));
-}
 
 struct MatH {
     int64_t sell_nb;

@@ -137,7 +137,9 @@ def test_symmetric_reads_match_spsolve(precond, monkeypatch):
         out[sym] = (V, st["iterations"])
         m.close()
     assert abs(out["0"][1] - out["1"][1]) <= 0.02 * out["0"][1]
-    assert np.abs(out["0"][0] - out["1"][0]).max() < 1e-8 * np.abs(out["0"][0]).max()
+    # (the multigrid cycle's bf16 output z makes the two paths' iterates part
+    # a little more than block Jacobi's: 1.7e-8 relative)
+    assert np.abs(out["0"][0] - out["1"][0]).max() < 1e-7 * np.abs(out["0"][0]).max()
 
 
 @pytest.mark.parametrize("same_I2", [True, False])
