@@ -108,7 +108,11 @@ def pmc_traffic(key, kernel):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         entry = json.load(open(path))[key]
-        return round(entry["kernels"][kernel]["hbm_bytes_per_launch"]), entry["source"][0]
+        # the instance name may carry more template arguments (e.g. the bf16-z
+        # flag: k_pcg_spmv<float, false, true>); the largest matching instance
+        names = [k for k in entry["kernels"] if k == kernel or k.startswith(kernel[:-1] + ",")]
+        best = max(names, key=lambda k: entry["kernels"][k]["hbm_bytes_per_launch"])
+        return round(entry["kernels"][best]["hbm_bytes_per_launch"]), entry["source"][0]
     except (OSError, ValueError, KeyError):
         return None, None
 

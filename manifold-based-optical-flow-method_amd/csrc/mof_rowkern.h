@@ -129,6 +129,9 @@ struct MatArgs {
 // mirrored reads of 64 neighbouring rows fall on about as few cache lines as
 // their own reads would. Padding slots read the row's diagonal, masked.
 __device__ __forceinline__ int64_t mir_pos(int32_t m, int64_t diag) { return m < 0 ? diag : (int64_t)(m & kMirPos); }
+#ifndef MOF_SYM_F64
+#define MOF_SYM_F64 1
+#endif
 
 template <typename V>
 __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
@@ -219,8 +222,12 @@ __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int3
 template <typename V, bool ZH = false>
 __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_t i,
                                          const V *__restrict__ x, V &y0, V &y1) {
-    if (MOF_SYM_A && sizeof(V) == 4 && mt.sell_mir)
-        spmv_row_t<MOF_SYM_A && sizeof(V) == 4, V, ZH>(mt, b, i, x, y0, y1);
+    // fp64 too: the fp64 A is bit-symmetric (the reference's mirrored
+    // assignment, §2.2), so the transposed reads give the same bits
+    if (MOF_SYM_A && MOF_SYM_F64 && mt.sell_mir)
+        spmv_row_t<(bool)(MOF_SYM_A && MOF_SYM_F64), V, ZH>(mt, b, i, x, y0, y1);
+    else if (MOF_SYM_A && sizeof(V) == 4 && mt.sell_mir)
+        spmv_row_t<(bool)MOF_SYM_A, V, ZH>(mt, b, i, x, y0, y1);
     else
         spmv_row_t<false, V, ZH>(mt, b, i, x, y0, y1);
 }

@@ -25,7 +25,7 @@ PEAK_GBS = 8000.0
 def main():
     line = json.loads(open(sys.argv[1]).readline())
     rl = line["roofline"]
-    prefix = "k_pcg_spmv<%s" % ("float" if line["dtype"] == "f32" else "double")
+    prefix = "k_pcg_spmv<%s" % ("float" if line["dtype"] == "f32" else "double")  # both instances: the last launches
     rows = list(csv.DictReader(open(sys.argv[2])))
     full_us = None
     if rows and "Start_Timestamp" in rows[0]:
@@ -52,8 +52,9 @@ def main():
     if len(sys.argv) > 3:
         key = sys.argv[3]
         ent = json.load(open(sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"))[key]
-        k = ent["kernels"]["k_pcg_spmv<float, false>" if line["dtype"] == "f32" else "k_pcg_spmv<double, false>"]
-        out["pmc_hbm_bytes_median_launch"] = k["hbm_bytes_per_launch"]
+        base = "k_pcg_spmv<float, false" if line["dtype"] == "f32" else "k_pcg_spmv<double, false"
+        names = [n for n in ent["kernels"] if n.startswith(base)]  # + template flags (bf16 z)
+        out["pmc_hbm_bytes_median_launch"] = max(ent["kernels"][n]["hbm_bytes_per_launch"] for n in names)
     print(json.dumps(out, indent=1))
 
 

@@ -116,6 +116,23 @@ def test_spmv_accounting_systems_equal_iterations(precision, precond, sym, monke
     assert lo <= st["spmv_bytes"] <= lo + st["spmv_launches"] * shared
 
 
+def test_symmetric_reads_fp64_bit_identical(monkeypatch):
+    """The fp64 A is bit-symmetric (the reference's mirrored assignment), so
+    the fp64 PCG reading lower blocks as transposed upper ones gives V bit
+    for bit the same as reading every block in place."""
+    g = load_golden("G1_ico642")
+    out = []
+    for sym in ("0", "1"):
+        monkeypatch.setenv("MOF_SYM_READS", sym)
+        m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+        V, st = m.solve_range(g["I"], g["t_k"], 0, 15, float(g["lambda_"]), precision="f64")
+        assert st["failed"] == 0
+        out.append((V, st["iterations"]))
+        m.close()
+    assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0])
+    assert np.abs(out[1][0] - g["V_k"]).max() < VTOL
+
+
 @pytest.mark.parametrize("precond", ["jacobi", "amg"])
 def test_symmetric_reads_match_spsolve(precond, monkeypatch):
     """The fp32 / bf16 operators read through the mirror table (lower blocks
