@@ -457,6 +457,50 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
 #ifndef MOF_ASM_ROWS_U
 #define MOF_ASM_ROWS_U 1
 #endif
+// Row i's stores of one system: A blocks (+ lambda a2), the bf16 copies,
+// the diagonal block's inverse and f_i.
+template <int WMAX>
+__device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f0, double f1, int32_t i, int32_t b,
+                                           int32_t N, int32_t deg, int64_t o, int64_t sell_nb,
+                                           const int32_t *__restrict__ sell_col, const float *__restrict__ a2s,
+                                           int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
+                                           double *__restrict__ rhs, uint2 *__restrict__ Ah, uint2 *__restrict__ Dh,
+                                           int32_t nown, const int32_t *__restrict__ mir) {
+#pragma unroll
+    for (int z = 0; z < WMAX; ++z) {
+        if (z >= deg) continue;
+        const int64_t pos = o + (int64_t)z * kSlice;
+        // symmetric layout: lower blocks are read as transposed upper
+        // ones and never leave the registers
+        if (mir && (mir[pos] & kMirT)) continue;
+        const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
+        const float Av[4] = {acc[z][0] + s4.x, acc[z][1] + s4.y, acc[z][2] + s4.z, acc[z][3] + s4.w};
+        const int64_t qq = (int64_t)b * sell_nb + pos;
+        reinterpret_cast<float4 *>(A)[qq] = make_float4(Av[0], Av[1], Av[2], Av[3]);
+        if (Ah) {
+            const bool g = i >= nown || sell_col[pos] >= nown;
+            Ah[qq] = g ? bf16x4(z == 0 ? 1.f : 0.f, 0.f, 0.f, z == 0 ? 1.f : 0.f) : bf16x4(Av[0], Av[1], Av[2], Av[3]);
+        }
+        if (z != 0) continue;
+        double inv[4];
+        const double d0 = Av[0], d1 = Av[1], d2 = Av[2], d3 = Av[3];
+        if (block_jacobi) {
+            const double det = d0 * d3 - d1 * d2;
+            inv[0] = d3 / det; inv[1] = -d1 / det; inv[2] = -d2 / det; inv[3] = d0 / det;
+        } else {
+            inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
+        }
+        const int64_t vi = (int64_t)b * N + i;
+        if (Dh)
+            Dh[vi] = i >= nown ? bf16x4(1.f, 0.f, 0.f, 1.f)
+                               : bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+        else
+            reinterpret_cast<float4 *>(dinv32)[vi] =
+                make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
+        *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
+    }
+}
+
 template <int WMAX>
 __global__ __launch_bounds__(kWG) void k_assemble_rows(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
@@ -534,40 +578,138 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows(
                 }
             }
         }
-        const int32_t deg = vptr[i + 1] - vptr[i];
-        const int64_t o = sell_off[s];
+        rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
+                         block_jacobi, A, dinv32, rhs, Ah, Dh, nown, mir);
+    }
+}
+
+// Row assembly that forms the triangle terms itself (MOF_ASM_RC): per
+// incident triangle, u = grad_M I . e at (i, v_{a+1}, v_{a+2}) and row i's f
+// term in k_tri_step's exact arithmetic (the I0 values in the triangle's own
+// corner order, np.dot's fma chain, the f term's operation order), so
+// k_tri_step and its u32 / fc round trip (72 B stored and 120 B gathered per
+// triangle and system) drop out of the mixed path. A workgroup runs NS
+// systems over one row block (MOF_ASM_NS): each incident triangle's geometry
+// (tinc, tslot, the weight, gw, e of the other two corners, the area: ~200 B
+// of scattered loads) is fetched once for NS systems, which only gather their
+// I values -- but NS = 2 / 4 lower the occupancy (124 -> 290 VGPRs at NS = 4)
+// and measured no faster (C3: 10.0 / 10.4 / 14.6 ms per launch at NS = 1 / 2
+// / 4). The fp32 a1 fold adds the terms one by one in triangle order (fma by
+// 0/1 slot masks: 10.0 ms vs 11.9 ms with k_assemble_rows' mul-add fold); f
+// folds in fp64 in the reference's triangle order.
+#ifndef MOF_ASM_RC
+#define MOF_ASM_RC 1
+#endif
+#ifndef MOF_ASM_NS
+#define MOF_ASM_NS 1
+#endif
+
+struct TriGeo {
+    const double *gw, *e, *area, *J0, *J1, *dt;  // J0 / J1: the batch's I rows (internal order, stride N)
+};
+template <int WMAX, int NS>
+__global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
+    int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
+    const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
+    const int4 *__restrict__ tinc, const int32_t *__restrict__ tslot, const float *__restrict__ w12,
+    const float *__restrict__ a2s, int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
+    double *__restrict__ rhs, uint2 *__restrict__ Ah, uint2 *__restrict__ Dh, int32_t nown,
+    const int32_t *__restrict__ mir, TriGeo geo) {
+    int32_t rb, bq;
+    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpAsm)) return;
+    const double *I0b[NS], *I1b[NS];
+    double hb[NS];
 #pragma unroll
-        for (int z = 0; z < WMAX; ++z) {
-            if (z >= deg) continue;
-            const int64_t pos = o + (int64_t)z * kSlice + l;
-            // symmetric layout: lower blocks are read as transposed upper
-            // ones and never leave the registers
-            if (mir && (mir[pos] & kMirT)) continue;
-            const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
-            const float Av[4] = {acc[z][0] + s4.x, acc[z][1] + s4.y, acc[z][2] + s4.z, acc[z][3] + s4.w};
-            const int64_t qq = (int64_t)b * sell_nb + pos;
-            reinterpret_cast<float4 *>(A)[qq] = make_float4(Av[0], Av[1], Av[2], Av[3]);
-            if (Ah) {
-                const bool g = i >= nown || sell_col[pos] >= nown;
-                Ah[qq] = g ? bf16x4(z == 0 ? 1.f : 0.f, 0.f, 0.f, z == 0 ? 1.f : 0.f) : bf16x4(Av[0], Av[1], Av[2], Av[3]);
+    for (int k = 0; k < NS; ++k) {
+        const int32_t b = min(bq * NS + k, B - 1);  // slots past B recompute B-1 and store nothing
+        I0b[k] = geo.J0 + (int64_t)b * N;
+        I1b[k] = geo.J1 + (int64_t)b * N;
+        hb[k] = geo.dt[b];
+    }
+#pragma unroll 1
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= N) break;
+        const int32_t s = i >> 6, l = i & 63;
+        float acc[NS][WMAX][4];
+        double f0[NS], f1[NS], Ii0[NS], pdi[NS];
+        double ei[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ei[k] = geo.e[6 * (int64_t)i + k];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+#pragma unroll
+            for (int z = 0; z < WMAX; ++z) acc[k][z][0] = acc[k][z][1] = acc[k][z][2] = acc[k][z][3] = 0.f;
+            f0[k] = f1[k] = 0.0;
+            Ii0[k] = I0b[k][i];
+            pdi[k] = (I1b[k][i] - Ii0[k]) / hb[k];
+        }
+        const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
+        for (int32_t t = 0; t < tw; ++t) {
+            const int64_t e = (int64_t)to + (int64_t)t * kSlice + l;
+            const int4 q = tinc[e];
+            const int32_t sl = tslot[e];
+            const bool real = q.x < M;                   // padding (T = M): weight 0, no f term
+            const int64_t T = min(q.x, M - 1);
+            const int32_t c = q.y, vj = q.z, vk = q.w;
+            double g[9], ej[6], ek[6];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) g[k] = geo.gw[9 * T + k];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                ej[k] = geo.e[6 * (int64_t)vj + k];
+                ek[k] = geo.e[6 * (int64_t)vk + k];
             }
-            if (z != 0) continue;
-            double inv[4];
-            const double d0 = Av[0], d1 = Av[1], d2 = Av[2], d3 = Av[3];
-            if (block_jacobi) {
-                const double det = d0 * d3 - d1 * d2;
-                inv[0] = d3 / det; inv[1] = -d1 / det; inv[2] = -d2 / det; inv[3] = d0 / det;
-            } else {
-                inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
+            const double At = geo.area[T];
+            const float wv = w12[q.x];
+            const int32_t sj = sl & 0xff, sk = sl >> 8;
+            // a term on the diagonal block takes A/6 = 2 A/12 (a degenerate
+            // triangle's second corner at i included)
+            const float wd = 2.f * wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
+            // set(T) - {i} in corner order: at most 2 distinct other corners
+            const bool hj = vj != i, hk = vk != i && vk != vj;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                const double aj = I0b[k][vj], ak = I0b[k][vk];
+                const double pdj = (I1b[k][vj] - aj) / hb[k], pdk = (I1b[k][vk] - ak) / hb[k];
+                // the triangle's I0 in its own corner order (corner c is i)
+                const double c0 = c == 0 ? Ii0[k] : (c == 1 ? ak : aj);
+                const double c1 = c == 0 ? aj : (c == 1 ? Ii0[k] : ak);
+                const double c2 = c == 0 ? ak : (c == 1 ? aj : Ii0[k]);
+                double gI[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[d] + c1 * g[3 + d]) + c2 * g[6 + d];
+                const double ui0 = dot64(gI, ei), ui1 = dot64(gI, ei + 3);
+                const double po = hj ? (hk ? pdj + pdk : pdj) : (hk ? pdk : 0.0);
+                if (real) {  // f in the reference's triangle order
+                    f0[k] += ui0 * (2 * pdi[k] + po) * At / 12;
+                    f1[k] += ui1 * (2 * pdi[k] + po) * At / 12;
+                }
+                const float2 ui = make_float2((float)ui0, (float)ui1);
+                const float2 uj = make_float2((float)dot64(gI, ej), (float)dot64(gI, ej + 3));
+                const float2 uk = make_float2((float)dot64(gI, ek), (float)dot64(gI, ek + 3));
+                const float d4[4] = {ui.x * ui.x * wd, ui.x * ui.y * wd, ui.y * ui.x * wd, ui.y * ui.y * wd};
+                const float cj[4] = {ui.x * uj.x * wj, ui.x * uj.y * wj, ui.y * uj.x * wj, ui.y * uj.y * wj};
+                const float ck[4] = {ui.x * uk.x * wk, ui.x * uk.y * wk, ui.y * uk.x * wk, ui.y * uk.y * wk};
+#pragma unroll
+                for (int z = 0; z < WMAX; ++z) {
+                    const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        float a = z == 0 ? acc[k][z][x] + d4[x] : acc[k][z][x];
+                        a = __builtin_fmaf(mj, cj[x], a);
+                        acc[k][z][x] = __builtin_fmaf(mk, ck[x], a);
+                    }
+                }
             }
-            const int64_t vi = (int64_t)b * N + i;
-            if (Dh)
-                Dh[vi] = i >= nown ? bf16x4(1.f, 0.f, 0.f, 1.f)
-                                   : bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
-            else
-                reinterpret_cast<float4 *>(dinv32)[vi] =
-                    make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
-            *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
+        }
+        const int32_t deg = vptr[i + 1] - vptr[i];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const int32_t b = bq * NS + k;
+            if (b < B)
+                rows_store<WMAX>(acc[k], f0[k], f1[k], i, b, N, deg, sell_off[s] + l, sell_nb, sell_col, a2s,
+                                 block_jacobi, A, dinv32, rhs, Ah, Dh, nown, mir);
         }
     }
 }
@@ -809,15 +951,26 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     }
     const double *J0 = w.Iint.p, *J1 = w.Iint.p + (I1 == I0 + ldI ? (int64_t)m->N : (int64_t)m->N * B);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
-    // the mixed path's residual re-forms u from the I rows: no u64 stores
+    static const int rows_env = [] {
+        const char *v = std::getenv("MOF_ASM_ROWS");
+        return v ? std::atoi(v) : MOF_ASM_ROWS_DEFAULT;
+    }();
+    const int32_t W = m->pat.max_w;
+    const bool rows = precision == MOF_PREC_MIXED && rows_env && W <= 16;
+    // the row kernel forms the triangle terms itself (MOF_ASM_RC): no
+    // k_tri_step; otherwise the mixed path's residual still re-forms u from
+    // the I rows, so no u64 stores
+    const bool asm_rc = MOF_ASM_RC && rows;
     const bool skip_u64 = MOF_RES_RECOMPUTE && precision == MOF_PREC_MIXED;
-    k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
-                                  skip_u64 ? nullptr : w.u64.p, w.fc.p,
-                                  precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
-    w.u64_stale = skip_u64;
+    if (!asm_rc)
+        k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
+                                      skip_u64 ? nullptr : w.u64.p, w.fc.p,
+                                      precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
+    w.u64_stale = skip_u64 || asm_rc;  // u64 (and with asm_rc fc) re-formed by the fp64 recovery if needed
     w.J0 = J0;
     w.J1 = J1;
     w.JB = B;
+    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, J1, w.dt.p};
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
@@ -826,24 +979,32 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
     // row-wise assembly when the widest row fits the register accumulators
     // (MOF_ASM_ROWS=0: the per-block kernel)
-    static const int rows_env = [] {
-        const char *v = std::getenv("MOF_ASM_ROWS");
-        return v ? std::atoi(v) : MOF_ASM_ROWS_DEFAULT;
-    }();
-    const int32_t W = m->pat.max_w;
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
     const dim3 gr(xcd_grid(nblk_rows, B, kGrpAsm));
-    if (precision == MOF_PREC_MIXED && rows_env && W <= 8)
-        k_assemble_rows<8><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p,
-                                             m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p,
-                                             m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p, w.dinv32.p,
-                                             w.rhs.p, bf.A0h, bf.D0h, m->n_own, m->sym_reads && MOF_SKIP_LOWER ? m->sell_mir.p : nullptr);
-    else if (precision == MOF_PREC_MIXED && rows_env && W <= 16)
-        k_assemble_rows<16><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p,
-                                              m->vptr.p, m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p),
-                                              m->tslot.p, m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p,
-                                              w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own,
-                                              m->sym_reads && MOF_SKIP_LOWER ? m->sell_mir.p : nullptr);
+    const int32_t *mirw = m->sym_reads && MOF_SKIP_LOWER ? m->sell_mir.p : nullptr;
+#define MOF_ASM_ROWS_LAUNCH(WM)                                                                                   \
+    k_assemble_rows<WM><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p,   \
+                                           m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p,     \
+                                           m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p, w.dinv32.p,         \
+                                           w.rhs.p, bf.A0h, bf.D0h, m->n_own, mirw)
+#define MOF_ASM_RC_LAUNCH(WM, NS)                                                                                 \
+    k_assemble_rows_rc<WM, NS><<<xcd_grid(nblk_rows, (B + (NS)-1) / (NS), kGrpAsm), kWG, 0, s>>>(                 \
+        m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
+        reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p, m->w12_32.p, m->a2s32.p, bj, w.A32.p, w.dinv32.p,   \
+        w.rhs.p, bf.A0h, bf.D0h, m->n_own, mirw, geo)
+    if (rows && W <= 8) {
+        if (asm_rc)
+            MOF_ASM_RC_LAUNCH(8, MOF_ASM_NS);
+        else
+            MOF_ASM_ROWS_LAUNCH(8);
+    } else if (rows) {
+        if (asm_rc)
+            MOF_ASM_RC_LAUNCH(16, (MOF_ASM_NS + 1) / 2);
+        else
+            MOF_ASM_ROWS_LAUNCH(16);
+    }
+#undef MOF_ASM_ROWS_LAUNCH
+#undef MOF_ASM_RC_LAUNCH
     else if (precision == MOF_PREC_MIXED)
         k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                             m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,
