@@ -669,46 +669,76 @@ __global__ __launch_bounds__(kWG) void k_res3(Lvl L, const int32_t *__restrict__
 // kRG members forms its own group and is summed straight from memory.
 constexpr int kRG = 1024;
 
-template <int BSF>
+// NS systems per workgroup share each member's Q row load; the contributions
+// of all NS systems are staged in LDS (level 0: MOF_RESTR_S = 2, C3 232 ->
+// 194 us per 512-system launch; NS = 4: 235 us, its 48-KB LDS stage lowers
+// the occupancy).
+#ifndef MOF_RESTR_S
+#define MOF_RESTR_S 2
+#endif
+template <int BSF, int NS = 1>
 __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
                                                   int32_t B, int32_t smooth, float omega,
                                                   const int32_t *__restrict__ sysi) {
-    __shared__ float con[3][kRG];
-    int32_t g, b;
-    if (!xcd_map(ngrp, B, g, b, kGrpRestr) || retired(sysi, b)) return;
+    // no fp contraction: every system slot of the unrolled loops rounds alike
+#pragma clang fp contract(off)
+    __shared__ float con[NS][3][kRG];
+    int32_t g, bq;
+    if (!xcd_map(ngrp, (B + NS - 1) / NS, g, bq, kGrpRestr)) return;
+    const int32_t b0 = bq * NS;
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) any |= b0 + t < B && !retired(sysi, b0 + t);
+    if (!any) return;
     const int32_t I0 = grp[g], I1 = grp[g + 1];
     const int32_t q0 = F.mptr[I0], q1 = F.mptr[I1];
     if (q1 - q0 > kRG) {  // one oversized aggregate
-        if (threadIdx.x == 0) restrict_node<BSF>(F, C, b, I0, smooth != 0, omega);
+        if (threadIdx.x == 0)
+            for (int t = 0; t < NS; ++t)
+                if (b0 + t < B && !retired(sysi, b0 + t)) restrict_node<BSF>(F, C, b0 + t, I0, smooth != 0, omega);
         return;
     }
     for (int32_t q = q0 + threadIdx.x; q < q1; q += kWG) {
-        float ri[BSF];
-        ldr<BSF>(F.r, b, F.n, r_at<BSF>(F, q), ri);
+        float ri[NS][BSF];
+#pragma unroll
+        for (int t = 0; t < NS; ++t) ldr<BSF>(F.r, min(b0 + t, B - 1), F.n, r_at<BSF>(F, q), ri[t]);
         const float *qm = F.Qm + (int64_t)q * BSF * 3;
-        float c3[3] = {0.f, 0.f, 0.f};
+        float qv[BSF * 3];
 #pragma unroll
-        for (int k = 0; k < BSF; ++k)
+        for (int k = 0; k < BSF * 3; ++k) qv[k] = qm[k];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) c3[c] += qm[3 * k + c] * ri[k];
+        for (int t = 0; t < NS; ++t) {
+            float c3[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 3; ++c) con[c][q - q0] = c3[c];
+            for (int k = 0; k < BSF; ++k)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) c3[c] += qv[3 * k + c] * ri[t][k];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) con[t][c][q - q0] = c3[c];
+        }
     }
     __syncthreads();
     for (int32_t I = I0 + threadIdx.x; I < I1; I += kWG) {
-        float acc[3] = {0.f, 0.f, 0.f};
+        float acc[NS][3] = {};
         for (int32_t q = F.mptr[I]; q < F.mptr[I + 1]; ++q)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) acc[c] += con[c][q - q0];
-        const int64_t vo = (int64_t)b * C.n * 4;
-        stv<3>(C.b + vo, I, acc);
-        if (smooth) {
-            float d[3][3], x[3];
-            ld_dh(C, b, I, d);
-            matvec<3>(d, acc, x);
+            for (int t = 0; t < NS; ++t)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) x[c] *= omega;
-            stv<3>(C.x + vo, I, x);
+                for (int c = 0; c < 3; ++c) acc[t][c] += con[t][c][q - q0];
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            const int32_t b = b0 + t;
+            if (b >= B || retired(sysi, b)) continue;
+            const int64_t vo = (int64_t)b * C.n * 4;
+            stv<3>(C.b + vo, I, acc[t]);
+            if (smooth) {
+                float d[3][3], x[3];
+                ld_dh(C, b, I, d);
+                matvec<3>(d, acc[t], x);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) x[c] *= omega;
+                stv<3>(C.x + vo, I, x);
+            }
         }
     }
 }
@@ -857,14 +887,66 @@ __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__
 // node block run back to back on one XCD and share its Q rows in L2 instead
 // of re-reading Q per system (183 vs 261 us per 256-system launch with the
 // system-major grid; the coarse levels' kernels measured slower this way).
+// kProlR nodes x kProlS systems per thread, every load of the batch issued
+// before the first store: one node of one system per thread left each wave a
+// dependent agg -> y gather and little else (latency-bound), and the
+// systems of a thread share the node's agg and Q row loads. C3, 512
+// systems: 314 us (1 x 1), 270 (4 nodes), 231 (2 x 2), 202 (1 x 4), 210 (1 x 8)
+#ifndef MOF_PROL_R
+#define MOF_PROL_R 1
+#endif
+#ifndef MOF_PROL_S
+#define MOF_PROL_S 4
+#endif
+constexpr int kProlR = MOF_PROL_R, kProlS = MOF_PROL_S;
 template <int XM>
 __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, int32_t B,
                                                   const int32_t *__restrict__ sysi) {
-    int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b, kGrpProl) || retired(sysi, b)) return;
-    const int32_t i = rb * kWG + threadIdx.x;
-    if (i >= F.n) return;
-    prolong_node<2, XM>(F, C, b, i);
+    // no fp contraction: every system slot of the unrolled loops rounds alike
+#pragma clang fp contract(off)
+    int32_t rb, bq;
+    if (!xcd_map(nblk, (B + kProlS - 1) / kProlS, rb, bq, kGrpProl)) return;
+    const int32_t n = F.n;
+    int32_t ii[kProlR], ag[kProlR];
+    float q[kProlR][6];
+#pragma unroll
+    for (int r = 0; r < kProlR; ++r) {
+        ii[r] = (rb * kProlR + r) * kWG + threadIdx.x;
+        const int32_t i = min(ii[r], n - 1);
+        ag[r] = F.agg[i];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) q[r][k] = F.Q[(int64_t)i * 6 + k];
+    }
+    float2 x0[kProlS][kProlR];
+    float y[kProlS][kProlR][3];
+#pragma unroll
+    for (int t = 0; t < kProlS; ++t) {
+        const int32_t b = min(bq * kProlS + t, B - 1);
+        const float *yb = C.y + (int64_t)b * C.n * 4;
+#pragma unroll
+        for (int r = 0; r < kProlR; ++r) {
+            x0[t][r] = ld_x0(F.x, (int64_t)b * n + min(ii[r], n - 1));
+            ldv<3>(yb, ag[r], y[t][r]);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kProlS; ++t) {
+        const int32_t b = bq * kProlS + t;
+        if (b >= B || retired(sysi, b)) continue;
+        const int64_t vb = (int64_t)b * n;
+#pragma unroll
+        for (int r = 0; r < kProlR; ++r) {
+            if (ii[r] >= n) break;
+            float xi[2] = {x0[t][r].x, x0[t][r].y};
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                xi[k] += q[r][3 * k] * y[t][r][0] + q[r][3 * k + 1] * y[t][r][1] + q[r][3 * k + 2] * y[t][r][2];
+            if constexpr (XM == 2)  // full-precision x for the post-smoothing
+                reinterpret_cast<float2 *>(F.y)[vb + ii[r]] = make_float2(xi[0], xi[1]);
+            else
+                st_x0(F.x, vb + ii[r], xi[0], xi[1]);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kWG) void k_post3(Lvl L, float omega, const int32_t *__restrict__ sysi) {
@@ -1277,7 +1359,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                 k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNS - 1) / kNS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             } else {
-                k_restrict<2><<<dim3(xcd_grid(G.lv[0].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict<2, MOF_RESTR_S><<<dim3(xcd_grid(G.lv[0].ngrp, (B + MOF_RESTR_S - 1) / MOF_RESTR_S, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             }
         } else {
@@ -1298,13 +1380,14 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = S - 1; l >= 0; --l) {
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
-            const dim3 gsa(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), gp(xcd_grid(nb0, B, kGrpProl));
+            const int32_t nb0p = (v[0].n + kWG * kProlR - 1) / (kWG * kProlR);
+            const dim3 gsa(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), gp(xcd_grid(nb0p, (B + kProlS - 1) / kProlS, kGrpProl));
             const uint2 *D0h = reinterpret_cast<const uint2 *>(G.D0h.p);
             if (G.xm == 2) {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
-                    k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+                    k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
                     k_post0<2, true><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot,
                                                         rd);
@@ -1315,7 +1398,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
-                    k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
+                    k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
                     k_post0<1, true><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot,
                                                         rd);
