@@ -278,7 +278,13 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
 #ifndef MOF_GAL_NS
 #define MOF_GAL_NS 1
 #endif
-constexpr int kGalNS = 4;
+// systems per thread: C3 (512 systems) 6.08 ms per launch at 4, 8.06 at 8,
+// 14.7 at 16 (the per-system fine-block gathers, not the shared gather
+// lists, bound it; more systems per thread only lower the occupancy)
+#ifndef MOF_GAL_NSYS
+#define MOF_GAL_NSYS 4
+#endif
+constexpr int kGalNS = MOF_GAL_NSYS;
 __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
