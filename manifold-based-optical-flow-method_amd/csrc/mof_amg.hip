@@ -134,6 +134,45 @@ __device__ __forceinline__ void st_h9(uint4 *H, uint16_t *H22, int64_t q, const 
     H22[q] = (uint16_t)bf16_bits(c[2][2]);
 }
 
+// The coarse levels' sweep copy of A (levels >= 1 except the coarsest).
+// MOF_COARSE_I8 = 1: 12 B per 3x3 block, the 9 entries as offset-binary int8
+// (q + 128) with one bf16 scale per block (s = max |a| / 127): H viewed as
+// uint2[] (entries 0..7), H22 as uint32_t[] (entry 8 | scale << 16). A block
+// and its transposed twin have the same entries, so the same scale and the
+// same codes: the preconditioner stays symmetric. 0: bf16 entries, 18 B per
+// block (st_h9 / ld_h9).
+#ifndef MOF_COARSE_I8
+#define MOF_COARSE_I8 1
+#endif
+constexpr bool kCoarseI8 = MOF_COARSE_I8 != 0;
+// uint32 words of Ah and uint16 words of Ah22 per block
+constexpr size_t kAhWords = kCoarseI8 ? 2 : 4, kAh22Words = kCoarseI8 ? 2 : 1;
+
+__device__ __forceinline__ void st_a9(uint4 *H, uint16_t *H22, int64_t q, const float (&c)[3][3]) {
+    if constexpr (!kCoarseI8) {
+        st_h9(H, H22, q, c);
+    } else {
+        float m = 0.f;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) m = fmaxf(m, fabsf(c[r][k]));
+        const uint32_t sb = bf16_bits(m / 127.f);
+        const float sc = bf16_lo(sb);
+        uint32_t u[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float v = sc > 0.f ? rintf(c[r][k] / sc) : 0.f;
+                u[3 * r + k] = (uint32_t)(fminf(fmaxf(v, -127.f), 127.f) + 128.f);
+            }
+        reinterpret_cast<uint2 *>(H)[q] =
+            make_uint2(u[0] | (u[1] << 8) | (u[2] << 16) | (u[3] << 24), u[4] | (u[5] << 8) | (u[6] << 16) | (u[7] << 24));
+        reinterpret_cast<uint32_t *>(H22)[q] = u[8] | (sb << 16);
+    }
+}
+
 // ---- per-timestep setup --------------------------------------------------
 
 __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
@@ -248,7 +287,7 @@ __device__ __forceinline__ void galerkin_block(
         st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
     }
     st3(Ac, (int64_t)b * c_sell_nb + pos, C);
-    if (Ah) st_h9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, C);  // bf16 sweep copy
+    if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, C);  // sweep copy
 }
 
 // XCD-aware tiles: the B systems of a 256-position tile run back to back and
@@ -378,7 +417,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
             st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
         }
         st3(Ac, (int64_t)b * c_sell_nb + pos, Cm[t]);
-        if (Ah) st_h9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm[t]);
+        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm[t]);
     }
 }
 
@@ -495,6 +534,20 @@ __device__ __forceinline__ void ld_h9(const uint4 *H, const uint16_t *H22, int64
     a[2][1] = bf16_hi(h.w);
     a[2][2] = bf16_lo((uint32_t)H22[q]);
 }
+// block q of a coarse level's sweep copy (st_a9)
+__device__ __forceinline__ void ld_a9(const uint4 *H, const uint16_t *H22, int64_t q, float (&a)[3][3]) {
+    if constexpr (!kCoarseI8) {
+        ld_h9(H, H22, q, a);
+    } else {
+        const uint2 h = reinterpret_cast<const uint2 *>(H)[q];
+        const uint32_t t = reinterpret_cast<const uint32_t *>(H22)[q];
+        const float sc = bf16_hi(t);
+        const uint32_t w[3] = {h.x, h.y, t};
+#pragma unroll
+        for (int e = 0; e < 9; ++e)
+            a[e / 3][e % 3] = (float)((int32_t)((w[e >> 2] >> (8 * (e & 3))) & 0xffu) - 128) * sc;
+    }
+}
 // the smoother's 3x3 D^-1 of node i of system b
 __device__ __forceinline__ void ld_dh(const Lvl &L, int32_t b, int32_t i, float (&d)[3][3]) {
     ld_h9(L.Dh, L.Dh22, (int64_t)b * L.n + i, d);
@@ -527,8 +580,7 @@ __device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, co
                                           float (&acc)[3]) {
     constexpr int U = 4;
     const float *Ab = L.A + (int64_t)b * L.sell_nb * kB3;
-    const uint4 *Hb = L.Ah + (int64_t)b * L.sell_nb;
-    const uint16_t *H22 = L.Ah22 + (int64_t)b * L.sell_nb;
+    const int64_t hb = (int64_t)b * L.sell_nb;  // system b's first block of the sweep copy (ld_a9 index)
     const bool half = L.Ah != nullptr;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = L.sell_off[s], w = (L.sell_off[s + 1] - o) >> 6;
@@ -540,7 +592,7 @@ __device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, co
         for (int u = 0; u < U; ++u) j[u] = L.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
         if (half) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) ld_h9(Hb, H22, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, a[u]);
+            for (int u = 0; u < U; ++u) ld_a9(L.Ah, L.Ah22, hb + o + min(t0 + u, w - 1) * kSlice + l, a[u]);
         } else {
 #pragma unroll
             for (int u = 0; u < U; ++u) ldm<3>(Ab, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, a[u]);
@@ -1224,10 +1276,10 @@ void amg_ensure(mof_mesh *m, int32_t B) {
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
-            if (l + 1 < G.lv.size()) {  // bf16 sweep copy (the coarsest stays fp32)
-                D.Ah.alloc((size_t)4 * D.sell_nb * B);
+            if (l + 1 < G.lv.size()) {  // sweep copy, st_a9 (the coarsest stays fp32)
+                D.Ah.alloc(kAhWords * D.sell_nb * B);
                 D.Ah.zero(s);
-                D.Ah22.alloc((size_t)D.sell_nb * B);
+                D.Ah22.alloc(kAh22Words * D.sell_nb * B);
                 D.Ah22.zero(s);
             }
             D.Dh.alloc((size_t)4 * n * B);

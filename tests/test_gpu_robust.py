@@ -154,9 +154,11 @@ def test_symmetric_reads_match_spsolve(precond, monkeypatch):
         out[sym] = (V, st["iterations"])
         m.close()
     assert abs(out["0"][1] - out["1"][1]) <= 0.02 * out["0"][1]
-    # (the multigrid cycle's bf16 output z makes the two paths' iterates part
-    # a little more than block Jacobi's: 1.7e-8 relative)
-    assert np.abs(out["0"][0] - out["1"][0]).max() < 1e-7 * np.abs(out["0"][0]).max()
+    # (both iterates meet the 1e-8 relative residual; the multigrid cycle's
+    # bf16 z and int8 coarse sweep copy make them part a little more than
+    # block Jacobi's: 1.7e-7 relative on this mesh, inside the solve's own
+    # tolerance times the operator's condition)
+    assert np.abs(out["0"][0] - out["1"][0]).max() < 5e-7 * np.abs(out["0"][0]).max()
 
 
 @pytest.mark.parametrize("same_I2", [True, False])

@@ -19,6 +19,10 @@ mixed solve -- for aggregation-multigrid variants:
               with the system's own A (per timestep)
   sa2=X       the same with lambda*a2 only (a per-mesh, timestep-free P)
   w2          two coarse-grid visits per level-1 cycle (W-cycle at level 1)
+  q1=F        the sweeps at levels >= 1 on a stored copy of the operator: 1 bf16,
+              2 int8 + one scale per block, 3 fp8 e4m3 + one scale per block,
+              4 int8 + one scale per row
+  q0=F        the same for the level-0 sweeps (the PCG operator stays exact)
 
 The oracle is test infrastructure; this script is a design tool, never part
 of the product path.
@@ -241,17 +245,52 @@ def build(A, a2m, e, opts):
     return levels
 
 
+def quantize(A, bs, fmt):
+    """The sweep copy of a coarse operator in a storage format (emulated)."""
+    Ab = A.tobsr(blocksize=(bs, bs)).copy()
+    d = Ab.data.astype(np.float64)
+    if fmt == 1:  # bf16 (round to nearest even on the fp32 bits)
+        u = d.astype(np.float32).view(np.uint32).astype(np.uint64)
+        u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+        d = u.astype(np.uint32).view(np.float32).astype(np.float64)
+    elif fmt == 2:  # int8 with one scale per block
+        m = np.abs(d).max(axis=(1, 2), keepdims=True)
+        sc = np.where(m > 0, m / 127.0, 1.0)
+        d = np.round(d / sc) * sc
+    elif fmt == 3:  # fp8 e4m3 with one scale per block (3 mantissa bits)
+        m = np.abs(d).max(axis=(1, 2), keepdims=True)
+        sc = np.where(m > 0, m / 448.0, 1.0)
+        v = d / sc
+        ex = np.floor(np.log2(np.maximum(np.abs(v), 2.0 ** -6)))
+        q = 2.0 ** (ex - 3)
+        d = np.round(v / q) * q * sc
+    elif fmt == 4:  # int8 with one scale per row block (row of blocks)
+        rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
+        m = np.zeros(Ab.shape[0] // bs)
+        np.maximum.at(m, rows, np.abs(d).max(axis=(1, 2)))
+        sc = np.where(m > 0, m / 127.0, 1.0)[rows][:, None, None]
+        d = np.round(d / sc) * sc
+    Ab.data = d
+    return Ab.tocsr()
+
+
 def vcycle(levels, l, b, opts):
     L = levels[l]
     if hasattr(L, "coarse"):
         return L.coarse @ b
+    Aw = L.A
+    qf = opts.get("q1") if l >= 1 else opts.get("q0")
+    if qf:
+        if not hasattr(L, "Aq"):
+            L.Aq = quantize(L.A, L.bs, int(qf))
+        Aw = L.Aq
     x = L.om * bsr_apply(L.Dinv, b, L.bs)
     cyc = 2 if (opts.get("w2") and l == 1) else 1
     for _ in range(cyc):
-        r = b - L.A @ x
+        r = b - Aw @ x
         y = vcycle(levels, l + 1, L.P.T @ r, opts)
         x = x + L.P @ y
-        x = x + L.om * bsr_apply(L.Dinv, b - L.A @ x, L.bs)
+        x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
     return x
 
 
@@ -268,6 +307,7 @@ def pcg(A, f, M, tol=1e-4, maxit=2000):
         x += a * p
         r -= a * q
         if np.linalg.norm(r) <= tol * nf:
+            pcg.rho = (np.linalg.norm(r) / nf) ** (1.0 / it)
             return it
         z = M(r)
         rz2 = r @ z
@@ -303,8 +343,8 @@ def main():
         blk = [round(lv.A.nnz / lv.bs ** 2 / (lv.A.shape[0] / lv.bs), 1) for lv in levels]
         pb = [round(lv.p_blocks, 2) for lv in levels if hasattr(lv, "p_blocks")]
         gal = [getattr(lv, "gal_terms", 0) for lv in levels]
-        print("%s %-24s its(1e-4) %4d  levels %s  op complexity %.2f  blocks/row %s  P blocks/row %s  "
-              "Galerkin terms %s" % (cfg, spec, its, sizes, nnz / A.nnz, blk, pb, gal), flush=True)
+        print("%s %-24s its(1e-4) %4d  rho %.4f  levels %s  op complexity %.2f  blocks/row %s  P blocks/row %s  "
+              "Galerkin terms %s" % (cfg, spec, its, pcg.rho, sizes, nnz / A.nnz, blk, pb, gal), flush=True)
 
 
 if __name__ == "__main__":
