@@ -181,6 +181,13 @@ __global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__rest
     const float4 v = A[q];
     H[q] = make_uint2(bf16_bits(v.x) | (bf16_bits(v.y) << 16), bf16_bits(v.z) | (bf16_bits(v.w) << 16));
 }
+// A32 -> the level-0 sweep copy (h0_st)
+__global__ __launch_bounds__(kWG) void k_to_h0(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
+    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (q >= n) return;
+    const float4 v = A[q];
+    h0_st(H, q, v.x, v.y, v.z, v.w);
+}
 
 // Block (I, J) at coarse SELL position pos of A_{l+1} = Q^T A_l Q for system
 // b, summed over its gather list in list order; the diagonal block also gets
@@ -224,9 +231,8 @@ __device__ __forceinline__ void galerkin_block(
                     // of the fp32 A: 5.35 vs 6.78 ms per 256 systems, same
                     // iteration counts) -- the coarse operator is then the
                     // Galerkin product of the operator the smoother sweeps
-                    const uint2 t = Afh[(int64_t)b * f_sell_nb + fq];
-                    a[u][0][0] = bf16_lo(t.x); a[u][0][1] = bf16_hi(t.x);
-                    a[u][1][0] = bf16_lo(t.y); a[u][1][1] = bf16_hi(t.y);
+                    h0_dec(h0_ld(Afh, (int64_t)b * f_sell_nb + fq), a[u][0][0], a[u][0][1], a[u][1][0],
+                           a[u][1][1]);
                 } else {
                     ldm<BSF>(A, fq, a[u]);
                 }
@@ -368,9 +374,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
             for (int t = 0; t < kGalNS; ++t) {
                 const int64_t bb = min(b0 + t, B - 1);
                 if (Afh) {
-                    const uint2 h = Afh[bb * f_sell_nb + fq];
-                    a[u][t][0] = bf16_lo(h.x); a[u][t][1] = bf16_hi(h.x);
-                    a[u][t][2] = bf16_lo(h.y); a[u][t][3] = bf16_hi(h.y);
+                    h0_dec(h0_ld(Afh, bb * f_sell_nb + fq), a[u][t][0], a[u][t][1], a[u][t][2], a[u][t][3]);
                 } else {
                     const float4 v = reinterpret_cast<const float4 *>(Af)[bb * f_sell_nb + fq];
                     a[u][t][0] = v.x; a[u][t][1] = v.y; a[u][t][2] = v.z; a[u][t][3] = v.w;
@@ -1270,7 +1274,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.x.alloc(2 * n * B);
             if (G.xm == 2) D.y.alloc(2 * n * B);
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
-            G.A0h.alloc(2 * (size_t)m->pat.sell_nb() * B);
+            G.A0h.alloc((size_t)(kH0HalfWords * m->pat.sell_nb() * B / 2));
             G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
             G.D0h.alloc(2 * n * B);
         } else {
@@ -1325,7 +1329,7 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     const size_t L = G.lv.size();
     if (!G.bf16_fresh) {
         const int64_t nb0 = m->pat.sell_nb() * B;
-        k_to_bf16<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
+        k_to_h0<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
             nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
         const int64_t nd0 = (int64_t)m->N * B;
         k_to_bf16<<<dim3((unsigned)((nd0 + kWG - 1) / kWG)), kWG, 0, s>>>(

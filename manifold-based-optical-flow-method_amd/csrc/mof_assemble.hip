@@ -395,7 +395,10 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
         // a decomposed part's ghost rows: identity rows, no coupling (the
         // smoother and coarse levels see the owned rows' Dirichlet problem)
         const bool g = i >= nown || vcol[p] >= nown;
-        Ah[q] = g ? bf16x4(diag ? 1.f : 0.f, 0.f, 0.f, diag ? 1.f : 0.f) : bf16x4(Av[0], Av[1], Av[2], Av[3]);
+        if (g)
+            h0_st(Ah, q, diag ? 1.f : 0.f, 0.f, 0.f, diag ? 1.f : 0.f);
+        else
+            h0_st(Ah, q, Av[0], Av[1], Av[2], Av[3]);
     }
     if (!diag) return;
     // f_i in fp64, in the reference's triangle order
@@ -479,7 +482,10 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
         reinterpret_cast<float4 *>(A)[qq] = make_float4(Av[0], Av[1], Av[2], Av[3]);
         if (Ah) {
             const bool g = i >= nown || sell_col[pos] >= nown;
-            Ah[qq] = g ? bf16x4(z == 0 ? 1.f : 0.f, 0.f, 0.f, z == 0 ? 1.f : 0.f) : bf16x4(Av[0], Av[1], Av[2], Av[3]);
+            if (g)
+                h0_st(Ah, qq, z == 0 ? 1.f : 0.f, 0.f, 0.f, z == 0 ? 1.f : 0.f);
+            else
+                h0_st(Ah, qq, Av[0], Av[1], Av[2], Av[3]);
         }
         if (z != 0) continue;
         double inv[4];

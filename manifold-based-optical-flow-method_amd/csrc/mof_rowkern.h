@@ -58,6 +58,76 @@ __device__ __forceinline__ uint2 bf16x4(float a, float b, float c, float d) {
     return make_uint2(bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16));
 }
 
+// The level-0 sweep copy of A (k_res0, k_post0, the smoother's D from the
+// diagonal block, the level-0 Galerkin product). MOF_L0_I8 = 1: 6 B per 2x2
+// block -- 4 signed int8 codes and one bf16 scale (max |a| / 127) -- in
+// records of 64 consecutive SELL positions (one slot column of a slice: 256
+// B of codes, then 128 B of scales), so a wave's loads stay contiguous; a
+// zero-filled record reads as zero blocks. A block and its transposed twin
+// hold the same entries, hence the same scale and codes. 0: 4 bf16 entries
+// (8 B). Both are handled as a raw uint2 (bf16: the entries; int8: codes,
+// scale bits) until h0_dec. Measured (same box, B = 512,
+// profiles/r02_ab/l0_i8_*): the sweeps move fewer bytes but issue more
+// (two loads and a record address per slot, the decode): k_post0 934 ->
+// 1206 us, k_res0 959 -> 1045 us, the assembly 9.9 -> 11.0 ms; C3 3390 ->
+// 3197 timesteps/s (-5.7 %), C2 mixed -6 %, R3 +2.5 %. Off by default.
+#ifndef MOF_L0_I8
+#define MOF_L0_I8 0
+#endif
+constexpr bool kL0I8 = MOF_L0_I8 != 0;
+// uint32 words of the level-0 copy per block x 2 (8 B: 4, 6 B: 3)
+constexpr int64_t kH0HalfWords = kL0I8 ? 3 : 4;
+
+__device__ __forceinline__ uint2 h0_ld(const uint2 *H, int64_t q) {
+    if constexpr (!kL0I8) {
+        return H[q];
+    } else {
+        const char *rec = reinterpret_cast<const char *>(H) + (q >> 6) * 384;
+        const int l = (int)(q & 63);
+        return make_uint2(reinterpret_cast<const uint32_t *>(rec)[l],
+                          (uint32_t)reinterpret_cast<const uint16_t *>(rec + 256)[l]);
+    }
+}
+__device__ __forceinline__ void h0_st(uint2 *H, int64_t q, float a, float b, float c, float d) {
+    if constexpr (!kL0I8) {
+        H[q] = bf16x4(a, b, c, d);
+    } else {
+        const float m = fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
+        const uint32_t sb = bf16_bits(m / 127.f);
+        const float sc = bf16_lo(sb);
+        const float v[4] = {a, b, c, d};
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float t = sc > 0.f ? fminf(fmaxf(rintf(v[e] / sc), -127.f), 127.f) : 0.f;
+            w |= ((uint32_t)(int32_t)t & 0xffu) << (8 * e);
+        }
+        char *rec = reinterpret_cast<char *>(H) + (q >> 6) * 384;
+        const int l = (int)(q & 63);
+        reinterpret_cast<uint32_t *>(rec)[l] = w;
+        reinterpret_cast<uint16_t *>(rec + 256)[l] = (uint16_t)sb;
+    }
+}
+// the transposed block (swap the off-diagonal entries)
+__device__ __forceinline__ uint2 h0_tr(uint2 h) {
+    if constexpr (!kL0I8)
+        return make_uint2((h.x & 0xFFFFu) | (h.y << 16), (h.x >> 16) | (h.y & 0xFFFF0000u));
+    else
+        return make_uint2((h.x & 0xFF0000FFu) | ((h.x >> 8) & 0x0000FF00u) | ((h.x << 8) & 0x00FF0000u), h.y);
+}
+// entries a00, a01, a10, a11
+__device__ __forceinline__ void h0_dec(uint2 h, float &a00, float &a01, float &a10, float &a11) {
+    if constexpr (!kL0I8) {
+        a00 = bf16_lo(h.x); a01 = bf16_hi(h.x); a10 = bf16_lo(h.y); a11 = bf16_hi(h.y);
+    } else {
+        const float sc = bf16_lo(h.y);
+        a00 = (float)(int32_t)(int8_t)(h.x & 0xffu) * sc;
+        a01 = (float)(int32_t)(int8_t)((h.x >> 8) & 0xffu) * sc;
+        a10 = (float)(int32_t)(int8_t)((h.x >> 16) & 0xffu) * sc;
+        a11 = (float)(int32_t)(int8_t)(h.x >> 24) * sc;
+    }
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -291,7 +361,7 @@ struct MatH {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;
     const int32_t *sell_mir;  // mirror table (MOF_SYM_A)
-    const uint2 *A;  // [B][sell_nb] 4 bf16 per block
+    const uint2 *A;  // the level-0 sweep copy (h0_ld), [B][sell_nb] blocks
 };
 
 // spmv_row on the bf16 blocks; the operand of column j comes from
@@ -300,7 +370,7 @@ struct MatH {
 template <bool sym, int U = MOF_SWEEP_U, typename XL>
 __device__ __forceinline__ void spmv_row_hx_t(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
                                               float &y1, uint2 *diag) {
-    const uint2 *A = mt.A + (int64_t)b * mt.sell_nb;
+    const uint2 *A = mt.A;  // h0_ld index: system b's positions from b * sell_nb
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
     const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
@@ -316,23 +386,23 @@ __device__ __forceinline__ void spmv_row_hx_t(const MatH &mt, int32_t b, int32_t
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            blk[u] = A[sym ? mir_pos(mr[u], (int64_t)o + l) : (int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+            blk[u] = h0_ld(A, (int64_t)b * mt.sell_nb +
+                                  (sym ? mir_pos(mr[u], (int64_t)o + l) : (int64_t)o + min(t0 + u, w - 1) * kSlice + l));
         if (diag && t0 == 0) *diag = blk[0];
 #pragma unroll
         for (int u = 0; u < U; ++u) xj[u] = xload(j[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             bool on = t0 + u < w;
-            uint32_t bx = blk[u].x, by = blk[u].y;
+            uint2 h = blk[u];
             if constexpr (sym) {
                 on = on && mr[u] >= 0;
-                const bool tr = (mr[u] & kMirT) != 0;  // transpose: swap the off-diagonal halves
-                const uint32_t tx = (bx & 0xFFFFu) | (by << 16), ty = (bx >> 16) | (by & 0xFFFF0000u);
-                bx = tr ? tx : bx;
-                by = tr ? ty : by;
+                if (mr[u] & kMirT) h = h0_tr(h);  // transpose: swap the off-diagonal entries
             }
-            a0 += on ? bf16_lo(bx) * xj[u].x + bf16_hi(bx) * xj[u].y : 0.f;
-            a1 += on ? bf16_lo(by) * xj[u].x + bf16_hi(by) * xj[u].y : 0.f;
+            float e00, e01, e10, e11;
+            h0_dec(h, e00, e01, e10, e11);
+            a0 += on ? e00 * xj[u].x + e01 * xj[u].y : 0.f;
+            a1 += on ? e10 * xj[u].x + e11 * xj[u].y : 0.f;
         }
     }
     y0 = a0;
@@ -393,14 +463,15 @@ __device__ __forceinline__ float2 bf16_mat2(uint2 d, float v0, float v1) {
 #define MOF_DINV_FROM_A 1
 #endif
 __device__ __forceinline__ float2 bf16_diag_solve(uint2 a, float v0, float v1) {
-    const float a00 = bf16_lo(a.x), a01 = bf16_hi(a.x), a10 = bf16_lo(a.y), a11 = bf16_hi(a.y);
+    float a00, a01, a10, a11;
+    h0_dec(a, a00, a01, a10, a11);
     const float id = 1.f / (a00 * a11 - a01 * a10);
     return make_float2((a11 * v0 - a01 * v1) * id, (a00 * v1 - a10 * v0) * id);
 }
 // slot 0 (the diagonal block) of row i of system b in a SELL-64 bf16 operator
 __device__ __forceinline__ uint2 bf16_diag_block(const uint2 *A, int64_t sell_nb, const int32_t *sell_off,
                                                  int32_t b, int32_t i) {
-    return A[(int64_t)b * sell_nb + sell_off[i >> 6] + (i & 63)];
+    return h0_ld(A, (int64_t)b * sell_nb + sell_off[i >> 6] + (i & 63));
 }
 
 }  // namespace
