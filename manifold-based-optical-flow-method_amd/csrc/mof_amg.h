@@ -89,8 +89,8 @@ struct AmgDevLevel {
     DevArray<float> A;           // [B][sell_nb][12] (level >= 1)
     DevArray<uint32_t> Dh;       // [B][n][4] 3x3 D^-1 bf16 entries 0..7 (level >= 1)
     DevArray<uint16_t> Dh22;     // [B][n] entry (2,2)
-    DevArray<uint32_t> Ah;       // [B][sell_nb][4] bf16 A entries 0..7 for the sweeps (not the coarsest)
-    DevArray<uint16_t> Ah22;     // [B][sell_nb] bf16 entry (2,2)
+    DevArray<uint32_t> Ah;       // sweep copy (not the coarsest), st_a9: [B][sell_nb][2] int8 codes 0..7
+    DevArray<uint16_t> Ah22;     // [B][sell_nb][2] code 8 | bf16 scale (MOF_COARSE_I8=0: [4] / [1] bf16)
     DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x [B][n][2], r bf16 pairs [B][n]
                                  // r is stored in member order of the next level
 };

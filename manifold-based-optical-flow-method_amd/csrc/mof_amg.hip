@@ -24,8 +24,9 @@
 // bf16 copies of the inner solver's SELL A and 2x2 D^-1, written by the
 // assembly (k_assemble_mixed), in the PCG row-kernel layout (XCD-aware,
 // batched loads); coarse levels keep fp32 3x3 blocks (12 floats, rows padded
-// to 4) for the Galerkin products and bf16 copies (18 B per block) for the
-// sweeps, vectors as float4. All sums run in a fixed order: the cycle is
+// to 4) for the Galerkin products and int8 copies (9 codes + a bf16 scale,
+// 12 B per block, st_a9; bf16 with MOF_COARSE_I8=0) for the sweeps, vectors
+// as float4. All sums run in a fixed order: the cycle is
 // deterministic and independent of B.
 #include <algorithm>
 #include <cstdio>
