@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-frac", type=float, default=1.0 / 4,
                     help="fraction of the triangle loop the CPU baseline times")
+    ap.add_argument("--cpu-timesteps-per-core", type=int, default=2,
+                    help="CPU baseline: timesteps per pool process (SURVEY.md 8(d): 2 per core)")
     ap.add_argument("--lambda_", type=float, default=0.01)
     ap.add_argument("--fixed-timesteps", type=int, default=0,
                     help="strong scaling: one step = this many timesteps split over the ranks")
@@ -133,36 +135,39 @@ def step_traffic(key, value):
             "source": "profiles/pmc_traffic.json[%s] (PMC run of %d timesteps)" % (key, run["timesteps"])}
 
 
-def cpu_baseline(p, t, n, a, lam, frac):
+def cpu_baseline(p, t, n, a, lam, frac, per_core=2):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
-    host on a bounded sample: Pool(C) runs C timesteps; each assembles the
-    first `frac` of the triangles with the reference's scalar loop and then
-    runs spsolve on the full-size system. Per-timestep time is extrapolated
-    linearly in the triangle count."""
+    host on a bounded sample: Pool(C) runs per_core * C timesteps (SURVEY.md
+    §8(d): 2 C); each assembles the first `frac` of the triangles with the
+    reference's scalar loop and then runs spsolve on the full-size system.
+    Every core runs per_core timesteps back to back, so the pool's wall
+    misses per_core x the unsampled part of the loop; per-timestep loop time
+    is extrapolated linearly in the triangle count."""
     import oracle
     import reference_clone as clone
     C = clone.default_cores()
+    K = per_core * C
     a2, gw, e, iw = oracle.geometry(p, n, t, a)
     a2l = clone.as_lil(a2)
-    T = C + 1
+    T = K + 1
     from mofhip import synth
     I = synth.travelling_wave(p, T)
     tk = list(range(T))
     M = len(t)
     S = max(1, int(M * frac))
-    res, wall = clone.pool_timesteps(range(C), a2l, gw, e, iw, t, tk, a, lam, I, I, C,
+    res, wall = clone.pool_timesteps(range(K), a2l, gw, e, iw, t, tk, a, lam, I, I, C,
                                      sample_tris=S)
     loop = float(np.mean([r[1] for r in res]))
     solve = float(np.mean([r[2] for r in res]))
-    full_wall = wall + loop * (M / S - 1.0)
-    value = C / full_wall
+    full_wall = wall + per_core * loop * (M / S - 1.0)
+    value = K / full_wall
     return {
         "value": value, "unit": "timesteps/s", "cores": C, "kind": "port",
         "sample": ("Pool(%d) x %d timesteps of the reference algorithm (lil scalar assembly, csr, "
                    "spsolve; oracle/reference_clone.py, calibrated vs the reference) on the %d-vertex "
                    "mesh; triangle loop timed on %d of %d triangles (%.1f s/step measured, "
                    "extrapolated x%.0f), spsolve on the full system (%.1f s/step); pool wall %.1f s"
-                   % (C, C, len(p), S, M, loop, M / S, solve, wall)),
+                   % (C, K, len(p), S, M, loop, M / S, solve, wall)),
     }
 
 
@@ -356,7 +361,7 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and not dry:
-        cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac)
+        cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core)
 
     if rank == 0:
         line = {
