@@ -1087,6 +1087,129 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 
 // Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
 // of the row block's record). PCG row layout, XCD-aware grid.
+// k_res0 with NS systems per thread sharing the row's column / mirror loads
+// (MOF_RES0_NS): grid over (row block, system group of NS) in the XCD order.
+#ifndef MOF_RES0_NS
+#define MOF_RES0_NS 2
+#endif
+constexpr int kRes0NS = MOF_RES0_NS;
+template <int NS>
+__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
+                                                 const float *__restrict__ rv, const float *__restrict__ xv,
+                                                 const int32_t *__restrict__ apos,
+                                                 const int32_t *__restrict__ sysi, float *__restrict__ r1) {
+#pragma clang fp contract(off)
+    int32_t rb, bq;
+    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpSmooth > NS ? kGrpSmooth / NS : 1)) return;
+    int32_t bs[NS];
+    bool act[NS];
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const int32_t b = bq * NS + t;
+        bs[t] = min(b, B - 1);
+        act[t] = b < B && !retired(sysi, b);
+        any |= act[t];
+    }
+    if (!any) return;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= N) break;
+        float y[NS][2];
+        auto xl = [&](int t, int32_t j) { return ld_x0(xv, (int64_t)bs[t] * N + j); };
+        if (MOF_SYM_A && mat.sell_mir)
+            spmv_row_hx_ns<(bool)MOF_SYM_A, NS>(mat, bs, i, xl, y);
+        else
+            spmv_row_hx_ns<false, NS>(mat, bs, i, xl, y);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            if (!act[t]) continue;
+            const int64_t vb = (int64_t)bs[t] * N;
+            const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
+            reinterpret_cast<uint32_t *>(r1)[vb + (apos ? apos[i] : i)] =
+                bf16_bits(ri.x - y[t][0]) | (bf16_bits(ri.y - y[t][1]) << 16);
+        }
+    }
+}
+
+// k_post0 with NS systems per thread sharing the row's column / mirror loads
+// (MOF_POST0_NS), same per-system arithmetic and partials as k_post0.
+#ifndef MOF_POST0_NS
+#define MOF_POST0_NS 1
+#endif
+constexpr int kPost0NS = MOF_POST0_NS;
+template <int XM, bool ZH, int NS>
+__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
+                                                  const uint2 *__restrict__ Dh,
+                                                  const float *__restrict__ rv,
+                                                  const float *__restrict__ xv, float omega,
+                                                  const int32_t *__restrict__ sysi,
+                                                  float *__restrict__ zv, double *__restrict__ part,
+                                                  RedArgs rd) {
+#pragma clang fp contract(off)
+    __shared__ double lds[8 * NS];
+    int32_t rb, bq;
+    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpSmooth > NS ? kGrpSmooth / NS : 1)) return;
+    int32_t bs[NS];
+    bool act[NS];
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const int32_t b = bq * NS + t;
+        bs[t] = min(b, B - 1);
+        act[t] = b < B && !retired(sysi, b);
+        any |= act[t];
+    }
+    if (!any) return;
+    double rz[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) rz[t] = 0.0;
+#pragma unroll
+    for (int g = 0; g < kRows; ++g) {
+        const int32_t i = rb * kRowsPerWG + g * kWG + threadIdx.x;
+        if (i >= N) break;
+        float y[NS][2];
+        uint2 dg[NS];  // the rows' diagonal blocks (slot 0), kept from the SpMV
+        auto xl = [&](int t, int32_t j) {
+            const int64_t vj = (int64_t)bs[t] * N + j;
+            if constexpr (XM == 2)
+                return reinterpret_cast<const float2 *>(xv)[vj];
+            else
+                return ld_x0(xv, vj);
+        };
+        if (MOF_SYM_A && mat.sell_mir)
+            spmv_row_hx_ns<(bool)MOF_SYM_A, NS>(mat, bs, i, xl, y, dg);
+        else
+            spmv_row_hx_ns<false, NS>(mat, bs, i, xl, y, dg);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            const int64_t vb = (int64_t)bs[t] * N;
+            const float2 xi = xl(t, i);
+            const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
+            const float2 ds = MOF_DINV_FROM_A ? bf16_diag_solve(dg[t], ri.x - y[t][0], ri.y - y[t][1])
+                                              : bf16_mat2(Dh[vb + i], ri.x - y[t][0], ri.y - y[t][1]);
+            float z0 = xi.x + omega * ds.x;
+            float z1 = xi.y + omega * ds.y;
+            if constexpr (ZH) {
+                const uint32_t h = bf16_bits(z0) | (bf16_bits(z1) << 16);
+                if (act[t]) reinterpret_cast<uint32_t *>(zv)[vb + i] = h;
+                z0 = bf16_lo(h);
+                z1 = bf16_hi(h);
+            } else {
+                if (act[t]) reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
+            }
+            if (i < rd.nown) rz[t] += (double)ri.x * z0 + (double)ri.y * z1;
+        }
+    }
+    block_sum<NS>(rz, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+            if (act[t]) part[2 * (((int64_t)rd.part * B + bs[t]) * rd.nmax + rb)] = rz[t];
+    }
+}
+
 template <int XM, bool ZH>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                const uint2 *__restrict__ Dh,
@@ -1132,6 +1255,18 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nb
     double v[1] = {rz};
     block_sum<1>(v, lds);
     if (threadIdx.x == 0) part[2 * (((int64_t)rd.part * B + b) * rd.nmax + rb)] = v[0];
+}
+
+// k_post0 (one system per thread) or k_post0_ns (kPost0NS systems)
+template <int XM, bool ZH, typename... Args>
+void launch_post0(dim3 gx, int32_t nblk, int32_t B, hipStream_t s, int32_t n, int32_t nblk_, int32_t B_,
+                  Args... args) {
+    if constexpr (kPost0NS > 1) {
+        const dim3 g(xcd_grid(nblk, (B + kPost0NS - 1) / kPost0NS, kGrpSmooth > kPost0NS ? kGrpSmooth / kPost0NS : 1));
+        k_post0_ns<XM, ZH, kPost0NS><<<g, kWG, 0, s>>>(n, nblk_, B_, args...);
+    } else {
+        k_post0<XM, ZH><<<gx, kWG, 0, s>>>(n, nblk_, B_, args...);
+    }
 }
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
@@ -1416,8 +1551,15 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = 0; l < S; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
-            k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
-                                      MOF_R1_NATURAL || G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
+            if (kRes0NS > 1)
+                k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (B + kRes0NS - 1) / kRes0NS,
+                                                   kGrpSmooth > kRes0NS ? kGrpSmooth / kRes0NS : 1)),
+                                     kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
+                                                  MOF_R1_NATURAL || G.lv[0].smoothed ? nullptr : v[0].apos, sysi,
+                                                  v[0].r);
+            else
+                k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
+                                          MOF_R1_NATURAL || G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
             if (G.lv[0].smoothed) {
                 k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNS - 1) / kNS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
@@ -1452,10 +1594,10 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                 else
                     k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
-                    k_post0<2, true><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot,
+                    launch_post0<2, true>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot,
                                                         rd);
                 else
-                    k_post0<2, false><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0,
+                    launch_post0<2, false>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0,
                                                          part_slot, rd);
             } else {
                 if (G.lv[0].smoothed)
@@ -1463,10 +1605,10 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                 else
                     k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
-                    k_post0<1, true><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot,
+                    launch_post0<1, true>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot,
                                                         rd);
                 else
-                    k_post0<1, false><<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0,
+                    launch_post0<1, false>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0,
                                                          part_slot, rd);
             }
         } else {

@@ -409,6 +409,73 @@ __device__ __forceinline__ void spmv_row_hx_t(const MatH &mt, int32_t b, int32_t
     y1 = a1;
 }
 
+// spmv_row_hx_t for NS systems of one row per thread: the column and mirror
+// loads (shared by all systems) are issued once for the NS systems. No fp
+// contraction, so every system slot rounds alike (a system's bits must not
+// depend on its slot, i.e. on the batch split). xload(t, j): system t's
+// operand of column j.
+template <bool sym, int NS, int U = MOF_SWEEP_U, typename XL>
+__device__ __forceinline__ void spmv_row_hx_ns(const MatH &mt, const int32_t (&bs)[NS], int32_t i, XL &&xload,
+                                               float (&y)[NS][2], uint2 *diag = nullptr) {
+#pragma clang fp contract(off)
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = mt.sell_off[s];
+    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    float acc[NS][2];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.f;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U], mr[U];
+        int64_t pos[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pos[u] = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
+            j[u] = mt.sell_col[pos[u]];
+            if constexpr (sym) mr[u] = mt.sell_mir[pos[u]];
+        }
+        if constexpr (sym) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) pos[u] = mir_pos(mr[u], (int64_t)o + l);
+        }
+        uint2 blk[NS][U];
+        float2 xj[NS][U];
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int u = 0; u < U; ++u) blk[t][u] = h0_ld(mt.A, (int64_t)bs[t] * mt.sell_nb + pos[u]);
+        if (diag && t0 == 0) {  // slot 0: the diagonal block, never mirrored
+#pragma unroll
+            for (int t = 0; t < NS; ++t) diag[t] = blk[t][0];
+        }
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int u = 0; u < U; ++u) xj[t][u] = xload(t, j[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            bool on = t0 + u < w;
+            bool tr = false;
+            if constexpr (sym) {
+                on = on && mr[u] >= 0;
+                tr = (mr[u] & kMirT) != 0;
+            }
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                const uint2 h = tr ? h0_tr(blk[t][u]) : blk[t][u];
+                float e00, e01, e10, e11;
+                h0_dec(h, e00, e01, e10, e11);
+                acc[t][0] += on ? e00 * xj[t][u].x + e01 * xj[t][u].y : 0.f;
+                acc[t][1] += on ? e10 * xj[t][u].x + e11 * xj[t][u].y : 0.f;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        y[t][0] = acc[t][0];
+        y[t][1] = acc[t][1];
+    }
+}
+
 template <typename XL>
 __device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
                                             float &y1, uint2 *diag = nullptr) {
