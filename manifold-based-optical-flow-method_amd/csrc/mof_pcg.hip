@@ -643,6 +643,134 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     if (threadIdx.x == 0) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, b, rb)] = v[0];
 }
 
+// The fp32 SpMV with two systems per thread (MOF_SPMV_NS = 2): each slot's
+// column index and mirror entry are loaded once for the pair (spmv_row_ns).
+// Both systems' products are always formed (a retired partner's are
+// discarded) with no fp contraction, so a system's bits do not depend on its
+// partner or slot; the per-system bookkeeping is pcg_spmv_body's.
+// Measured (same box, C3 B = 512, profiles/r02_ab/spmvns_*): the main launch
+// takes the same time (1624.8 vs 1625.5 us: bound by its bytes, not by the
+// index loads), the first-iteration one 1555 vs 1625 us; C3, C2 and R3 within
+// noise. Off by default.
+#ifndef MOF_SPMV_NS
+#define MOF_SPMV_NS 1
+#endif
+constexpr int kSpmvNS = MOF_SPMV_NS;
+template <bool FIRST, bool ZH>
+__device__ __forceinline__ void pcg_spmv_pair(const PcgArgs<float> &a, int32_t it, int32_t flags) {
+#pragma clang fp contract(off)
+    static_assert(MOF_PRS, "the paired SpMV reads the pre-reduced scalars");
+    constexpr int NS = 2, NT = kSpmvWG, RPT = kRowsPerWG / NT;
+    constexpr int U = MOF_SPMV_U >= 8 ? MOF_SPMV_U / 2 : MOF_SPMV_U;
+    __shared__ double lds[NS * (NT / 64)];
+    int32_t rb, bq;
+    if (!xcd_map(a.nblk, (a.B + NS - 1) / NS, rb, bq, kGrpSpmv > NS ? kGrpSpmv / NS : 1)) return;
+    const bool force = flags & kForce;
+    const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;  // p.q slot stride
+    int32_t bs[NS];
+    bool work[NS];
+    float alpha_prev[NS], beta[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const int32_t b = bq * NS + t;
+        bs[t] = min(b, a.B - 1);
+        work[t] = false;
+        alpha_prev[t] = 0.f;
+        beta[t] = 0.f;
+        if (b >= a.B) continue;
+        const int32_t conv = a.sysi[b * kSysStride + SI_CONV];
+        if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || (conv >= 0 && conv != it))) continue;
+        const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
+        const double cur[2] = {c[0], c[1]};
+        double old[2] = {1.0, 1.0};
+        if (!FIRST) {
+            const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
+            old[0] = o[0];
+            old[1] = o[1];
+            if (!force) alpha_prev[t] = (float)(old[0] / *sc_pq(a.sc, a.B, (it + 1) & 1, b));
+        }
+        if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {  // converged: finish x, retire
+            if (!FIRST) {
+                const int64_t vb = (int64_t)b * a.N;
+#pragma unroll
+                for (int r = 0; r < RPT; ++r) {
+                    const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
+                    if (i >= a.N) break;
+                    const int64_t vi = vb + i;
+                    const float2 p0 = *reinterpret_cast<const float2 *>(a.p + 2 * vi);
+                    float2 xi = *reinterpret_cast<const float2 *>(a.x + 2 * vi);
+                    xi.x += alpha_prev[t] * p0.x;
+                    xi.y += alpha_prev[t] * p0.y;
+                    *reinterpret_cast<float2 *>(a.x + 2 * vi) = xi;
+                }
+            }
+            if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
+                a.sysi[b * kSysStride + SI_CONV] = it;
+            continue;
+        }
+        if (!force && rb == 0 && threadIdx.x == 0 && cur[1] < a.sysd[b * kSysStride + SD_BEST]) {
+            a.sysd[b * kSysStride + SD_BEST] = cur[1];
+            a.sysi[b * kSysStride + SI_BEST_IT] = it;
+        }
+        if (!FIRST) beta[t] = (float)(cur[0] / old[0]);
+        work[t] = true;
+    }
+    if (!work[0] && !work[1]) return;
+    const float *xs[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+        xs[t] = ZH ? reinterpret_cast<const float *>(reinterpret_cast<const uint32_t *>(a.z) + (int64_t)bs[t] * a.N)
+                   : a.z + 2 * (int64_t)bs[t] * a.N;
+    double pq[NS] = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
+        if (i >= a.N) break;
+        float y[NS][2];
+        if (MOF_SYM_A && a.mat.sell_mir)
+            spmv_row_ns<(bool)MOF_SYM_A, NS, U, ZH>(a.mat, bs, i, xs, y);
+        else
+            spmv_row_ns<false, NS, U, ZH>(a.mat, bs, i, xs, y);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            if (!work[t]) continue;
+            const int64_t vi = (int64_t)bs[t] * a.N + i;
+            float2 zi;
+            if constexpr (ZH) {
+                const uint32_t h = reinterpret_cast<const uint32_t *>(a.z)[vi];
+                zi = float2{bf16_lo(h), bf16_hi(h)};
+            } else {
+                zi = *reinterpret_cast<const float2 *>(a.z + 2 * vi);
+            }
+            float2 qi, pi;
+            if (FIRST) {
+                qi = float2{y[t][0], y[t][1]};
+                pi = zi;
+            } else {
+                const float2 q0 = *reinterpret_cast<const float2 *>(a.q + 2 * vi);
+                const float2 p0 = *reinterpret_cast<const float2 *>(a.p + 2 * vi);
+                qi = float2{y[t][0] + beta[t] * q0.x, y[t][1] + beta[t] * q0.y};
+                pi = float2{zi.x + beta[t] * p0.x, zi.y + beta[t] * p0.y};
+                if (!force) {
+                    float2 xi = *reinterpret_cast<const float2 *>(a.x + 2 * vi);
+                    xi.x += alpha_prev[t] * p0.x;
+                    xi.y += alpha_prev[t] * p0.y;
+                    *reinterpret_cast<float2 *>(a.x + 2 * vi) = xi;
+                }
+            }
+            *reinterpret_cast<float2 *>(a.q + 2 * vi) = qi;
+            *reinterpret_cast<float2 *>(a.p + 2 * vi) = pi;
+            if (i < a.red.nown) pq[t] += (double)pi.x * qi.x + (double)pi.y * qi.y;
+        }
+    }
+    block_sum<NS, NT>(pq, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+            if (work[t]) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, bs[t], rb)] = pq[t];
+    }
+}
+
 // the fp32 instances run at >= 5 waves per SIMD (MOF_ROW_OCC: +1 % at C3);
 // the fp64 ones keep the compiler's choice (the hint costs C2 fp64 2.7 %)
 template <typename V, bool FIRST, bool ZH = false>
@@ -654,7 +782,10 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
     __global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, FIRST, ZH>(PcgArgs<float> a,   \
                                                                                        int32_t it,          \
                                                                                        int32_t flags) {     \
-        pcg_spmv_body<float, FIRST, kSpmvWG, ZH>(a, it, flags);                                              \
+        if constexpr (kSpmvNS == 2)                                                                          \
+            pcg_spmv_pair<FIRST, ZH>(a, it, flags);                                                          \
+        else                                                                                                 \
+            pcg_spmv_body<float, FIRST, kSpmvWG, ZH>(a, it, flags);                                          \
     }
 MOF_SPMV_F32(true, false)
 MOF_SPMV_F32(false, false)
@@ -664,8 +795,18 @@ MOF_SPMV_F32(false, true)
 // workgroup size of an SpMV launch
 template <typename V>
 constexpr int spmv_wg() { return sizeof(V) == 4 ? kSpmvWG : kWG; }
+// grid of an SpMV launch over (row block, system) -- or system pairs for the
+// paired fp32 kernel -- in the XCD order its body maps
 template <typename V>
-void launch_spmv(const PcgArgs<V> &a, bool first, dim3 g, hipStream_t s, int32_t it, int32_t flags) {
+dim3 spmv_grid(const PcgArgs<V> &a) {
+    if constexpr (sizeof(V) == 4 && kSpmvNS == 2)
+        return dim3(xcd_grid(a.nblk, (a.B + 1) / 2, kGrpSpmv > 2 ? kGrpSpmv / 2 : 1));
+    else
+        return dim3(xcd_grid(a.nblk, a.B, kGrpSpmv));
+}
+template <typename V>
+void launch_spmv(const PcgArgs<V> &a, bool first, dim3, hipStream_t s, int32_t it, int32_t flags) {
+    const dim3 g = spmv_grid(a);
     if (first)
         a.zh ? k_pcg_spmv<V, true, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags)
              : k_pcg_spmv<V, true, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
@@ -1121,7 +1262,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 // separate marker packets around it
                 auto kf = it == 0 ? (a.zh ? k_pcg_spmv<V, true, true> : k_pcg_spmv<V, true, false>)
                                   : (a.zh ? k_pcg_spmv<V, false, true> : k_pcg_spmv<V, false, false>);
-                hipExtLaunchKernelGGL(kf, gx, dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0, a, it, 0);
+                hipExtLaunchKernelGGL(kf, spmv_grid(a), dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0, a, it, 0);
             } else {
                 launch_spmv(a, it == 0, gx, s, it, 0);
             }
@@ -1548,7 +1689,7 @@ double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipS
     auto launch = [&]() {
         if (precision == MOF_PREC_MIXED) {
             PcgArgs<float> a = make_args<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p);
-            k_pcg_spmv<float, false><<<gx, spmv_wg<float>(), 0, s>>>(a, 1, kForce);
+            k_pcg_spmv<float, false><<<spmv_grid(a), spmv_wg<float>(), 0, s>>>(a, 1, kForce);
         } else {
             PcgArgs<double> a = make_args<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p);
             k_pcg_spmv<double, false><<<gx, spmv_wg<double>(), 0, s>>>(a, 1, kForce);

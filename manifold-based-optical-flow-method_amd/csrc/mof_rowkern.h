@@ -230,6 +230,73 @@ __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
 #define MOF_SWEEP_U 8
 #endif
 
+// spmv_row_t for NS fp32 systems of one row per thread: each slot's column
+// index and mirror entry are loaded once for the NS systems (U slots per
+// load batch for each). No fp contraction: every system slot rounds alike.
+// x[t]: system t's operand (bf16 pairs with ZH).
+template <bool sym, int NS, int U, bool ZH>
+__device__ __forceinline__ void spmv_row_ns(const MatArgs<float> &mt, const int32_t (&bs)[NS], int32_t i,
+                                            const float *const (&x)[NS], float (&y)[NS][2]) {
+#pragma clang fp contract(off)
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = mt.sell_off[s];
+    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    float acc[NS][2];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.f;
+    for (int32_t t0 = 0; t0 < w; t0 += U) {
+        int32_t j[U], mr[U];
+        int64_t pos[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pos[u] = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
+            j[u] = mt.sell_col[pos[u]];
+            if constexpr (sym) mr[u] = mt.sell_mir[pos[u]];
+        }
+        if constexpr (sym) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) pos[u] = mir_pos(mr[u], (int64_t)o + l);
+        }
+        float blk[NS][U][4];
+        float2 xj[NS][U];
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int u = 0; u < U; ++u) ld_blk(mt.A + 4 * (int64_t)bs[t] * mt.sell_nb, pos[u], blk[t][u]);
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if constexpr (ZH) {
+                    const uint32_t h = reinterpret_cast<const uint32_t *>(x[t])[j[u]];
+                    xj[t][u] = float2{bf16_lo(h), bf16_hi(h)};
+                } else {
+                    xj[t][u] = reinterpret_cast<const float2 *>(x[t])[j[u]];
+                }
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            bool on = t0 + u < w;
+            bool tr = false;
+            if constexpr (sym) {
+                on = on && mr[u] >= 0;
+                tr = (mr[u] & kMirT) != 0;
+            }
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                const float b1 = tr ? blk[t][u][2] : blk[t][u][1], b2 = tr ? blk[t][u][1] : blk[t][u][2];
+                acc[t][0] += on ? blk[t][u][0] * xj[t][u].x + b1 * xj[t][u].y : 0.f;
+                acc[t][1] += on ? b2 * xj[t][u].x + blk[t][u][3] * xj[t][u].y : 0.f;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        y[t][0] = acc[t][0];
+        y[t][1] = acc[t][1];
+    }
+}
+
 // ZH: the operand is a bf16 pair per row (uint32 each; x points at the
 // system's first one) instead of V2
 template <bool sym, typename V, bool ZH = false>
