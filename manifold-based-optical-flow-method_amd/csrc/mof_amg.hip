@@ -1093,6 +1093,9 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 #define MOF_RES0_NS 2
 #endif
 constexpr int kRes0NS = MOF_RES0_NS;
+#ifndef MOF_RES0_U
+#define MOF_RES0_U MOF_SWEEP_U
+#endif
 template <int NS>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                  const float *__restrict__ rv, const float *__restrict__ xv,
@@ -1119,9 +1122,9 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t 
         float y[NS][2];
         auto xl = [&](int t, int32_t j) { return ld_x0(xv, (int64_t)bs[t] * N + j); };
         if (MOF_SYM_A && mat.sell_mir)
-            spmv_row_hx_ns<(bool)MOF_SYM_A, NS>(mat, bs, i, xl, y);
+            spmv_row_hx_ns<(bool)MOF_SYM_A, NS, MOF_RES0_U>(mat, bs, i, xl, y);
         else
-            spmv_row_hx_ns<false, NS>(mat, bs, i, xl, y);
+            spmv_row_hx_ns<false, NS, MOF_RES0_U>(mat, bs, i, xl, y);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
             if (!act[t]) continue;
@@ -1136,9 +1139,12 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t 
 // k_post0 with NS systems per thread sharing the row's column / mirror loads
 // (MOF_POST0_NS), same per-system arithmetic and partials as k_post0.
 #ifndef MOF_POST0_NS
-#define MOF_POST0_NS 1
+#define MOF_POST0_NS 2
 #endif
 constexpr int kPost0NS = MOF_POST0_NS;
+#ifndef MOF_POST0_U
+#define MOF_POST0_U 4
+#endif
 template <int XM, bool ZH, int NS>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                   const uint2 *__restrict__ Dh,
@@ -1179,9 +1185,9 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t
                 return ld_x0(xv, vj);
         };
         if (MOF_SYM_A && mat.sell_mir)
-            spmv_row_hx_ns<(bool)MOF_SYM_A, NS>(mat, bs, i, xl, y, dg);
+            spmv_row_hx_ns<(bool)MOF_SYM_A, NS, MOF_POST0_U>(mat, bs, i, xl, y, dg);
         else
-            spmv_row_hx_ns<false, NS>(mat, bs, i, xl, y, dg);
+            spmv_row_hx_ns<false, NS, MOF_POST0_U>(mat, bs, i, xl, y, dg);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
             const int64_t vb = (int64_t)bs[t] * N;
