@@ -78,6 +78,11 @@ def parse():
                     help="strong scaling: one step = this many timesteps split over the ranks")
     ap.add_argument("--io", default="device", choices=["device", "host"],
                     help="device: I/V resident in HBM; host: pageable numpy in and out (drop-in path)")
+    ap.add_argument("--parity-samples", type=int, default=2,
+                    help="timesteps of the last timed batch checked against the oracle + spsolve (0: none)")
+    ap.add_argument("--host-batches", type=int, default=4,
+                    help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
+                         "the device-resident region (0: none)")
     return ap.parse_args()
 
 
@@ -135,7 +140,37 @@ def step_traffic(key, value):
             "source": "profiles/pmc_traffic.json[%s] (PMC run of %d timesteps)" % (key, run["timesteps"])}
 
 
-def cpu_baseline(p, t, n, a, lam, frac, per_core=2):
+def parity_check(geom, t, a, lam, samples):
+    """Parity in the measured run: for each sampled timestep of the last timed
+    batch, the reference's system (oracle.step_system: the bit-exact
+    restatement of worker's assembly, compute_optical_flow.py:100-146) solved
+    by the reference's own solver, scipy's spsolve (:147), against the V the
+    timed GPU solve returned. The samples run in host threads (the C oracle
+    and SuperLU release the GIL)."""
+    import oracle
+    from concurrent.futures import ThreadPoolExecutor
+    from scipy.sparse.linalg import spsolve
+    a2, gw, e, iw = geom
+
+    def one(smp):
+        k, I0, I1, dt, V = smp
+        A, f = oracle.step_system(a2, gw, e, iw, t, a, lam, I0, I1, dt)
+        Vo = spsolve(A.tocsc(), f)
+        return k, float(np.abs(V - Vo).max()), float(np.abs(Vo).max()), \
+            float(np.linalg.norm(f - A @ V) / np.linalg.norm(f))
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max(1, len(samples))) as ex:
+        res = list(ex.map(one, samples))
+    return {"max_abs_err": max(r[1] for r in res), "timesteps": [r[0] for r in res],
+            "per_timestep_max_abs_err": [r[1] for r in res], "max_abs_V": max(r[2] for r in res),
+            "rel_residual_oracle_A": max(r[3] for r in res), "bar": 1e-6,
+            "reference": "oracle.step_system (bit-exact A_k, f_k of compute_optical_flow.py:100-146) + "
+                         "scipy spsolve (:147), on timesteps of the last timed batch",
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
+def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
     host on a bounded sample: Pool(C) runs per_core * C timesteps (SURVEY.md
     §8(d): 2 C); each assembles the first `frac` of the triangles with the
@@ -147,7 +182,7 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2):
     import reference_clone as clone
     C = clone.default_cores()
     K = per_core * C
-    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    a2, gw, e, iw = geom if geom is not None else oracle.geometry(p, n, t, a)
     a2l = clone.as_lil(a2)
     T = K + 1
     from mofhip import synth
@@ -163,6 +198,9 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2):
     value = K / full_wall
     return {
         "value": value, "unit": "timesteps/s", "cores": C, "kind": "port",
+        "host_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+        "cores_reason": "the GPU box's CPU share is 16 cores per GPU (OMP_NUM_THREADS=16 there); "
+                        "os.cpu_count() reports the whole machine",
         "sample": ("Pool(%d) x %d timesteps of the reference algorithm (lil scalar assembly, csr, "
                    "spsolve; oracle/reference_clone.py, calibrated vs the reference) on the %d-vertex "
                    "mesh; triangle loop timed on %d of %d triangles (%.1f s/step measured, "
@@ -267,7 +305,13 @@ def main():
                                        V_dev.data_ptr(), device=local, time_spmv=timed, **opts)
 
     if strong:
-        batches = [(a, min(a + B, K_rank)) for a in range(0, K_rank, B)]
+        # balanced batches: 625 timesteps per rank at N = 8 run as 2 x 313,
+        # not 512 + 113 (a narrow tail batch pays the whole setup and
+        # iteration sequence at a fraction of the width)
+        nbat = max(1, -(-K_rank // B))
+        B_eff = max(1, -(-K_rank // nbat))
+        opts["batch"] = B_eff
+        batches = [(a, min(a + B_eff, K_rank)) for a in range(0, K_rank, B_eff)]
         warm = batches[:max(1, args.warmup)] if batches else []
         if host_io:
             step_calls = [(0, K_rank)]
@@ -300,6 +344,20 @@ def main():
         agg["max_outer_steps"] = max(agg.get("max_outer_steps", 0), st["outer_steps"])
     sync()
     elapsed = time.perf_counter() - t0
+    # parity samples: timesteps of the last timed call, its V as the timed
+    # solve returned it (V_dev holds the last call's batch; host io: kept[-1])
+    samples = []
+    if rank == 0 and args.parity_samples > 0 and not dry and timed_calls:
+        a_, b_ = timed_calls[-1]
+        ks = sorted({a_ + round(q * (b_ - a_ - 1) / max(1, args.parity_samples - 1))
+                     for q in range(args.parity_samples)})
+        for k in ks:
+            if host_io:
+                Vk, I0k, I1k = kept[-1][k - a_], I_host[k], I_host[k + 1]
+            else:
+                Vk = V_dev[k - a_].cpu().numpy()
+                I0k, I1k = I_dev[k].cpu().numpy(), I_dev[k + 1].cpu().numpy()
+            samples.append((k_off + k, I0k, I1k, float(tk[k + 1] - tk[k]), Vk))
     kept.clear()
     cdev = torch.device("cpu") if (rehearse or dry) else dev
     elapsed = max_over_ranks(elapsed, dist, cdev)
@@ -359,9 +417,37 @@ def main():
                 "kernel_full_launch_frac": round((B * k_sys + k_shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
                 if t_full > 0 else None}
 
-    cpu = None
+    # host-to-host leg (SURVEY.md 8(d)'s metric: host I -> host V_k, the
+    # reference's submit -> join, compute_optical_flow.py:160-182), measured in
+    # this invocation after the device-resident region: pageable numpy I in,
+    # V into a numpy array, one mof_solve_range call per rank over
+    # --host-batches batches (the drop-in's pipelined path)
+    host_leg = None
+    if not host_io and not dry and args.host_batches > 0:
+        R = min(K_rank, args.host_batches * B)
+        I_h = I_dev[:R + 1].cpu().numpy()
+        mesh.solve_range(I_h, tk, 0, min(R, B), args.lambda_, device=local, **opts)  # pinned ring, slots
+        if dist:
+            dist.barrier()
+        sync()
+        th = time.perf_counter()
+        Vh, sh = mesh.solve_range(I_h, tk, 0, R, args.lambda_, device=local, **opts)
+        th = time.perf_counter() - th
+        th = max_over_ranks(th, dist, cdev)
+        nh = int(sum_over_ranks(sh["systems"], dist, cdev))
+        host_leg = {"value": round(nh / th, 3), "unit": "timesteps/s", "timesteps": nh,
+                    "seconds": round(th, 4), "failed": int(sum_over_ranks(sh["failed"], dist, cdev)),
+                    "io": "host: pageable numpy I (T, N) in, numpy V (T-1, 2N) out, PCIe inclusive "
+                          "(SURVEY.md 8(d) metric; reference timer compute_optical_flow.py:160-182)"}
+        del Vh, I_h
+
+    cpu = geom = None
+    if rank == 0 and not dry and (not args.no_cpu_baseline or samples):
+        import oracle
+        geom = oracle.geometry(p, n, t, a)
+    parity = parity_check(geom, t, a, args.lambda_, samples) if samples else None
     if rank == 0 and not args.no_cpu_baseline and not dry:
-        cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core)
+        cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom)
 
     if rank == 0:
         line = {
@@ -376,12 +462,15 @@ def main():
             "config": {"workload": CONFIG_NAMES[args.config], "vertices": N, "triangles": len(t),
                        "timesteps_per_step": args.fixed_timesteps if strong else world * B,
                        "timesteps_timed": n_ts, "batch": B, "precision": precision,
+                       "batch_effective": opts["batch"],
                        "precond": opts["precond"], "rtol": args.rtol,
                        "io": "host (pageable numpy I in, numpy V out; PCIe inclusive)" if host_io
                              else "device (I and V resident in HBM)",
                        "parallelism": "timestep shards x%d" % world},
             "roofline": roofline,
             "step_traffic": step_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), value),
+            "host_io": host_leg,
+            "parity": parity,
             "cpu_baseline": cpu,
             "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / n_local, 1),
                        "failed": agg["failed"], "recovered": agg["recovered"],

@@ -28,7 +28,12 @@
 extern "C" {
 #endif
 
-#define MOF_ABI_VERSION 1
+/* ABI version: bumped whenever a public struct or signature changes (2:
+ * mof_stats grew recovered / recovered_f64 and the SpMV accounting fields,
+ * mof_mesh_info blocks_read; mof_mesh_clone). A binding checks
+ * mof_abi_version() == MOF_ABI_VERSION of the header it was built against:
+ * the library writes whole structs, so a stale header would be overrun. */
+#define MOF_ABI_VERSION 2
 
 /* status codes */
 #define MOF_OK 0
@@ -69,10 +74,19 @@ extern "C" {
                                   NaN-filled at once. Default: they are
                                   re-solved, alone, with block-Jacobi PCG in
                                   the same precision (after a multigrid
-                                  solve) and then in fp64, and only a system
-                                  all of these fail is NaN-filled -- spsolve
-                                  is direct and always answers an SPD system
-                                  (compute_optical_flow.py:147) */
+                                  solve) and then in fp64 (an fp64 solve:
+                                  once more in fp64 with block Jacobi when
+                                  it ran without it or with max_iter below
+                                  10^4), each with max(max_iter, 10^4)
+                                  iterations and no stagnation test, and
+                                  only a system all of these fail is
+                                  NaN-filled -- spsolve is direct and always
+                                  answers an SPD system
+                                  (compute_optical_flow.py:147). The same in
+                                  mof_dd_solve_range. A recovery pass whose
+                                  fp64 workspace cannot be allocated leaves
+                                  its systems NaN-filled (MOF_E_NOCONV)
+                                  rather than failing the call */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */
@@ -140,6 +154,7 @@ typedef struct mof_mesh_info {
 
 /* Library / device queries. */
 const char *mof_version(void);
+int mof_abi_version(void);  /* MOF_ABI_VERSION the library was built with */
 const char *mof_last_error(void);
 int mof_device_count(int32_t *count);
 
@@ -151,6 +166,14 @@ int mof_device_count(int32_t *count);
 int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri,
                     const double *area, int32_t N, int32_t M, int32_t device,
                     uint32_t flags, mof_mesh **out);
+/* Another handle of the same mesh on `device` (one handle per GPU of a
+ * timestep-sharded compute_velocity_field, :157-177): the source's host
+ * state -- internal vertex order, block pattern, mirror table and every
+ * multigrid hierarchy built so far (or later, by either handle) -- is shared,
+ * not rebuilt; only the uploads and the per-mesh kernels run on `device`.
+ * Results are bit-identical to a mof_mesh_create handle. Handles may be
+ * cloned concurrently from different host threads. */
+int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out);
 int mof_mesh_destroy(mof_mesh *mesh);
 int mof_mesh_get_info(const mof_mesh *mesh, mof_mesh_info *info);
 

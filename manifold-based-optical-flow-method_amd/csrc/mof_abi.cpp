@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <functional>
 #include <future>
+#include <memory>
+#include <mutex>
 #include <new>
 
 #include "mof_amg.h"
@@ -124,42 +126,70 @@ void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
     }
 }
 
+}  // namespace
+
+namespace mof {
+
 // Systems of the batch whose solve failed are re-solved alone: with 2x2
 // block-Jacobi PCG in the same precision after a multigrid solve, then in
 // fp64 (no stagnation test, the full iteration budget); only what all of
-// them fail stays failed (NaN-filled by k_to_planar).
-void recover_failed(mof_mesh *m, int32_t nb, const mof::SolveParams &sp, int32_t user_max_iter, hipStream_t s,
-                    std::vector<uint8_t> &only, mof_stats &st) {
-    auto failed = [&](int32_t b) { return m->h_sysi[b * mof::kSysStride + mof::SI_FAILED] != 0; };
+// them fail stays failed (NaN-filled by k_to_planar). An fp64 solve gets
+// one fp64 block-Jacobi pass when its first solve ran without block Jacobi
+// or with a smaller budget (else the same solve would only repeat). An fp64
+// pass whose A64 workspace cannot be allocated leaves its systems failed
+// (NaN-filled, reported) instead of failing the whole call; after a mixed
+// solve the A64 it allocated is released again. Shared by the single-domain
+// and the decomposed paths: `ensure` sizes the workspace of a pass, `solve`
+// runs it on the `only` systems, `sysi` is the host flag mirror.
+void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, const int32_t *sysi,
+                     std::vector<uint8_t> &only, mof_stats &st, const std::function<void(uint32_t)> &ensure,
+                     const std::function<int64_t(const SolveParams &, const uint8_t *)> &solve,
+                     const std::function<void()> &release_f64) {
+    auto failed = [&](int32_t b) { return sysi[b * kSysStride + SI_FAILED] != 0; };
+    const int32_t budget = std::max(user_max_iter, 10000);  // the full budget, never less than the caller's
     std::vector<uint32_t> passes;
     if (sp.precision == MOF_PREC_MIXED && sp.amg) passes.push_back(MOF_PREC_MIXED);
-    if (sp.precision == MOF_PREC_MIXED) passes.push_back(MOF_PREC_F64);
+    if (sp.precision == MOF_PREC_MIXED || !sp.block_jacobi || sp.max_iter < budget) passes.push_back(MOF_PREC_F64);
     std::vector<uint8_t> first(nb, 0);
-    for (int32_t b = 0; b < nb; ++b) first[b] = failed(b);
+    int32_t nfirst = 0;
+    for (int32_t b = 0; b < nb; ++b) nfirst += (first[b] = failed(b));
+    if (!nfirst) return;
+    bool used_f64 = false;
     for (uint32_t prec : passes) {
         int32_t n = 0;
         for (int32_t b = 0; b < nb; ++b) n += (only[b] = failed(b));
         if (!n) break;
-        mof::SolveParams rp = sp;
+        SolveParams rp = sp;
         rp.precision = prec;
         rp.amg = false;
         rp.block_jacobi = true;
         rp.stall = 0;
         rp.fail_at_max_iter = false;
         rp.time_spmv = false;
-        rp.max_iter = user_max_iter > 0 ? user_max_iter : 10000;
-        mof::ensure_workspace(m, nb, prec);
-        mof::launch_recovery_operator(m, nb, prec, s);
-        int32_t outer = 0;
-        st.iterations += mof::solve_batch(m, nb, rp, s, &outer, &st.max_iterations, nullptr, only.data());
+        rp.max_iter = budget;
+        if (prec == MOF_PREC_F64 && sp.precision == MOF_PREC_MIXED) {
+            try {
+                ensure(prec);
+            } catch (const Error &e) {
+                if (e.code != MOF_E_HIP) throw;
+                (void)hipGetLastError();  // an allocation failure: the systems stay failed
+                release_f64();
+                break;
+            }
+            used_f64 = true;
+        } else {
+            ensure(prec);
+        }
+        st.iterations += solve(rp, only.data());
         for (int32_t b = 0; b < nb; ++b)
             if (only[b] && !failed(b) && prec == MOF_PREC_F64) st.recovered_f64++;
     }
+    if (used_f64) release_f64();
     for (int32_t b = 0; b < nb; ++b)
         if (first[b] && !failed(b)) st.recovered++;
 }
 
-}  // namespace
+}  // namespace mof
 
 // error handling for the host-only entry points of mof_io.cpp
 int mof_io_guard(const std::function<void()> &f) { return guarded(f); }
@@ -172,7 +202,25 @@ void mesh_set_own(mof_mesh *m, int32_t nown) {
     // MOF_SYM_READS: 1 / 0 force the symmetric / plain reads, unset: per mesh
     const char *env = std::getenv("MOF_SYM_READS");
     const int sym = !MOF_SYM_A ? 0 : env && *env ? (std::atoi(env) != 0) : -1;
-    const std::vector<int32_t> mir = sell_mirror(m->pat, nown, sym, &m->sym_reads);
+    // one host mirror table per (mesh, nown, mode), shared by the clones
+    std::shared_ptr<const MirrorTable> mt;
+    {
+        MeshShared *sh = m->shared.get();
+        std::unique_lock<std::mutex> lk;
+        if (sh) lk = std::unique_lock<std::mutex>(sh->mu);
+        if (sh && sh->mirror && sh->mirror->nown == nown && sh->mirror->sym == sym) {
+            mt = sh->mirror;
+        } else {
+            auto t = std::make_shared<MirrorTable>();
+            t->nown = nown;
+            t->sym = sym;
+            t->table = sell_mirror(m->pat, nown, sym, &t->used);
+            if (sh) sh->mirror = t;
+            mt = t;
+        }
+    }
+    m->sym_reads = mt->used;
+    const std::vector<int32_t> &mir = mt->table;
     m->sell_mir.alloc(mir.size());
     m->sell_mir.upload(mir.data(), mir.size(), m->stream);
     int64_t own = 0;  // positions read at their own place: diagonal + upper blocks
@@ -181,13 +229,15 @@ void mesh_set_own(mof_mesh *m, int32_t nown) {
     MOF_HIP(hipStreamSynchronize(m->stream));
 }
 
-void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t *tri,
-                const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
-                const int32_t *perm_in, const int32_t *tri_ids) {
+// Host half of a mesh build: internal vertex / triangle order, the
+// relabelled inputs and the block pattern. Kept in MeshShared so further
+// handles of the same mesh on other devices (mof_mesh_clone) only upload.
+void mesh_prepare_host(mof_mesh *m, const double *xyz, const double *nrm, const int32_t *tri,
+                       const double *area, int32_t N, int32_t M, uint32_t flags, const int32_t *perm_in,
+                       const int32_t *tri_ids) {
     m->N = N;
     m->n_own = N;
     m->M = M;
-    m->device = device;
     m->flags = flags;
     double t0 = now_ms();
     MOF_REQUIRE(N > 0 && M > 0, "mesh needs N > 0 vertices and M > 0 triangles");
@@ -218,42 +268,51 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
     for (int32_t i = 0; i < N; ++i) m->inv[m->perm[i]] = i;
     m->tinv.resize(M);
     for (int32_t T = 0; T < M; ++T) m->tinv[m->tperm[T]] = T;
-    std::vector<int32_t> tri_new(3 * (size_t)M), tri_old(3 * (size_t)M);
-    std::vector<double> area_new(M);
+    auto sh = std::make_shared<MeshShared>();
+    sh->tri_new.resize(3 * (size_t)M);
+    sh->tri_old.resize(3 * (size_t)M);
+    sh->area_new.resize(M);
     for (int32_t T = 0; T < M; ++T) {
         const int32_t To = m->tperm[T];
         for (int c = 0; c < 3; ++c) {
-            tri_old[3 * (size_t)T + c] = (tri_ids ? tri_ids : tri)[3 * (size_t)To + c];
-            tri_new[3 * (size_t)T + c] = m->perm[tri[3 * (size_t)To + c]];
+            sh->tri_old[3 * (size_t)T + c] = (tri_ids ? tri_ids : tri)[3 * (size_t)To + c];
+            sh->tri_new[3 * (size_t)T + c] = m->perm[tri[3 * (size_t)To + c]];
         }
-        area_new[T] = area[To];
+        sh->area_new[T] = area[To];
     }
-    std::vector<double> xyz_new(3 * (size_t)N), nrm_new(3 * (size_t)N);
+    sh->xyz_new.resize(3 * (size_t)N);
+    sh->nrm_new.resize(3 * (size_t)N);
     for (int32_t i = 0; i < N; ++i)
         for (int d = 0; d < 3; ++d) {
-            xyz_new[3 * (size_t)m->perm[i] + d] = xyz[3 * (size_t)i + d];
-            nrm_new[3 * (size_t)m->perm[i] + d] = nrm[3 * (size_t)i + d];
+            sh->xyz_new[3 * (size_t)m->perm[i] + d] = xyz[3 * (size_t)i + d];
+            sh->nrm_new[3 * (size_t)m->perm[i] + d] = nrm[3 * (size_t)i + d];
         }
-    mof::build_pattern(tri_new.data(), N, M, m->pat, m->tinv.data());
+    // vertices in no triangle are never gathered: column 0
+    sh->icol.assign(N, 0);
+    for (size_t q = 0; q < 3 * (size_t)M; ++q) sh->icol[sh->tri_new[q]] = sh->tri_old[q];
+    mof::build_pattern(sh->tri_new.data(), N, M, m->pat, m->tinv.data());
+    m->shared = std::move(sh);
     m->ms_pattern = now_ms() - t0;
+}
+
+// Device half: uploads, the per-mesh kernels (bases, hat gradients, a2) on
+// m->device. Identical results on every device (same inputs, same kernels).
+void mesh_upload(mof_mesh *m) {
+    const MeshShared &H = *m->shared;
+    const int32_t N = m->N, M = m->M;
     MOF_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
     hipStream_t s = m->stream;
     const mof::Pattern &P = m->pat;
     m->tri.alloc(3 * (size_t)M);
-    m->tri.upload(tri_new.data(), 3 * (size_t)M, s);
+    m->tri.upload(H.tri_new.data(), 3 * (size_t)M, s);
     m->tri_orig.alloc(3 * (size_t)M);
-    m->tri_orig.upload(tri_old.data(), 3 * (size_t)M, s);
+    m->tri_orig.upload(H.tri_old.data(), 3 * (size_t)M, s);
     m->perm_d.alloc(N);
     m->perm_d.upload(m->perm.data(), N, s);
-    {
-        // vertices in no triangle are never gathered: column 0
-        std::vector<int32_t> icol(N, 0);
-        for (size_t q = 0; q < 3 * (size_t)M; ++q) icol[tri_new[q]] = tri_old[q];
-        m->icol.alloc(N);
-        m->icol.upload(icol.data(), N, s);
-    }
+    m->icol.alloc(N);
+    m->icol.upload(H.icol.data(), N, s);
     m->area.alloc(M);
-    m->area.upload(area_new.data(), M, s);
+    m->area.upload(H.area_new.data(), M, s);
     auto put = [&](mof::DevArray<int32_t> &d, const std::vector<int32_t> &h) {
         d.alloc(h.size());
         d.upload(h.data(), h.size(), s);
@@ -273,9 +332,9 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
     mesh_set_own(m, N);
     mof::DevArray<double> dxyz, dnrm;
     dxyz.alloc(3 * (size_t)N);
-    dxyz.upload(xyz_new.data(), 3 * (size_t)N, s);
+    dxyz.upload(H.xyz_new.data(), 3 * (size_t)N, s);
     dnrm.alloc(3 * (size_t)N);
-    dnrm.upload(nrm_new.data(), 3 * (size_t)N, s);
+    dnrm.upload(H.nrm_new.data(), 3 * (size_t)N, s);
     m->e.alloc(6 * (size_t)N);
     m->gw.alloc(9 * (size_t)M);
     m->iw.alloc(2 * (size_t)M);
@@ -290,18 +349,28 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
     m->fexp.alloc(2 * (size_t)N);
     Events ev;
     MOF_HIP(hipEventRecord(ev.e[0], s));
-    mof::launch_geometry(m, dxyz.p, dnrm.p, (flags & MOF_GEOM_F32_POINTS) != 0);
+    mof::launch_geometry(m, dxyz.p, dnrm.p, (m->flags & MOF_GEOM_F32_POINTS) != 0);
     mof::launch_a2(m);
     MOF_HIP(hipEventRecord(ev.e[1], s));
     MOF_HIP(hipStreamSynchronize(s));
     m->ms_geometry = ev.ms(0, 1);
 }
 
+void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t *tri,
+                const double *area, int32_t N, int32_t M, int32_t device, uint32_t flags,
+                const int32_t *perm_in, const int32_t *tri_ids) {
+    m->device = device;
+    mesh_prepare_host(m, xyz, nrm, tri, area, N, M, flags, perm_in, tri_ids);
+    mesh_upload(m);
+}
+
 }  // namespace mof
 
 extern "C" {
 
-const char *mof_version(void) { return "mofhip 0.1 (gfx950, abi 1)"; }
+const char *mof_version(void) { return "mofhip 0.3 (gfx950, abi 2)"; }
+
+int mof_abi_version(void) { return MOF_ABI_VERSION; }
 
 const char *mof_last_error(void) { return g_err.c_str(); }
 
@@ -327,6 +396,39 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri, co
         auto *m = new mof_mesh();
         try {
             mof::mesh_build(m, xyz, nrm, tri, area, N, M, device, flags, nullptr, nullptr);
+        } catch (...) {
+            mof_mesh_destroy(m);
+            throw;
+        }
+        *out = m;
+    });
+}
+
+int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out) {
+    return guarded([&] {
+        MOF_REQUIRE(out, "out is NULL");
+        *out = nullptr;
+        MOF_REQUIRE(src && src->shared, "source mesh is NULL or not a mof_mesh_create handle");
+        int ndev = 0;
+        MOF_HIP(hipGetDeviceCount(&ndev));
+        MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+        DeviceGuard dg(device);
+        auto *m = new mof_mesh();
+        try {
+            // host state of the source (pattern, orders): copied, not rebuilt
+            m->N = src->N;
+            m->M = src->M;
+            m->n_own = src->N;
+            m->flags = src->flags;
+            m->device = device;
+            m->pat = src->pat;
+            m->perm = src->perm;
+            m->inv = src->inv;
+            m->tperm = src->tperm;
+            m->tinv = src->tinv;
+            m->shared = src->shared;
+            m->ms_pattern = 0.0;
+            mof::mesh_upload(m);
         } catch (...) {
             mof_mesh_destroy(m);
             throw;
@@ -589,7 +691,18 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 int32_t outer = 0;
                 st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
                 st.outer_steps = outer;
-                if (recovery) recover_failed(m, nb, sp, o.max_iter, s, only, st);
+                if (recovery)
+                    mof::recover_systems(
+                        nb, sp, o.max_iter, m->h_sysi, only, st,
+                        [&](uint32_t prec) {
+                            mof::ensure_workspace(m, nb, prec);
+                            mof::launch_recovery_operator(m, nb, prec, s);
+                        },
+                        [&](const mof::SolveParams &rp, const uint8_t *on) {
+                            int32_t outer_r = 0;
+                            return mof::solve_batch(m, nb, rp, s, &outer_r, &st.max_iterations, nullptr, on);
+                        },
+                        [&] { m->ws.A64.release(); });
                 double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[sl].p;
                 mof::launch_to_planar(m, nb, Vdst, s);
                 if (!dev_io) MOF_HIP(hipEventRecord(m->hev[4 + sl], s));

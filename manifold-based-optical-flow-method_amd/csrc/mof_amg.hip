@@ -1302,24 +1302,48 @@ bool amg_build(mof_mesh *m) {
     if (!m->amg) m->amg = new AmgDevice();
     AmgDevice &G = *m->amg;
     hipStream_t s = m->stream;
-    std::vector<double> e(6 * (size_t)m->N);
-    MOF_HIP(hipMemcpyAsync(e.data(), m->e.p, e.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-    MOF_HIP(hipStreamSynchronize(s));
-    // the mesh's a2 (unscaled, fine SELL layout) for the smoothed prolongator
-    std::vector<double> a2;
-    if (prm.nown < 0 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) {
-        a2.resize(4 * (size_t)m->pat.sell_nb());
-        MOF_HIP(hipMemcpyAsync(a2.data(), m->a2.p, a2.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    // the host hierarchy of this mesh and parameter set: built once per mesh
+    // and shared by its handles on other devices (MeshShared); the inputs
+    // (pattern, e, a2) are the same on every device, bit for bit
+    MeshShared *sh = m->shared.get();
+    char key[160];
+    std::snprintf(key, sizeof(key), "%a/%a/%d/%d/%a/%d", (double)prm.omega, (double)prm.omega1, prm.smooth,
+                  prm.nown, (double)prm.smooth_omega, (int)(m->sym_reads && MOF_SKIP_LOWER));
+    std::unique_lock<std::mutex> build_lock;
+    std::shared_ptr<const AmgHierarchy> Hp;
+    if (sh) {
+        build_lock = std::unique_lock<std::mutex>(sh->amg_build_mu);
+        std::lock_guard<std::mutex> lk(sh->mu);
+        for (const auto &kv : sh->amg)
+            if (kv.first == key) Hp = kv.second;
+    }
+    if (!Hp) {
+        std::vector<double> e(6 * (size_t)m->N);
+        MOF_HIP(hipMemcpyAsync(e.data(), m->e.p, e.size() * sizeof(double), hipMemcpyDeviceToHost, s));
         MOF_HIP(hipStreamSynchronize(s));
-        prm.a2 = a2.data();
+        // the mesh's a2 (unscaled, fine SELL layout) for the smoothed prolongator
+        std::vector<double> a2;
+        if (prm.nown < 0 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) {
+            a2.resize(4 * (size_t)m->pat.sell_nb());
+            MOF_HIP(hipMemcpyAsync(a2.data(), m->a2.p, a2.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+            MOF_HIP(hipStreamSynchronize(s));
+            prm.a2 = a2.data();
+        }
+        std::vector<int32_t> mir;
+        if (m->sym_reads && MOF_SKIP_LOWER) {
+            mir = sell_mirror(m->pat, m->n_own, 1, nullptr);
+            prm.mirror = mir.data();
+        }
+        auto built = std::make_shared<AmgHierarchy>();
+        build_amg(m->pat, e.data(), prm, *built);
+        Hp = built;
+        if (sh) {
+            std::lock_guard<std::mutex> lk(sh->mu);
+            sh->amg.emplace_back(key, Hp);
+        }
     }
-    std::vector<int32_t> mir;
-    if (m->sym_reads && MOF_SKIP_LOWER) {
-        mir = sell_mirror(m->pat, m->n_own, 1, nullptr);
-        prm.mirror = mir.data();
-    }
-    AmgHierarchy H;
-    build_amg(m->pat, e.data(), prm, H);
+    if (build_lock.owns_lock()) build_lock.unlock();
+    const AmgHierarchy &H = *Hp;
     G.omega = prm.omega;
     G.omega1 = prm.omega1;
     // level 0's corrected iterate x0 + Q y: bf16 in place on meshes with the

@@ -20,6 +20,25 @@ __device__ __forceinline__ double dot64(const double *x, const double *y) {
     return fma(x[2], y[2], fma(x[1], y[1], x[0] * y[0]));
 }
 
+// x / 12, correctly rounded, without the divide sequence (the f term's
+// "... * T_area / 12", compute_optical_flow.py:311): q0 = x c with
+// c = RN(1/12), the residual r = x - 12 q0 (exact in an fma: q0 is within an
+// ulp of x/12), q = RN(q0 + r c). Bit-identical to x / 12 for every x whose
+// quotient is a normal double: x/12 = (x/3)/4, and x/3 of a 53-bit
+// significand lies 0, 1/3 or 2/3 of an ulp past a double, at least 1/6 ulp
+// from every rounding midpoint, while q0 + r c is within 2^-53 ulp of it.
+// Quotients near or below the subnormal range (where the residual is no
+// longer exact), zeros and nan take the IEEE divide; infinities q0 (= x / 12).
+// Checked on the host against x / 12 (tests/test_div12.py: the same
+// operations in C over random bit patterns of every exponent).
+__device__ __forceinline__ double div12(double x) {
+    constexpr double c = 1.0 / 12.0;
+    const double q0 = x * c;
+    if (!(fabs(q0) >= 0x1p-1020)) return x / 12.0;
+    const double q = fma(fma(-q0, 12.0, x), c, q0);
+    return __builtin_isfinite(q0) ? q : q0;
+}
+
 // np.dot of two float32 3-vectors on scipy-openblas: float products summed
 // in double, rounded to float once.
 __device__ __forceinline__ float dot32(const float *x, const float *y) {
@@ -180,7 +199,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
                                                   const double *__restrict__ I1, int64_t ldI,
                                                   const double *__restrict__ dt,
                                                   double *__restrict__ u, double *__restrict__ fc,
-                                                  float *__restrict__ u32) {
+                                                  float *__restrict__ u32, const double *__restrict__ dI) {
     // one triangle per thread for all B systems: the geometry is read once
     const int32_t T = blockIdx.x * kWG + threadIdx.x;
     if (T >= M) return;
@@ -205,8 +224,18 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
         double gI[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) gI[d] = (a0 * g[d] + a1 * g[3 + d]) + a2 * g[6 + d];
-        const double h = dt[b];
-        const double pd[3] = {(i1[vo[0]] - a0) / h, (i1[vo[1]] - a1) / h, (i1[vo[2]] - a2) / h};
+        double pd[3];
+        if (dI) {  // k_gather_I's (I1 - I0) / dt of the internal-order rows: the same bits
+            const double *db = dI + b * ldI;
+            pd[0] = db[vo[0]];
+            pd[1] = db[vo[1]];
+            pd[2] = db[vo[2]];
+        } else {
+            const double h = dt[b];
+            pd[0] = (i1[vo[0]] - a0) / h;
+            pd[1] = (i1[vo[1]] - a1) / h;
+            pd[2] = (i1[vo[2]] - a2) / h;
+        }
         const int64_t base = 6 * ((int64_t)b * (M + 1) + T);
         double uo[6], fo[6];
 #pragma unroll
@@ -227,7 +256,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
             for (int al = 0; al < 2; ++al) {
                 const double uu = dot64(gI, &ev[a][3 * al]);
                 uo[2 * a + al] = uu;
-                fo[2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
+                fo[2 * a + al] = div12(uu * (2 * pd[a] + po) * A);
             }
         }
 #pragma unroll
@@ -612,6 +641,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows(
 
 struct TriGeo {
     const double *gw, *e, *area, *J0, *J1, *dt;  // J0 / J1: the batch's I rows (internal order, stride N)
+    const double *dI;                            // (J1 - J0) / dt per system (k_gather_I), stride N
 };
 template <int WMAX, int NS>
 __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
@@ -623,14 +653,12 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     const int32_t *__restrict__ mir, TriGeo geo) {
     int32_t rb, bq;
     if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpAsm)) return;
-    const double *I0b[NS], *I1b[NS];
-    double hb[NS];
+    const double *I0b[NS], *Db[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         const int32_t b = min(bq * NS + k, B - 1);  // slots past B recompute B-1 and store nothing
         I0b[k] = geo.J0 + (int64_t)b * N;
-        I1b[k] = geo.J1 + (int64_t)b * N;
-        hb[k] = geo.dt[b];
+        Db[k] = geo.dI + (int64_t)b * N;
     }
 #pragma unroll 1
     for (int r = 0; r < kRows; ++r) {
@@ -648,7 +676,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             for (int z = 0; z < WMAX; ++z) acc[k][z][0] = acc[k][z][1] = acc[k][z][2] = acc[k][z][3] = 0.f;
             f0[k] = f1[k] = 0.0;
             Ii0[k] = I0b[k][i];
-            pdi[k] = (I1b[k][i] - Ii0[k]) / hb[k];
+            pdi[k] = Db[k][i];
         }
         const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
         for (int32_t t = 0; t < tw; ++t) {
@@ -677,7 +705,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
                 const double aj = I0b[k][vj], ak = I0b[k][vk];
-                const double pdj = (I1b[k][vj] - aj) / hb[k], pdk = (I1b[k][vk] - ak) / hb[k];
+                const double pdj = Db[k][vj], pdk = Db[k][vk];
                 // the triangle's I0 in its own corner order (corner c is i)
                 const double c0 = c == 0 ? Ii0[k] : (c == 1 ? ak : aj);
                 const double c1 = c == 0 ? aj : (c == 1 ? Ii0[k] : ak);
@@ -688,8 +716,8 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
                 const double ui0 = dot64(gI, ei), ui1 = dot64(gI, ei + 3);
                 const double po = hj ? (hk ? pdj + pdk : pdj) : (hk ? pdk : 0.0);
                 if (real) {  // f in the reference's triangle order
-                    f0[k] += ui0 * (2 * pdi[k] + po) * At / 12;
-                    f1[k] += ui1 * (2 * pdi[k] + po) * At / 12;
+                    f0[k] += div12(ui0 * (2 * pdi[k] + po) * At);
+                    f1[k] += div12(ui1 * (2 * pdi[k] + po) * At);
                 }
                 const float2 ui = make_float2((float)ui0, (float)ui1);
                 const float2 uj = make_float2((float)dot64(gI, ej), (float)dot64(gI, ej + 3));
@@ -923,16 +951,30 @@ void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
 // 256-system k_tri_step on C3, 5151 -> 2979 us with a random vertex order).
 // One XCD per row (workgroup w runs on XCD w mod 8): the row's gathers stay
 // in that XCD's L2. Row r < R0 comes from I0 + r ldI, the others from I1.
+// Rows r < B also write system r's time derivative dI = (I1 - I0) / dt in
+// the internal order (the row-assembly reads it instead of I1): the same IEEE
+// subtract and divide compute_f does per vertex (compute_optical_flow.py:
+// 303-309, k_tri_step's pd), once per vertex and system instead of once per
+// incidence -- two fp64 divides fewer per incident triangle.
 __global__ __launch_bounds__(kWG) void k_gather_I(int32_t N, int32_t R, int32_t R0, const double *__restrict__ I0,
                                                   const double *__restrict__ I1, int64_t ldI,
-                                                  const int32_t *__restrict__ icol, double *__restrict__ out) {
+                                                  const int32_t *__restrict__ icol, double *__restrict__ out,
+                                                  int32_t B, const double *__restrict__ dt,
+                                                  double *__restrict__ dI) {
     const int32_t w = blockIdx.x, q = w >> 3;
     const int32_t nbi = (N + kWG - 1) / kWG;
     const int32_t r = (w & 7) + 8 * (q / nbi);
     const int32_t i = (q % nbi) * kWG + threadIdx.x;
     if (r >= R || i >= N) return;
+    const int32_t c = icol[i];
     const double *src = r < R0 ? I0 + r * ldI : I1 + (int64_t)(r - R0) * ldI;
-    out[(int64_t)r * N + i] = src[icol[i]];
+    const double v0 = src[c];
+    out[(int64_t)r * N + i] = v0;
+    if (dI && r < B) {
+        // system r pairs I0 row r with I1 row r (in the shared layout I1 = I0 + ldI)
+        const double v1 = I1[(int64_t)r * ldI + c];
+        dI[(int64_t)r * N + i] = (v1 - v0) / dt[r];
+    }
 }
 
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
@@ -945,7 +987,8 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
                 "assembly workspace / operator not prepared");
     MOF_REQUIRE(precision == MOF_PREC_MIXED ? w.A32.n >= 4 * nbs * B : w.A64.n >= 4 * nbs * B,
                 "assembly target A not allocated");
-    MOF_REQUIRE(ldI >= 1 && m->icol.n >= (size_t)m->N && w.Iint.n >= 2 * (size_t)m->N * B,
+    MOF_REQUIRE(ldI >= 1 && m->icol.n >= (size_t)m->N && w.Iint.n >= 2 * (size_t)m->N * B &&
+                    w.dI.n >= (size_t)m->N * B,
                 "I permutation buffers not prepared");
     {
         // consecutive timesteps of one array share B-1 rows: B+1 rows then
@@ -953,7 +996,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
         const int32_t R = shared ? B + 1 : 2 * B, R0 = shared ? R : B;
         const int32_t nbi = (m->N + kWG - 1) / kWG;
         k_gather_I<<<dim3((unsigned)(8 * ((R + 7) / 8) * nbi)), kWG, 0, s>>>(m->N, R, R0, I0, I1, ldI, m->icol.p,
-                                                                            w.Iint.p);
+                                                                            w.Iint.p, B, w.dt.p, w.dI.p);
     }
     const double *J0 = w.Iint.p, *J1 = w.Iint.p + (I1 == I0 + ldI ? (int64_t)m->N : (int64_t)m->N * B);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
@@ -971,12 +1014,12 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (!asm_rc)
         k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
                                       skip_u64 ? nullptr : w.u64.p, w.fc.p,
-                                      precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
+                                      precision == MOF_PREC_MIXED ? w.u32.p : nullptr, w.dI.p);
     w.u64_stale = skip_u64 || asm_rc;  // u64 (and with asm_rc fc) re-formed by the fp64 recovery if needed
     w.J0 = J0;
     w.J1 = J1;
     w.JB = B;
-    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, J1, w.dt.p};
+    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, J1, w.dt.p, w.dI.p};
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
@@ -1039,7 +1082,7 @@ void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStr
             MOF_REQUIRE(w.J0 && w.J1 && w.JB >= B, "recovery: the batch's I rows are gone");
             k_tri_step<<<dim3((unsigned)((m->M + kWG - 1) / kWG)), kWG, 0, s>>>(
                 m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, w.J0, w.J1, m->N, w.dt.p, w.u64.p, w.fc.p,
-                nullptr);
+                nullptr, w.dI.p);
             w.u64_stale = false;
         }
         const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
@@ -1055,7 +1098,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
     Workspace &w = m->ws;
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, 1, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
-                                  w.u64.p, w.fc.p, nullptr);
+                                  w.u64.p, w.fc.p, nullptr, nullptr);
     const int64_t snb = m->pat.sell_nb();
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
                                                  m->vcol.p, m->cptr.p, m->clist.p, m->iw.p, m->a2.p,

@@ -108,8 +108,10 @@ namespace mof {
 void dd_ensure(mof_dd *d, int32_t B, uint32_t precision);
 // One batch of B assembled systems: mixed (fp32 inner + fp64 refinement) or
 // fp64 block-Jacobi PCG over all parts; returns summed inner iterations.
+// only (B flags, optional): re-solve just these systems from x = 0; the
+// others keep their solution and flags (the recovery passes).
 int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
-                       int32_t *max_iters);
+                       int32_t *max_iters, const uint8_t *only = nullptr);
 // transport hooks (mof_dd.hip)
 void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s);
 // refresh the ghost rows of every local part's z (which = 0; fp32 when f32) or

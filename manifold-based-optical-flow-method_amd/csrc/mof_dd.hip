@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -697,6 +698,11 @@ int mof_dd_get_info(const mof_dd *d, mof_dd_info *info) {
     });
 }
 
+static int env_int_dd(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
 int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const double *t_k, int32_t T, int32_t k0,
                        int32_t k1, double lambda, const mof_opts *opts, double *V_out, mof_stats *stats) {
     return mof_io_guard([&] {
@@ -716,10 +722,16 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
         MOF_REQUIRE(!sp.amg || o.precision == MOF_PREC_MIXED, "MOF_PRECOND_AMG needs MOF_PREC_MIXED");
         sp.block_jacobi = sp.amg || !(o.flags & MOF_NO_BLOCK_JACOBI);
         sp.time_spmv = false;
-        sp.max_iter = o.max_iter > 0 ? o.max_iter : 10000;
+        // the single-domain defaults (mof_solve_range): a multigrid inner
+        // solve takes tens of iterations, so 1000 and a stagnation window
+        // mark a bad preconditioner, and the system goes to the recovery
+        sp.max_iter = o.max_iter > 0 ? o.max_iter : (sp.amg ? 1000 : 10000);
         sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
         sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
         sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
+        sp.stall = sp.amg ? env_int_dd("MOF_PCG_STALL", 64) : 0;
+        sp.fail_at_max_iter = sp.amg;
+        const bool recovery = !(o.flags & MOF_NO_RECOVERY);
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
         if (!I2) I2 = I;
         DevGuard g(d->device);
@@ -752,6 +764,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
             hipEvent_t ev[3];
             for (auto &e : ev) MOF_HIP(hipEventCreate(&e));
             std::vector<double> dts(B);
+            std::vector<uint8_t> only(B);
             try {
                 for (int32_t k = k0; k < k1; k += B) {
                     const int32_t nb = std::min(B, k1 - k);
@@ -777,6 +790,22 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                     int32_t outer = 0;
                     st.iterations += solve_batch_dd(d, nb, sp, s, &outer, &st.max_iterations);
                     st.outer_steps = outer;
+                    // failed systems re-solved alone, as in mof_solve_range
+                    // (every part / rank sees the same flags)
+                    if (recovery)
+                        recover_systems(
+                            nb, sp, o.max_iter, d->parts[0]->h_sysi, only, st,
+                            [&](uint32_t prec) {
+                                dd_ensure(d, nb, prec);
+                                for (mof_mesh *m : d->parts) launch_recovery_operator(m, nb, prec, s);
+                            },
+                            [&](const SolveParams &rp, const uint8_t *on) {
+                                int32_t outer_r = 0;
+                                return solve_batch_dd(d, nb, rp, s, &outer_r, &st.max_iterations, on);
+                            },
+                            [&] {
+                                for (mof_mesh *m : d->parts) m->ws.A64.release();
+                            });
                     double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : Vbuf.p;
                     dd_gather_v(d, nb, Vdst, s);
                     MOF_HIP(hipEventRecord(ev[2], s));

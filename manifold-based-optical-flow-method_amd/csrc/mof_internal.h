@@ -17,6 +17,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -150,6 +153,7 @@ struct Workspace {
     DevArray<double> dt;               // [B]
     DevArray<double> Ibuf;             // [B][N] I0 rows + [B][N] I1 rows (host-staged)
     DevArray<double> Iint;             // the batch's I rows in internal vertex order ([B+1] or [2B] rows)
+    DevArray<double> dI;               // [B][N] (I1 - I0) / dt per system, internal order (k_gather_I)
     DevArray<double> Vbuf;             // [B][2N] planar output staging
     // MOF_RES_RECOMPUTE: the mixed path's k_tri_step leaves u64 unwritten
     // (the fp64 residual re-forms u from the batch's I rows); the fp64
@@ -173,8 +177,29 @@ enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_BEST_IT = 4, SI_FAIL_I
 enum FailWhy { FW_BREAKDOWN = 1, FW_DIVERGED = 2, FW_STALLED = 3, FW_MAXITER = 4, FW_RESIDUAL = 5 };
 constexpr int kSysStride = 8;
 
-struct AmgDevice;  // mof_amg.h
-class HostStage;   // mof_hostio.h
+struct AmgDevice;     // mof_amg.h
+struct AmgHierarchy;  // mof_amg.h
+class HostStage;      // mof_hostio.h
+
+// Host state of one mesh shared by its handles on several devices
+// (mof_mesh_create builds it once, mof_mesh_clone reuses it): the inputs in
+// the internal vertex / triangle order, the symmetric-read mirror table, and
+// the multigrid hierarchies built so far (per parameter set), so N device
+// handles cost one host pattern + hierarchy build, not N.
+struct MirrorTable {
+    int32_t nown = 0;
+    int sym = -1;
+    bool used = false;
+    std::vector<int32_t> table;
+};
+struct MeshShared {
+    std::vector<int32_t> tri_new, tri_old, icol;
+    std::vector<double> area_new, xyz_new, nrm_new;
+    std::mutex mu;  // guards mirror and amg
+    std::shared_ptr<const MirrorTable> mirror;
+    std::vector<std::pair<std::string, std::shared_ptr<const AmgHierarchy>>> amg;
+    std::mutex amg_build_mu;  // one hierarchy build at a time per mesh
+};
 
 // Cross-part reduction layout of the PCG kernels: partial record of
 // (part, system b, workgroup w) at ((part * B + b) * nmax + w) * NV; rows
@@ -235,6 +260,8 @@ struct mof_mesh {
     // [4..5] V written
     mof::HostStage *stage = nullptr;
     mof::DevArray<double> hin[2], hout[2];
+    // host state shared with the clones of this mesh on other devices
+    std::shared_ptr<mof::MeshShared> shared;
     hipEvent_t hev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -309,6 +336,12 @@ struct SolveParams {
 // their x64 and flags from the previous solve of the batch.
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
                     int32_t *max_iters, SpmvTiming *timing, const uint8_t *only = nullptr);
+// Re-solve the failed systems of a solved batch (block Jacobi in the same
+// precision after a multigrid solve, then fp64); mof_abi.cpp.
+void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, const int32_t *sysi,
+                     std::vector<uint8_t> &only, mof_stats &st, const std::function<void(uint32_t)> &ensure,
+                     const std::function<int64_t(const SolveParams &, const uint8_t *)> &solve,
+                     const std::function<void()> &release_f64);
 // Operators a recovery solve needs that the first solve's assembly did not
 // write: with MOF_PREC_MIXED the fp32 2x2 block-Jacobi inverses from the fp32
 // A (the multigrid assembly keeps D^-1 in bf16 only); with MOF_PREC_F64 the

@@ -1375,6 +1375,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.dt.alloc(B);
     w.Ibuf.alloc(2 * N * B);
     w.Iint.alloc(2 * N * B);
+    w.dI.alloc(N * B);
     w.Vbuf.alloc(2 * N * B);
     if (m->h_cap < B) {
         if (m->h_sysi) (void)hipHostFree(m->h_sysi);
@@ -1512,9 +1513,13 @@ std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, bool amg) {
 }
 
 template <typename V>
-int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_iter, hipStream_t s,
+int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, const SolveParams &sp, hipStream_t s,
                int32_t *max_iters, int32_t *hint, bool amg) {
+    const int32_t max_iter = sp.max_iter;
     std::vector<PcgArgs<V>> args = dd_args<V>(d, B, amg);
+    // the single-domain solve's failure tests: stagnation window, a capped
+    // multigrid solve fails the system (every part takes the same decision)
+    for (PcgArgs<V> &a : args) a.stall = sp.stall;
     const size_t L = args.size();
     mof_mesh *m0 = d->parts[0];
     const int64_t rec = (int64_t)B * d->nmax;  // records of one part
@@ -1580,14 +1585,19 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
     }
     if (!done) {
         spmv(false, it);
+        if (sp.fail_at_max_iter)
+            for (size_t l = 0; l < L; ++l)
+                k_fail_running<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, it, args[l].sysi);
+        MOF_HIP(hipGetLastError());
         fetch_flags(m0, B, s);
     }
     int64_t total = 0;
     int32_t slowest = 0, slowest_conv = 0;
     for (int32_t b = 0; b < B; ++b) {
         if (!was_active[b]) continue;
-        const int32_t c = m0->h_sysi[b * kSysStride + SI_CONV];
-        const int32_t its = c >= 0 ? c : it;
+        const int32_t *si = m0->h_sysi + b * kSysStride;
+        const int32_t c = si[SI_CONV];
+        const int32_t its = c >= 0 ? c : (si[SI_FAILED] && si[SI_FAIL_WHY] != FW_MAXITER ? si[SI_FAIL_IT] + 1 : it);
         total += its;
         slowest = std::max(slowest, its);
         if (c >= 0) slowest_conv = std::max(slowest_conv, c);
@@ -1600,7 +1610,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, int32_t max_
 }  // namespace
 
 int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
-                       int32_t *max_iters) {
+                       int32_t *max_iters, const uint8_t *only) {
     const size_t L = d->parts.size();
     mof_mesh *m0 = d->parts[0];
     // records of workgroups past a part's own count must read as zero, and
@@ -1608,17 +1618,24 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
     MOF_HIP(hipMemsetAsync(d->part_pq.p, 0, d->part_pq.bytes(), s));
     MOF_HIP(hipMemsetAsync(d->part_rzrr.p, 0, d->part_rzrr.bytes(), s));
     MOF_HIP(hipMemsetAsync(d->part_rr0.p, 0, d->part_rr0.bytes(), s));
-    for (size_t l = 0; l < L; ++l) {
-        Workspace &w = d->parts[l]->ws;
-        k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
+    if (!only) {
+        for (size_t l = 0; l < L; ++l) {
+            Workspace &w = d->parts[l]->ws;
+            k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
+        }
+        MOF_HIP(hipGetLastError());
     }
-    MOF_HIP(hipGetLastError());
     for (int32_t b = 0; b < B; ++b) {
+        if (only && !only[b]) continue;
         int32_t *si = m0->h_sysi + b * kSysStride;
         for (int k = 0; k < kSysStride; ++k) si[k] = 0;
         si[SI_ACTIVE] = 1;
         si[SI_CONV] = -1;
     }
+    if (only)  // every part holds the same flags (all take the same decisions)
+        for (size_t l = 0; l < L; ++l)
+            MOF_HIP(hipMemcpyAsync(d->parts[l]->ws.sysi.p, m0->h_sysi, sizeof(int32_t) * kSysStride * B,
+                                   hipMemcpyHostToDevice, s));
     if (m0->iter_hint.size() < 2 * 16) m0->iter_hint.assign(2 * 16, 0);
     bool amg = sp.amg && sp.precision == MOF_PREC_MIXED;
     for (size_t l = 0; l < L && amg; ++l) amg = amg_build(d->parts[l]);
@@ -1631,10 +1648,10 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
     int32_t o = 0;
     for (; o < sp.max_outer; ++o) {
         if (sp.precision == MOF_PREC_MIXED)
-            iters += pcg_dd<float>(d, B, o == 0, sp.inner_rtol, sp.max_iter, s, max_iters,
+            iters += pcg_dd<float>(d, B, o == 0, sp.inner_rtol, sp, s, max_iters,
                                    &m0->iter_hint[16 + std::min(o, 15)], amg);
         else
-            iters += pcg_dd<double>(d, B, o == 0, o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp.max_iter, s,
+            iters += pcg_dd<double>(d, B, o == 0, o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s,
                                     max_iters, &m0->iter_hint[std::min(o, 15)], false);
         for (size_t l = 0; l < L; ++l) {
             mof_mesh *m = d->parts[l];

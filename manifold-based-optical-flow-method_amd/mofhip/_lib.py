@@ -19,6 +19,9 @@ CSRC_DIR = os.path.join(ROOT_DIR, "csrc")
 # MOFHIP_LIB: another in-tree build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("MOFHIP_LIB") or os.path.join(PKG_DIR, "libmofhip.so")
 
+# include/mof.h MOF_ABI_VERSION this binding's structs follow
+MOF_ABI_VERSION = 2
+
 MOF_OK = 0
 MOF_E_ARG = -1
 MOF_E_HIP = -2
@@ -42,7 +45,7 @@ MOF_CSR_A_LAST = 1
 
 # every symbol include/mof.h declares
 EXPORTS = (
-    "mof_version", "mof_last_error", "mof_device_count", "mof_mesh_create",
+    "mof_version", "mof_abi_version", "mof_last_error", "mof_device_count", "mof_mesh_create", "mof_mesh_clone",
     "mof_mesh_destroy", "mof_mesh_get_info", "mof_geometry_export", "mof_csr_export",
     "mof_assemble", "mof_solve_range", "mof_bench_spmv", "mof_velocity_vectors",
     "mof_csv_write", "mof_csv_shape", "mof_csv_read", "mof_ply_info", "mof_ply_read",
@@ -151,9 +154,11 @@ def lib():
                                  ctypes.c_int64, ctypes.c_double)
         sig = {
             "mof_version": ([], ctypes.c_char_p),
+            "mof_abi_version": ([], ctypes.c_int),
             "mof_last_error": ([], ctypes.c_char_p),
             "mof_device_count": ([P], ctypes.c_int),
             "mof_mesh_create": ([P, P, P, P, i32, i32, i32, u32, P], ctypes.c_int),
+            "mof_mesh_clone": ([P, i32, P], ctypes.c_int),
             "mof_mesh_destroy": ([P], ctypes.c_int),
             "mof_mesh_get_info": ([P, P], ctypes.c_int),
             "mof_geometry_export": ([P, P, P, P], ctypes.c_int),
@@ -193,6 +198,13 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        # the library writes whole mof_stats / mof_mesh_info structs: a
+        # library of another ABI would overrun (or under-fill) these
+        if not os.environ.get("MOFHIP_LIB"):
+            abi = L.mof_abi_version() if hasattr(L, "mof_abi_version") else 1
+            if abi != MOF_ABI_VERSION:
+                raise ImportError("libmofhip.so has ABI %d, this binding needs %d (rebuild: make -C %s)"
+                                  % (abi, MOF_ABI_VERSION, CSRC_DIR))
         _lib = L
     return _lib
 

@@ -53,13 +53,23 @@ def plan_info(triangles, N: int, part) -> dict:
 class HostTransport:
     """mof_dd_transport over a torch.distributed group (gloo, CPU tensors):
     the all-gather of partial records / owned V and the neighbour exchange of
-    packed halo segments, called from inside the solver loop."""
+    packed halo segments, called from inside the solver loop.
+
+    Errors end the solve on every rank, not only on the rank that saw them:
+    a local failure inside an exchange (copying a segment in or out) still
+    completes that exchange's sends and receives with placeholder bytes, and
+    every all-gather carries a status byte, so the next all-gather (the solver
+    runs one after every exchange) returns failure on all ranks at the same
+    call. A failure of the transport itself (a peer gone) can only end at the
+    process group's timeout: create the group with a short ``timeout`` for
+    this transport."""
 
     def __init__(self, group=None):
         import torch
         import torch.distributed as dist
         self._dist, self._torch, self.group = dist, torch, group
         self.world = dist.get_world_size(group)
+        self._failed = False  # a local error waiting to be reported to every rank
         self._ag = L.ALLGATHER_FN(self._allgather)
         self._ex = L.EXCHANGE_FN(self._exchange)
         self.struct = L.MofDdTransport(None, self._ag, self._ex)
@@ -71,24 +81,39 @@ class HostTransport:
         return self._dist.get_global_rank(g, int(r))
 
     def _allgather(self, ctx, send, recv, nbytes):
+        t = self._torch
         try:
-            t = self._torch
-            src = t.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=t.uint8)
-            out = [t.empty(nbytes, dtype=t.uint8) for _ in range(self.world)]
+            src = t.zeros(nbytes + 1, dtype=t.uint8)
+            try:
+                src[1:] = t.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=t.uint8)
+            except Exception:
+                self._failed = True
+            src[0] = 1 if self._failed else 0
+            out = [t.empty(nbytes + 1, dtype=t.uint8) for _ in range(self.world)]
             self._dist.all_gather(out, src, group=self.group)
-            for r, o in enumerate(out):
-                ctypes.memmove(recv + r * nbytes, o.data_ptr(), nbytes)
-            return 0
-        except Exception:  # reported as a status to the library
+        except Exception:  # the transport itself failed
             return 1
+        if any(int(o[0]) for o in out):
+            self._failed = False
+            return 1  # some rank failed: every rank reports it at this call
+        try:
+            for r, o in enumerate(out):
+                ctypes.memmove(recv + r * nbytes, o.data_ptr() + 1, nbytes)
+        except Exception:
+            return 1  # local only, after the collective: the peers are not blocked
+        return 0
 
     def _exchange(self, ctx, n, peers, send, sbytes, recv, rbytes):
+        t = self._torch
         try:
-            t = self._torch
             reqs, bufs = [], []
             for k in range(n):
                 if sbytes[k]:
-                    st = t.frombuffer(bytearray(ctypes.string_at(send[k], sbytes[k])), dtype=t.uint8)
+                    try:
+                        st = t.frombuffer(bytearray(ctypes.string_at(send[k], sbytes[k])), dtype=t.uint8)
+                    except Exception:
+                        self._failed = True
+                        st = t.zeros(sbytes[k], dtype=t.uint8)
                     reqs.append(self._dist.isend(st, self._peer(peers[k]), group=self.group))
                 if rbytes[k]:
                     rt = t.empty(rbytes[k], dtype=t.uint8)
@@ -96,11 +121,14 @@ class HostTransport:
                     reqs.append(self._dist.irecv(rt, self._peer(peers[k]), group=self.group))
             for q in reqs:
                 q.wait()
+        except Exception:  # the transport itself failed
+            return 1
+        try:
             for k, rt in bufs:
                 ctypes.memmove(recv[k], rt.data_ptr(), rbytes[k])
-            return 0
         except Exception:
-            return 1
+            self._failed = True
+        return 0
 
 
 class DecomposedMesh:

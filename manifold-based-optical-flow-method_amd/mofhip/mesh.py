@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import time
 
 import numpy as np
 
@@ -44,25 +45,71 @@ class DeviceMesh:
         self.reorder = bool(reorder)  # RCM vertex order on the device (results unaffected)
         self._handles = {}
         self._locks = {}
-        self._glock = threading.Lock()
+        self._build_locks = {}
+        self._glock = threading.Lock()  # guards the dicts only; builds run outside it
+        self.build_seconds = {}  # wall seconds of each handle's build (per device)
         self.device = int(device)
         self.handle(self.device)
 
     # -- handles ---------------------------------------------------------
     def handle(self, device: int | None = None) -> ctypes.c_void_p:
+        """The handle on ``device``, built on first use: the primary device's
+        with ``mof_mesh_create`` (host pattern, orders, the per-mesh kernels),
+        every other device's with ``mof_mesh_clone`` of it (the host state
+        and multigrid hierarchy are shared, only uploads and the per-mesh
+        kernels run). Builds of different devices run concurrently; only the
+        same device's build is serialised."""
         device = self.device if device is None else int(device)
+        h = self._handles.get(device)
+        if h is not None:
+            return h
         with self._glock:
+            blk = self._build_locks.setdefault(device, threading.Lock())
+        with blk:
             h = self._handles.get(device)
-            if h is None:
-                h = ctypes.c_void_p()
+            if h is not None:
+                return h
+            t0 = time.perf_counter()
+            h = ctypes.c_void_p()
+            if device != self.device:
+                src = self.handle(self.device)
+                L.check(L.lib().mof_mesh_clone(src, device, ctypes.byref(h)))
+            else:
                 flags = ((L.MOF_GEOM_F32_POINTS if self.f32_points else 0)
                          | (0 if self.reorder else L.MOF_NO_REORDER))
                 L.check(L.lib().mof_mesh_create(
                     L.ptr(self._xyz), L.ptr(self._nrm), L.ptr(self._tri), L.ptr(self._area),
                     self.N, self.M, device, flags, ctypes.byref(h)))
-                self._handles[device] = h
+            with self._glock:
+                self.build_seconds[device] = time.perf_counter() - t0
                 self._locks[device] = threading.Lock()
+                self._handles[device] = h
         return h
+
+    def prepare(self, devices) -> dict:
+        """Build the handles of ``devices`` that do not exist yet, concurrently
+        (one host thread per device; ctypes releases the GIL). Returns the
+        build seconds per device."""
+        todo = [int(d) for d in dict.fromkeys(devices) if int(d) not in self._handles]
+        if self.device in todo:  # the clones need the primary handle
+            self.handle(self.device)
+            todo.remove(self.device)
+        errors = []
+
+        def run(d):
+            try:
+                self.handle(d)
+            except BaseException as exc:  # re-raised below
+                errors.append(exc)
+
+        threads = [threading.Thread(target=run, args=(d,)) for d in todo]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
+        return dict(self.build_seconds)
 
     def lock(self, device: int | None = None) -> threading.Lock:
         device = self.device if device is None else int(device)
@@ -71,9 +118,10 @@ class DeviceMesh:
 
     def close(self):
         with self._glock:
-            for h in self._handles.values():
-                L.lib().mof_mesh_destroy(h)
+            hs = list(self._handles.values())
             self._handles.clear()
+        for h in hs:
+            L.lib().mof_mesh_destroy(h)
 
     def __del__(self):
         try:

@@ -29,6 +29,7 @@ def shard_ranges(k0: int, k1: int, parts: int):
 def velocity_field_sharded(mesh, I, t_k, k0, k1, lambda_, I2=None, devices=(0,), **opts):
     """Solve k in [k0, k1) on ``devices``; returns (V (k1-k0, 2N), [stats per device])."""
     devices = list(devices) or [mesh.device]
+    mesh.prepare(devices)  # concurrent handle builds (clones share the host state)
     ranges = shard_ranges(k0, k1, len(devices))
     V = np.empty((max(k1 - k0, 0), 2 * mesh.N))
     stats = [None] * len(devices)

@@ -124,6 +124,9 @@ def compute_velocity_field(processes_num, time_steps, a2, grad_w, e, integral_wi
     I = np.ascontiguousarray(np.asarray(I_k, dtype=np.float64)[:time_steps])
     I2 = np.ascontiguousarray(np.asarray(I_k_2, dtype=np.float64)[:time_steps])
     tk = np.asarray(t_k, dtype=np.float64)
+    # one handle per GPU, built concurrently before the clock starts -- as the
+    # reference creates its Pool(processes_num) before start_time (:155-158)
+    mesh.prepare(range(ndev))
     start = time.time()
     V, stats = velocity_field_sharded(mesh, I, tk, 0, max(K, 0), lambda_, I2=I2,
                                       devices=range(ndev), **_solver_options())

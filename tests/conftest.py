@@ -57,3 +57,12 @@ def _torch_hip_first(request):
         except Exception:
             pass
     yield
+
+
+def assert_csr_equal(A, ref):
+    """Bit-identical canonical CSR (sorted indices)."""
+    A.sort_indices()
+    assert A.shape == ref.shape
+    assert np.array_equal(A.indptr, ref.indptr)
+    assert np.array_equal(A.indices, ref.indices)
+    assert np.array_equal(A.data, ref.data)

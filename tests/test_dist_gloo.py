@@ -129,3 +129,59 @@ def test_bench_gpus_must_match_world_size():
     out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--no-cpu-baseline"],
                          env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def _transport_worker(rank, world, port, out):
+    """HostTransport callbacks driven directly (no device): rank 1 fails while
+    copying its send segment; the exchange still completes on both ranks and
+    the next all-gather reports the failure on every rank."""
+    import ctypes
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "manifold-based-optical-flow-method_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mofhip import decomp
+    tr = decomp.HostTransport()
+    nb = 16
+    send = (ctypes.c_uint8 * nb)(*([rank + 1] * nb))
+    recv = (ctypes.c_uint8 * nb)()
+    gat = (ctypes.c_uint8 * (world * nb))()
+    peers = (ctypes.c_int32 * 1)(1 - rank)
+    sp = (ctypes.c_void_p * 1)(ctypes.addressof(send))
+    rp = (ctypes.c_void_p * 1)(ctypes.addressof(recv))
+    sz = (ctypes.c_int64 * 1)(nb)
+    ok0 = tr._allgather(None, ctypes.addressof(send), ctypes.addressof(gat), nb)
+    first = bytes(gat)
+    if rank == 1:  # a local failure while reading the send segment
+        real = ctypes.string_at
+        decomp.ctypes.string_at = lambda *a: (_ for _ in ()).throw(RuntimeError("boom"))
+    ex = tr._exchange(None, 1, peers, sp, sz, rp, sz)
+    if rank == 1:
+        decomp.ctypes.string_at = real
+    got = bytes(recv)
+    ag = tr._allgather(None, ctypes.addressof(send), ctypes.addressof(gat), nb)
+    ag2 = tr._allgather(None, ctypes.addressof(send), ctypes.addressof(gat), nb)  # cleared afterwards
+    out.put((rank, ok0, first, ex, got, ag, ag2))
+    dist.destroy_process_group()
+
+
+def test_host_transport_failure_reaches_every_rank():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok0, first, ex, got, ag, ag2 in res:
+        assert ok0 == 0 and first == bytes([1] * 16 + [2] * 16)
+        assert ex == 0  # the exchange completed on both ranks (nobody left blocked)
+        assert ag == 1, rank  # ... and the failure surfaces on every rank at the same call
+        assert ag2 == 0
+    assert res[1][4] == bytes([1] * 16)  # rank 1 received rank 0's segment
+    assert res[0][4] == bytes(16)  # rank 0 received the placeholder

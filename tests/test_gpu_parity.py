@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import golden_csr, load_golden
+from conftest import assert_csr_equal, golden_csr, load_golden
 from mofhip import DeviceMesh, velocity_field_sharded
 from mofhip import synth
 
@@ -23,14 +23,6 @@ VTOL = 1e-6
 
 def make_mesh(g, reorder=True):
     return DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"], reorder=reorder)
-
-
-def assert_csr_equal(A, ref):
-    A.sort_indices()
-    assert A.shape == ref.shape
-    assert np.array_equal(A.indptr, ref.indptr)
-    assert np.array_equal(A.indices, ref.indices)
-    assert np.array_equal(A.data, ref.data)
 
 
 @pytest.mark.parametrize("reorder", [True, False])
@@ -266,3 +258,33 @@ def test_s3_sequence_dropin(tmp_path):
     V_c = np.sqrt(np.sum(V_k_coord[:, :, :3] ** 2, axis=2))
     assert V_c.shape == g6["V_c"].shape
     assert np.abs(V_c - g6["V_c"]).max() < VTOL
+
+
+def test_mesh_clone_bit_identical():
+    """mof_mesh_clone (the extra devices of a sharded compute_velocity_field)
+    shares the source's host pattern and multigrid hierarchy: its geometry,
+    a2 and V are bit-identical to the mof_mesh_create handle's (cloned onto
+    the same GPU here: the box has one)."""
+    import ctypes
+    import threading
+    from mofhip import _lib as L
+    g = load_golden("G1_ico642")
+    m = make_mesh(g)
+    I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    V0, s0 = m.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg")
+    h2 = ctypes.c_void_p()
+    L.check(L.lib().mof_mesh_clone(m.handle(), 0, ctypes.byref(h2)))
+    m._handles[99], m._locks[99] = h2, threading.Lock()  # a second handle under a spare key
+    info = m.info(99)
+    assert info["ms_pattern"] == 0.0 and info["nblocks"] == m.info()["nblocks"]
+    V1, s1 = m.solve_range(I, tk, 0, 15, lam, precision="mixed", precond="amg", device=99)
+    assert np.array_equal(V0, V1) and s0["iterations"] == s1["iterations"]
+    e0 = np.empty((m.N, 2, 3))
+    e1 = np.empty((m.N, 2, 3))
+    L.check(L.lib().mof_geometry_export(m.handle(), L.ptr(e0), None, None))
+    L.check(L.lib().mof_geometry_export(h2, L.ptr(e1), None, None))
+    assert np.array_equal(e0, e1)
+    V2, _ = velocity_field_sharded(m, I, tk, 0, 15, lam, devices=[0, 99], precision="f64")
+    V3, _ = m.solve_range(I, tk, 0, 15, lam, precision="f64")
+    assert np.array_equal(V2, V3)
+    assert np.abs(V1 - g["V_k"]).max() < VTOL
