@@ -201,7 +201,7 @@ void mesh_set_own(mof_mesh *m, int32_t nown) {
     m->n_own = nown;
     // MOF_SYM_READS: 1 / 0 force the symmetric / plain reads, unset: per mesh
     const char *env = std::getenv("MOF_SYM_READS");
-    const int sym = !MOF_SYM_A ? 0 : env && *env ? (std::atoi(env) != 0) : -1;
+    const int sym = env && *env ? (std::atoi(env) != 0) : -1;
     // one host mirror table per (mesh, nown, mode), shared by the clones
     std::shared_ptr<const MirrorTable> mt;
     {

@@ -104,8 +104,7 @@ struct AmgDevice {
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)
-    DevArray<uint32_t> D0h;  // [B][N][2] level-0 2x2 D^-1 in bf16
-    bool bf16_fresh = false;  // A0h / D0h written by the batch's assembly
+    bool bf16_fresh = false;  // A0h written by the batch's assembly
 };
 
 }  // namespace mof

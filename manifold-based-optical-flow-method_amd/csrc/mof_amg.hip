@@ -21,11 +21,11 @@
 //                 k_post0 / k_post3  y_l = x_l + w D^-1 (b_l - A_l x_l); at
 //                                  level 0 y = z and the partial r.z of the PCG
 // Every launch covers all B systems and skips retired systems. Level 0 sweeps
-// bf16 copies of the inner solver's SELL A and 2x2 D^-1, written by the
-// assembly (k_assemble_mixed), in the PCG row-kernel layout (XCD-aware,
+// a bf16 copy of the inner solver's SELL A (its diagonal blocks give the
+// smoother's D), written by the assembly, in the PCG row-kernel layout (XCD-aware,
 // batched loads); coarse levels keep fp32 3x3 blocks (12 floats, rows padded
 // to 4) for the Galerkin products and int8 copies (9 codes + a bf16 scale,
-// 12 B per block, st_a9; bf16 with MOF_COARSE_I8=0) for the sweeps, vectors
+// 12 B per block, st_a9) for the sweeps, vectors
 // as float4. All sums run in a fixed order: the cycle is
 // deterministic and independent of B.
 #include <algorithm>
@@ -135,24 +135,18 @@ __device__ __forceinline__ void st_h9(uint4 *H, uint16_t *H22, int64_t q, const 
     H22[q] = (uint16_t)bf16_bits(c[2][2]);
 }
 
-// The coarse levels' sweep copy of A (levels >= 1 except the coarsest).
-// MOF_COARSE_I8 = 1: 12 B per 3x3 block, the 9 entries as offset-binary int8
-// (q + 128) with one bf16 scale per block (s = max |a| / 127): H viewed as
-// uint2[] (entries 0..7), H22 as uint32_t[] (entry 8 | scale << 16). A block
-// and its transposed twin have the same entries, so the same scale and the
-// same codes: the preconditioner stays symmetric. 0: bf16 entries, 18 B per
-// block (st_h9 / ld_h9).
-#ifndef MOF_COARSE_I8
-#define MOF_COARSE_I8 1
-#endif
-constexpr bool kCoarseI8 = MOF_COARSE_I8 != 0;
+// The coarse levels' sweep copy of A (levels >= 1 except the coarsest):
+// 12 B per 3x3 block, the 9 entries as offset-binary int8 (q + 128) with one
+// bf16 scale per block (s = max |a| / 127): H viewed as uint2[] (entries
+// 0..7), H22 as uint32_t[] (entry 8 | scale << 16). A block and its
+// transposed twin have the same entries, so the same scale and the same
+// codes: the preconditioner stays symmetric (round 2: 18 B bf16 entries
+// before, level-1 k_res3 / k_post3 442 / 430 -> 360 / 337 us, C3 +1.6 %).
 // uint32 words of Ah and uint16 words of Ah22 per block
-constexpr size_t kAhWords = kCoarseI8 ? 2 : 4, kAh22Words = kCoarseI8 ? 2 : 1;
+constexpr size_t kAhWords = 2, kAh22Words = 2;
 
 __device__ __forceinline__ void st_a9(uint4 *H, uint16_t *H22, int64_t q, const float (&c)[3][3]) {
-    if constexpr (!kCoarseI8) {
-        st_h9(H, H22, q, c);
-    } else {
+    {
         float m = 0.f;
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -176,12 +170,6 @@ __device__ __forceinline__ void st_a9(uint4 *H, uint16_t *H22, int64_t q, const 
 
 // ---- per-timestep setup --------------------------------------------------
 
-__global__ __launch_bounds__(kWG) void k_to_bf16(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
-    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
-    if (q >= n) return;
-    const float4 v = A[q];
-    H[q] = make_uint2(bf16_bits(v.x) | (bf16_bits(v.y) << 16), bf16_bits(v.z) | (bf16_bits(v.w) << 16));
-}
 // A32 -> the level-0 sweep copy (h0_st)
 __global__ __launch_bounds__(kWG) void k_to_h0(int64_t n, const float4 *__restrict__ A, uint2 *__restrict__ H) {
     const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
@@ -321,16 +309,11 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
 // applied to the fine blocks of every system (level 0 has 7.5x the entries
 // with a smoothed prolongator). Fine blocks from the smoother's bf16 copy
 // (Afh) or the fp32 A (Af); same fold order per system as galerkin_block.
-#ifndef MOF_GAL_NS
-#define MOF_GAL_NS 1
-#endif
-// systems per thread: C3 (512 systems) 6.08 ms per launch at 4, 8.06 at 8,
+// Systems per thread: C3 (512 systems) 6.08 ms per launch at 4, 8.06 at 8,
 // 14.7 at 16 (the per-system fine-block gathers, not the shared gather
-// lists, bound it; more systems per thread only lower the occupancy)
-#ifndef MOF_GAL_NSYS
-#define MOF_GAL_NSYS 4
-#endif
-constexpr int kGalNS = MOF_GAL_NSYS;
+// lists, bound it; more systems per thread only lower the occupancy); one
+// system per thread (k_galerkin<2>): 9.02 ms.
+constexpr int kGalNS = 4;
 __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
@@ -541,9 +524,7 @@ __device__ __forceinline__ void ld_h9(const uint4 *H, const uint16_t *H22, int64
 }
 // block q of a coarse level's sweep copy (st_a9)
 __device__ __forceinline__ void ld_a9(const uint4 *H, const uint16_t *H22, int64_t q, float (&a)[3][3]) {
-    if constexpr (!kCoarseI8) {
-        ld_h9(H, H22, q, a);
-    } else {
+    {
         const uint2 h = reinterpret_cast<const uint2 *>(H)[q];
         const uint32_t t = reinterpret_cast<const uint32_t *>(H22)[q];
         const float sc = bf16_hi(t);
@@ -556,27 +537,6 @@ __device__ __forceinline__ void ld_a9(const uint4 *H, const uint16_t *H22, int64
 // the smoother's 3x3 D^-1 of node i of system b
 __device__ __forceinline__ void ld_dh(const Lvl &L, int32_t b, int32_t i, float (&d)[3][3]) {
     ld_h9(L.Dh, L.Dh22, (int64_t)b * L.n + i, d);
-}
-
-// Level 0: r1 = r - A x0 (x0 = w D^-1 r from the PCG update), stored at the
-// member position of each vertex. PCG row layout, XCD-aware grid.
-__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0(int32_t N, int32_t nblk, int32_t B, MatH mat,
-                                              const float *__restrict__ rv, const float *__restrict__ xv,
-                                              const int32_t *__restrict__ apos,
-                                              const int32_t *__restrict__ sysi, float *__restrict__ r1) {
-    int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b, kGrpSmooth) || retired(sysi, b)) return;
-    const int64_t vb = (int64_t)b * N;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
-        if (i >= N) break;
-        float y0, y1;
-        spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1);
-        const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-        reinterpret_cast<uint32_t *>(r1)[vb + (apos ? apos[i] : i)] =
-            bf16_bits(ri.x - y0) | (bf16_bits(ri.y - y1) << 16);
-    }
 }
 
 // (A x)_i of a coarse level, slots U at a time with all loads of a chunk
@@ -625,16 +585,12 @@ __device__ __forceinline__ void res3_node(const Lvl &L, int32_t b, int32_t i) {
     stv<3>(L.r + vo, L.apos[i], ri);
 }
 
-// MOF_R1_NATURAL = 1 stores level 0's restricted residual r1 in node order
-// (k_res0's stores coalesced instead of scattered into member order: 1053
-// -> 961 us) and lets the restriction gather member q's value at mlist[q]
-// (233 -> 361 us): a net loss, so r1 stays in member order (C3, B = 512).
-#ifndef MOF_R1_NATURAL
-#define MOF_R1_NATURAL 0
-#endif
+// Level 0's restricted residual r1 stays in aggregate member order (k_res0
+// scatters into it): node order made k_res0's stores coalesced (1053 -> 961
+// us) but the restriction's member gathers scattered (233 -> 361 us), a net
+// loss (round 2, C3, B = 512).
 template <int BSF>
-__device__ __forceinline__ int32_t r_at(const Lvl &F, int32_t q) {
-    if constexpr (BSF == 2 && MOF_R1_NATURAL) return F.mlist[q];
+__device__ __forceinline__ int32_t r_at(const Lvl &, int32_t q) {
     return q;
 }
 
@@ -733,12 +689,10 @@ __global__ __launch_bounds__(kWG) void k_res3(Lvl L, const int32_t *__restrict__
 constexpr int kRG = 1024;
 
 // NS systems per workgroup share each member's Q row load; the contributions
-// of all NS systems are staged in LDS (level 0: MOF_RESTR_S = 2, C3 232 ->
+// of all NS systems are staged in LDS (level 0: NS = kRestrS = 2, C3 232 ->
 // 194 us per 512-system launch; NS = 4: 235 us, its 48-KB LDS stage lowers
 // the occupancy).
-#ifndef MOF_RESTR_S
-#define MOF_RESTR_S 2
-#endif
+constexpr int kRestrS = 2;
 template <int BSF, int NS = 1>
 __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
                                                   int32_t B, int32_t smooth, float omega,
@@ -955,13 +909,7 @@ __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__
 // dependent agg -> y gather and little else (latency-bound), and the
 // systems of a thread share the node's agg and Q row loads. C3, 512
 // systems: 314 us (1 x 1), 270 (4 nodes), 231 (2 x 2), 202 (1 x 4), 210 (1 x 8)
-#ifndef MOF_PROL_R
-#define MOF_PROL_R 1
-#endif
-#ifndef MOF_PROL_S
-#define MOF_PROL_S 4
-#endif
-constexpr int kProlR = MOF_PROL_R, kProlS = MOF_PROL_S;
+constexpr int kProlR = 1, kProlS = 4;
 template <int XM>
 __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, int32_t B,
                                                   const int32_t *__restrict__ sysi) {
@@ -1085,17 +1033,11 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
     }
 }
 
-// Level 0: z = x + w D^-1 (r - A x) and the PCG's partial r.z (component 0
-// of the row block's record). PCG row layout, XCD-aware grid.
-// k_res0 with NS systems per thread sharing the row's column / mirror loads
-// (MOF_RES0_NS): grid over (row block, system group of NS) in the XCD order.
-#ifndef MOF_RES0_NS
-#define MOF_RES0_NS 2
-#endif
-constexpr int kRes0NS = MOF_RES0_NS;
-#ifndef MOF_RES0_U
-#define MOF_RES0_U MOF_SWEEP_U
-#endif
+// Level 0: r1 = r - A x0 (x0 = w D^-1 r from the PCG update), stored at the
+// member position of each vertex; PCG row layout. NS systems per thread sharing the row's column / mirror loads:
+// grid over (row block, system group of NS) in the XCD order (round 2: 916
+// -> 829 us per 512-system launch at NS = 2; 4 lowered the occupancy).
+constexpr int kRes0NS = 2, kRes0U = kSweepU;
 template <int NS>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
                                                  const float *__restrict__ rv, const float *__restrict__ xv,
@@ -1121,10 +1063,10 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t 
         if (i >= N) break;
         float y[NS][2];
         auto xl = [&](int t, int32_t j) { return ld_x0(xv, (int64_t)bs[t] * N + j); };
-        if (MOF_SYM_A && mat.sell_mir)
-            spmv_row_hx_ns<(bool)MOF_SYM_A, NS, MOF_RES0_U>(mat, bs, i, xl, y);
+        if (mat.sell_mir)
+            spmv_row_hx_ns<true, NS, kRes0U>(mat, bs, i, xl, y);
         else
-            spmv_row_hx_ns<false, NS, MOF_RES0_U>(mat, bs, i, xl, y);
+            spmv_row_hx_ns<false, NS, kRes0U>(mat, bs, i, xl, y);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
             if (!act[t]) continue;
@@ -1136,18 +1078,13 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t 
     }
 }
 
-// k_post0 with NS systems per thread sharing the row's column / mirror loads
-// (MOF_POST0_NS), same per-system arithmetic and partials as k_post0.
-#ifndef MOF_POST0_NS
-#define MOF_POST0_NS 2
-#endif
-constexpr int kPost0NS = MOF_POST0_NS;
-#ifndef MOF_POST0_U
-#define MOF_POST0_U 4
-#endif
+// Level 0's post-smoothing z = x + w D^-1 (r - A x) and the PCG's partial
+// r.z, NS systems per thread sharing the row's column / mirror loads, 4 slots
+// per load batch to keep the waves (round 2: 918 -> 864 us per 512-system
+// launch; 8 slots per batch 1030 us). D^-1 from the row's own diagonal block.
+constexpr int kPost0NS = 2, kPost0U = 4;
 template <int XM, bool ZH, int NS>
 __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
-                                                  const uint2 *__restrict__ Dh,
                                                   const float *__restrict__ rv,
                                                   const float *__restrict__ xv, float omega,
                                                   const int32_t *__restrict__ sysi,
@@ -1184,17 +1121,16 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t
             else
                 return ld_x0(xv, vj);
         };
-        if (MOF_SYM_A && mat.sell_mir)
-            spmv_row_hx_ns<(bool)MOF_SYM_A, NS, MOF_POST0_U>(mat, bs, i, xl, y, dg);
+        if (mat.sell_mir)
+            spmv_row_hx_ns<true, NS, kPost0U>(mat, bs, i, xl, y, dg);
         else
-            spmv_row_hx_ns<false, NS, MOF_POST0_U>(mat, bs, i, xl, y, dg);
+            spmv_row_hx_ns<false, NS, kPost0U>(mat, bs, i, xl, y, dg);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
             const int64_t vb = (int64_t)bs[t] * N;
             const float2 xi = xl(t, i);
             const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-            const float2 ds = MOF_DINV_FROM_A ? bf16_diag_solve(dg[t], ri.x - y[t][0], ri.y - y[t][1])
-                                              : bf16_mat2(Dh[vb + i], ri.x - y[t][0], ri.y - y[t][1]);
+            const float2 ds = bf16_diag_solve(dg[t], ri.x - y[t][0], ri.y - y[t][1]);
             float z0 = xi.x + omega * ds.x;
             float z1 = xi.y + omega * ds.y;
             if constexpr (ZH) {
@@ -1216,63 +1152,10 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t
     }
 }
 
-template <int XM, bool ZH>
-__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0(int32_t N, int32_t nblk, int32_t B, MatH mat,
-                                               const uint2 *__restrict__ Dh,
-                                               const float *__restrict__ rv,
-                                               const float *__restrict__ xv, float omega,
-                                               const int32_t *__restrict__ sysi,
-                                               float *__restrict__ zv, double *__restrict__ part,
-                                               RedArgs rd) {
-    __shared__ double lds[8];
-    int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b, kGrpSmooth) || retired(sysi, b)) return;
-    const int64_t vb = (int64_t)b * N;
-    double rz = 0.0;
-#pragma unroll
-    for (int g = 0; g < kRows; ++g) {
-        const int32_t i = rb * kRowsPerWG + g * kWG + threadIdx.x;
-        if (i >= N) break;
-        float y0, y1;
-        float2 xi;
-        uint2 dg;  // the row's diagonal block (slot 0), kept from the SpMV
-        if constexpr (XM == 2) {
-            spmv_row_h(mat, b, i, xv + 2 * vb, y0, y1, &dg);
-            xi = reinterpret_cast<const float2 *>(xv)[vb + i];
-        } else {
-            spmv_row_hx(mat, b, i, [&](int32_t j) { return ld_x0(xv, vb + j); }, y0, y1, &dg);
-            xi = ld_x0(xv, vb + i);
-        }
-        const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-        const float2 ds = MOF_DINV_FROM_A ? bf16_diag_solve(dg, ri.x - y0, ri.y - y1)
-                                          : bf16_mat2(Dh[vb + i], ri.x - y0, ri.y - y1);
-        float z0 = xi.x + omega * ds.x;
-        float z1 = xi.y + omega * ds.y;
-        if constexpr (ZH) {  // bf16 z: r.z of the rounded values the PCG uses
-            const uint32_t h = bf16_bits(z0) | (bf16_bits(z1) << 16);
-            reinterpret_cast<uint32_t *>(zv)[vb + i] = h;
-            z0 = bf16_lo(h);
-            z1 = bf16_hi(h);
-        } else {
-            reinterpret_cast<float2 *>(zv)[vb + i] = make_float2(z0, z1);
-        }
-        if (i < rd.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
-    }
-    double v[1] = {rz};
-    block_sum<1>(v, lds);
-    if (threadIdx.x == 0) part[2 * (((int64_t)rd.part * B + b) * rd.nmax + rb)] = v[0];
-}
-
-// k_post0 (one system per thread) or k_post0_ns (kPost0NS systems)
 template <int XM, bool ZH, typename... Args>
-void launch_post0(dim3 gx, int32_t nblk, int32_t B, hipStream_t s, int32_t n, int32_t nblk_, int32_t B_,
-                  Args... args) {
-    if constexpr (kPost0NS > 1) {
-        const dim3 g(xcd_grid(nblk, (B + kPost0NS - 1) / kPost0NS, kGrpSmooth > kPost0NS ? kGrpSmooth / kPost0NS : 1));
-        k_post0_ns<XM, ZH, kPost0NS><<<g, kWG, 0, s>>>(n, nblk_, B_, args...);
-    } else {
-        k_post0<XM, ZH><<<gx, kWG, 0, s>>>(n, nblk_, B_, args...);
-    }
+void launch_post0(int32_t nblk, int32_t B, hipStream_t s, Args... args) {
+    const dim3 g(xcd_grid(nblk, (B + kPost0NS - 1) / kPost0NS, kGrpSmooth > kPost0NS ? kGrpSmooth / kPost0NS : 1));
+    k_post0_ns<XM, ZH, kPost0NS><<<g, kWG, 0, s>>>(args...);
 }
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
@@ -1308,7 +1191,7 @@ bool amg_build(mof_mesh *m) {
     MeshShared *sh = m->shared.get();
     char key[160];
     std::snprintf(key, sizeof(key), "%a/%a/%d/%d/%a/%d", (double)prm.omega, (double)prm.omega1, prm.smooth,
-                  prm.nown, (double)prm.smooth_omega, (int)(m->sym_reads && MOF_SKIP_LOWER));
+                  prm.nown, (double)prm.smooth_omega, (int)m->sym_reads);
     std::unique_lock<std::mutex> build_lock;
     std::shared_ptr<const AmgHierarchy> Hp;
     if (sh) {
@@ -1330,7 +1213,7 @@ bool amg_build(mof_mesh *m) {
             prm.a2 = a2.data();
         }
         std::vector<int32_t> mir;
-        if (m->sym_reads && MOF_SKIP_LOWER) {
+        if (m->sym_reads) {
             mir = sell_mirror(m->pat, m->n_own, 1, nullptr);
             prm.mirror = mir.data();
         }
@@ -1361,7 +1244,6 @@ bool amg_build(mof_mesh *m) {
     // (R3 as measured; 1.2 diverges there with the tentative P)
     if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = H.levels[0].smoothed ? 1.05f : 1.1f;
     if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
-    if (MOF_X0_BF16 == 0) G.xm = 1;  // all-fp32 build: x0 and x in place, both float2
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
@@ -1440,9 +1322,8 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.x.alloc(2 * n * B);
             if (G.xm == 2) D.y.alloc(2 * n * B);
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
-            G.A0h.alloc((size_t)(kH0HalfWords * m->pat.sell_nb() * B / 2));
+            G.A0h.alloc((size_t)(2 * m->pat.sell_nb() * B));  // 8 B per block
             G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
-            G.D0h.alloc(2 * n * B);
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
@@ -1469,13 +1350,12 @@ AmgBf16 amg_bf16_targets(mof_mesh *m, int32_t B) {
     AmgDevice &G = *m->amg;
     MOF_REQUIRE(G.cap >= B, "multigrid storage not sized for the batch");
     G.bf16_fresh = true;
-    return AmgBf16{reinterpret_cast<uint2 *>(G.A0h.p), reinterpret_cast<uint2 *>(G.D0h.p)};
+    return AmgBf16{reinterpret_cast<uint2 *>(G.A0h.p)};
 }
 
 AmgFine amg_fine(mof_mesh *m) {
     AmgDevice &G = *m->amg;
     AmgFine f;
-    f.D0h = G.D0h.p;
     f.A0h = G.A0h.p;
     f.sell_nb = m->pat.sell_nb();
     f.sell_off = m->sell_off.p;
@@ -1497,14 +1377,11 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
         const int64_t nb0 = m->pat.sell_nb() * B;
         k_to_h0<<<dim3((unsigned)((nb0 + kWG - 1) / kWG)), kWG, 0, s>>>(
             nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
-        const int64_t nd0 = (int64_t)m->N * B;
-        k_to_bf16<<<dim3((unsigned)((nd0 + kWG - 1) / kWG)), kWG, 0, s>>>(
-            nd0, reinterpret_cast<const float4 *>(w.dinv32.p), reinterpret_cast<uint2 *>(G.D0h.p));
     }
     G.bf16_fresh = false;
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
-        if (l == 0 && MOF_GAL_NS)
+        if (l == 0)
             k_galerkin0_ns<<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGalNS - 1) / kGalNS,
                                            kGrpGal)),
                              kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p,
@@ -1512,16 +1389,6 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                           F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
                                               ? nullptr
                                               : reinterpret_cast<const uint2 *>(G.A0h.p));
-        else if (l == 0)
-            k_galerkin<2><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
-                                                              C.dead.p, F.gptr.p, F.gent.p, F.Q.p, w.A32.p,
-                                                              m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p,
-                                                              ah(C), ah22(C),
-                                                              // a smoothed P's product cancels far more (its
-                                                              // columns are A-smooth): fp32 blocks
-                                                              F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
-                                                                  ? nullptr
-                                                                  : reinterpret_cast<const uint2 *>(G.A0h.p));
         else
             k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
@@ -1571,7 +1438,6 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     const float om = G.omega;
     const float om1 = G.omega1;  // levels >= 1
     const MatH mat0 = level0_mat(m);
-    const dim3 gx(xcd_grid(nblk, B, kGrpSmooth));
     Lvl v[kMaxLevels];
     for (int32_t l = 0; l < L; ++l) v[l] = level_view(G.lv[l]);
     // levels S.. run fused in k_subcycle
@@ -1581,20 +1447,15 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = 0; l < S; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
-            if (kRes0NS > 1)
-                k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (B + kRes0NS - 1) / kRes0NS,
-                                                   kGrpSmooth > kRes0NS ? kGrpSmooth / kRes0NS : 1)),
-                                     kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
-                                                  MOF_R1_NATURAL || G.lv[0].smoothed ? nullptr : v[0].apos, sysi,
-                                                  v[0].r);
-            else
-                k_res0<<<gx, kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
-                                          MOF_R1_NATURAL || G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
+            k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (B + kRes0NS - 1) / kRes0NS,
+                                               kGrpSmooth > kRes0NS ? kGrpSmooth / kRes0NS : 1)),
+                                 kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
+                                              G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
             if (G.lv[0].smoothed) {
                 k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNS - 1) / kNS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             } else {
-                k_restrict<2, MOF_RESTR_S><<<dim3(xcd_grid(G.lv[0].ngrp, (B + MOF_RESTR_S - 1) / MOF_RESTR_S, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict<2, kRestrS><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kRestrS - 1) / kRestrS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             }
         } else {
@@ -1617,29 +1478,24 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
             const int32_t nb0p = (v[0].n + kWG * kProlR - 1) / (kWG * kProlR);
             const dim3 gsa(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), gp(xcd_grid(nb0p, (B + kProlS - 1) / kProlS, kGrpProl));
-            const uint2 *D0h = reinterpret_cast<const uint2 *>(G.D0h.p);
             if (G.xm == 2) {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
-                    launch_post0<2, true>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0, part_slot,
-                                                        rd);
+                    launch_post0<2, true>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
                 else
-                    launch_post0<2, false>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].y, om, sysi, z0,
-                                                         part_slot, rd);
+                    launch_post0<2, false>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
             } else {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
-                    launch_post0<1, true>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0, part_slot,
-                                                        rd);
+                    launch_post0<1, true>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
                 else
-                    launch_post0<1, false>(gx, nblk, B, s, v[0].n, nblk, B, mat0, D0h, r0, v[0].x, om, sysi, z0,
-                                                         part_slot, rd);
+                    launch_post0<1, false>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
             }
         } else {
             k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);

@@ -375,8 +375,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
     const int32_t *__restrict__ cptr, const int32_t *__restrict__ clist,
     const float *__restrict__ w12, const float *__restrict__ a2s, const float *__restrict__ u,
     const double *__restrict__ fc, int block_jacobi, float *__restrict__ A,
-    float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
-    uint2 *__restrict__ Dh, int32_t nown) {
+    float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah, int32_t nown) {
     int32_t tile, b;
     if (!xcd_map((int32_t)((sell_nb + kWG - 1) / kWG), B, tile, b, kGrpAsm)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
@@ -462,33 +461,13 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
         inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
     }
     const int64_t vi = (int64_t)b * N + i;
-    if (Dh)
-        Dh[vi] = i >= nown ? bf16x4(1.f, 0.f, 0.f, 1.f)
-                           : bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
-    else
+    // multigrid (Ah): the smoother's D comes from the bf16 diagonal blocks
+    if (!Ah)
         reinterpret_cast<float4 *>(dinv32)[vi] =
             make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
     *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
 }
 
-// Mixed-precision assembly by vertex rows (the PCG row layout and XCD-aware
-// (row block, system) order): thread i walks the incident triangles of
-// vertex i in the caller's triangle order (tinc, SELL-64) and adds each
-// triangle's three a1 terms of row i -- (i,i), (i,v_{a+1}), (i,v_{a+2}) --
-// to register accumulators of the row's SELL slots (tslot; WMAX >= the
-// widest row, unrolled predicated adds: no dynamic register indexing). A
-// triangle's 6 u values are one 24-B read per incident vertex instead of
-// two 8-B reads per term, and every row does the same work (the per-block
-// kernel's diagonal blocks fold every incident triangle, the others two).
-// Same results as k_assemble_mixed up to the fp32 summation order of a1
-// (the solve path's A32 is an fp32 fold either way); f is folded in fp64 in
-// the reference's triangle order, bit for bit.
-#ifndef MOF_ASM_ROWS_DEFAULT
-#define MOF_ASM_ROWS_DEFAULT 1
-#endif
-#ifndef MOF_ASM_ROWS_U
-#define MOF_ASM_ROWS_U 1
-#endif
 // Row i's stores of one system: A blocks (+ lambda a2), the bf16 copies,
 // the diagonal block's inverse and f_i.
 template <int WMAX>
@@ -496,8 +475,8 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
                                            int32_t N, int32_t deg, int64_t o, int64_t sell_nb,
                                            const int32_t *__restrict__ sell_col, const float *__restrict__ a2s,
                                            int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
-                                           double *__restrict__ rhs, uint2 *__restrict__ Ah, uint2 *__restrict__ Dh,
-                                           int32_t nown, const int32_t *__restrict__ mir) {
+                                           double *__restrict__ rhs, uint2 *__restrict__ Ah, int32_t nown,
+                                           const int32_t *__restrict__ mir) {
 #pragma unroll
     for (int z = 0; z < WMAX; ++z) {
         if (z >= deg) continue;
@@ -526,164 +505,63 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
             inv[0] = 1.0 / d0; inv[1] = 0.0; inv[2] = 0.0; inv[3] = 1.0 / d3;
         }
         const int64_t vi = (int64_t)b * N + i;
-        if (Dh)
-            Dh[vi] = i >= nown ? bf16x4(1.f, 0.f, 0.f, 1.f)
-                               : bf16x4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
-        else
+        if (!Ah)  // multigrid: the smoother's D comes from the bf16 diagonal blocks
             reinterpret_cast<float4 *>(dinv32)[vi] =
                 make_float4((float)inv[0], (float)inv[1], (float)inv[2], (float)inv[3]);
         *reinterpret_cast<double2 *>(rhs + 2 * vi) = make_double2(f0, f1);
     }
 }
 
+// Mixed-precision assembly by vertex rows (the PCG row layout and XCD-aware
+// (row block, system) order). Thread i walks the incident triangles of
+// vertex i in the caller's triangle order (tinc, SELL-64) and, per
+// triangle, forms grad_M I, u = grad_M I . e at (i, v_{a+1}, v_{a+2}) and
+// row i's f term in k_tri_step's exact arithmetic (the I0 values in the
+// triangle's own corner order, np.dot's fma chain, the f term's operation
+// order; dI from k_gather_I, the f term's "/ 12" by div12), then adds the
+// triangle's three a1 terms of row i -- (i,i), (i,v_{a+1}), (i,v_{a+2}) --
+// to register accumulators of the row's SELL slots (tslot; WMAX >= the
+// widest row: fma by 0/1 slot masks, no dynamic register indexing). f folds
+// in fp64 in the reference's triangle order, bit for bit; A32 is an fp32
+// fold (the inner operator). Measured and not kept (round 2): a separate
+// per-triangle pass storing u32 / f terms for the rows to gather back (72 B
+// stored and 120 B gathered per triangle and system: 4.13 + 8.22 vs 10.19 ms
+// per 512-system launch at C3), 2 / 4 systems per thread sharing each
+// triangle's geometry (VGPRs 124 -> 290, 10.0 / 10.4 / 14.6 ms at 1 / 2 / 4),
+// a mul-add fold (11.9 ms), LDS slot accumulators (21.0 ms).
+struct TriGeo {
+    const double *gw, *e, *area, *J0, *dt;  // J0: the batch's I0 rows (internal order, stride N)
+    const double *dI;                       // (I1 - I0) / dt per system (k_gather_I), stride N
+};
 template <int WMAX>
-__global__ __launch_bounds__(kWG) void k_assemble_rows(
+__global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
     const int4 *__restrict__ tinc, const int32_t *__restrict__ tslot, const float *__restrict__ w12,
-    const float *__restrict__ a2s, const float *__restrict__ u, const double *__restrict__ fc, int block_jacobi,
-    float *__restrict__ A, float *__restrict__ dinv32, double *__restrict__ rhs, uint2 *__restrict__ Ah,
-    uint2 *__restrict__ Dh, int32_t nown, const int32_t *__restrict__ mir) {
+    const float *__restrict__ a2s, int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
+    double *__restrict__ rhs, uint2 *__restrict__ Ah, int32_t nown, const int32_t *__restrict__ mir, TriGeo geo) {
     int32_t rb, b;
     if (!xcd_map(nblk, B, rb, b, kGrpAsm)) return;
-    const float *ub = u + 6 * (int64_t)b * (M + 1);
-    const double *fb = fc + 6 * (int64_t)b * (M + 1);
-    constexpr int U = MOF_ASM_ROWS_U;
+    const double *I0b = geo.J0 + (int64_t)b * N, *Db = geo.dI + (int64_t)b * N;
 #pragma unroll 1
     for (int r = 0; r < kRows; ++r) {
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         const int32_t s = i >> 6, l = i & 63;
         float acc[WMAX][4];
-#pragma unroll
-        for (int q = 0; q < WMAX; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
-        double f0 = 0.0, f1 = 0.0;
-        const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
-        for (int32_t t0 = 0; t0 < tw; t0 += U) {
-            int4 q[U];
-            int32_t sl[U];
-#pragma unroll
-            for (int v = 0; v < U; ++v) {
-                const int64_t e = (int64_t)to + min(t0 + v, tw - 1) * kSlice + l;
-                q[v] = tinc[e];
-                sl[v] = tslot[e];
-            }
-            float2 P[U][3];
-            float w[U];
-            double2 fv[U];
-#pragma unroll
-            for (int v = 0; v < U; ++v) {
-                const float2 *uT = reinterpret_cast<const float2 *>(ub + 6 * (int64_t)q[v].x);
-                P[v][0] = uT[0];
-                P[v][1] = uT[1];
-                P[v][2] = uT[2];
-                w[v] = w12[q[v].x];
-                fv[v] = *reinterpret_cast<const double2 *>(fb + 6 * (int64_t)q[v].x + 2 * q[v].y);
-            }
-#pragma unroll
-            for (int v = 0; v < U; ++v) {
-                const bool on = t0 + v < tw;
-                const int c = q[v].y;
-                // corner rotation by 0/1 masks (exact; selects on a runtime
-                // corner index would put P in scratch memory)
-                const float m0 = c == 0 ? 1.f : 0.f, m1 = c == 1 ? 1.f : 0.f, m2 = c == 2 ? 1.f : 0.f;
-                const float2 ui = make_float2(m0 * P[v][0].x + m1 * P[v][1].x + m2 * P[v][2].x,
-                                              m0 * P[v][0].y + m1 * P[v][1].y + m2 * P[v][2].y);
-                const float2 uj = make_float2(m0 * P[v][1].x + m1 * P[v][2].x + m2 * P[v][0].x,
-                                              m0 * P[v][1].y + m1 * P[v][2].y + m2 * P[v][0].y);
-                const float2 uk = make_float2(m0 * P[v][2].x + m1 * P[v][0].x + m2 * P[v][1].x,
-                                              m0 * P[v][2].y + m1 * P[v][0].y + m2 * P[v][1].y);
-                const int32_t sj = sl[v] & 0xff, sk = sl[v] >> 8;
-                const float wv = on ? w[v] : 0.f;
-                // a term on the diagonal block takes A/6 = 2 A/12 (a
-                // degenerate triangle's second corner at i included)
-                const float wd = 2.f * wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
-                const float d[4] = {ui.x * ui.x * wd, ui.x * ui.y * wd, ui.y * ui.x * wd, ui.y * ui.y * wd};
-                const float cj[4] = {ui.x * uj.x * wj, ui.x * uj.y * wj, ui.y * uj.x * wj, ui.y * uj.y * wj};
-                const float ck[4] = {ui.x * uk.x * wk, ui.x * uk.y * wk, ui.y * uk.x * wk, ui.y * uk.y * wk};
-#pragma unroll
-                for (int z = 0; z < WMAX; ++z) {
-                    const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[z][e] += (z == 0 ? d[e] : 0.f) + mj * cj[e] + mk * ck[e];
-                }
-                if (on) {  // f in the reference's triangle order
-                    f0 += fv[v].x;
-                    f1 += fv[v].y;
-                }
-            }
-        }
-        rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
-                         block_jacobi, A, dinv32, rhs, Ah, Dh, nown, mir);
-    }
-}
-
-// Row assembly that forms the triangle terms itself (MOF_ASM_RC): per
-// incident triangle, u = grad_M I . e at (i, v_{a+1}, v_{a+2}) and row i's f
-// term in k_tri_step's exact arithmetic (the I0 values in the triangle's own
-// corner order, np.dot's fma chain, the f term's operation order), so
-// k_tri_step and its u32 / fc round trip (72 B stored and 120 B gathered per
-// triangle and system) drop out of the mixed path. A workgroup runs NS
-// systems over one row block (MOF_ASM_NS): each incident triangle's geometry
-// (tinc, tslot, the weight, gw, e of the other two corners, the area: ~200 B
-// of scattered loads) is fetched once for NS systems, which only gather their
-// I values -- but NS = 2 / 4 lower the occupancy (124 -> 290 VGPRs at NS = 4)
-// and measured no faster (C3: 10.0 / 10.4 / 14.6 ms per launch at NS = 1 / 2
-// / 4). The fp32 a1 fold adds the terms one by one in triangle order (fma by
-// 0/1 slot masks: 10.0 ms vs 11.9 ms with k_assemble_rows' mul-add fold); f
-// folds in fp64 in the reference's triangle order.
-#ifndef MOF_ASM_RC
-#define MOF_ASM_RC 1
-#endif
-#ifndef MOF_ASM_NS
-#define MOF_ASM_NS 1
-#endif
-
-struct TriGeo {
-    const double *gw, *e, *area, *J0, *J1, *dt;  // J0 / J1: the batch's I rows (internal order, stride N)
-    const double *dI;                            // (J1 - J0) / dt per system (k_gather_I), stride N
-};
-template <int WMAX, int NS>
-__global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
-    int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
-    const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
-    const int4 *__restrict__ tinc, const int32_t *__restrict__ tslot, const float *__restrict__ w12,
-    const float *__restrict__ a2s, int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
-    double *__restrict__ rhs, uint2 *__restrict__ Ah, uint2 *__restrict__ Dh, int32_t nown,
-    const int32_t *__restrict__ mir, TriGeo geo) {
-    int32_t rb, bq;
-    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpAsm)) return;
-    const double *I0b[NS], *Db[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        const int32_t b = min(bq * NS + k, B - 1);  // slots past B recompute B-1 and store nothing
-        I0b[k] = geo.J0 + (int64_t)b * N;
-        Db[k] = geo.dI + (int64_t)b * N;
-    }
-#pragma unroll 1
-    for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
-        if (i >= N) break;
-        const int32_t s = i >> 6, l = i & 63;
-        float acc[NS][WMAX][4];
-        double f0[NS], f1[NS], Ii0[NS], pdi[NS];
         double ei[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) ei[k] = geo.e[6 * (int64_t)i + k];
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
-#pragma unroll
-            for (int z = 0; z < WMAX; ++z) acc[k][z][0] = acc[k][z][1] = acc[k][z][2] = acc[k][z][3] = 0.f;
-            f0[k] = f1[k] = 0.0;
-            Ii0[k] = I0b[k][i];
-            pdi[k] = Db[k][i];
-        }
+        for (int z = 0; z < WMAX; ++z) acc[z][0] = acc[z][1] = acc[z][2] = acc[z][3] = 0.f;
+        double f0 = 0.0, f1 = 0.0;
+        const double Ii0 = I0b[i], pdi = Db[i];
         const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
         for (int32_t t = 0; t < tw; ++t) {
             const int64_t e = (int64_t)to + (int64_t)t * kSlice + l;
             const int4 q = tinc[e];
             const int32_t sl = tslot[e];
-            const bool real = q.x < M;                   // padding (T = M): weight 0, no f term
+            const bool real = q.x < M;  // padding (T = M): weight 0, no f term
             const int64_t T = min(q.x, M - 1);
             const int32_t c = q.y, vj = q.z, vk = q.w;
             double g[9], ej[6], ek[6];
@@ -702,49 +580,40 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             const float wd = 2.f * wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
             // set(T) - {i} in corner order: at most 2 distinct other corners
             const bool hj = vj != i, hk = vk != i && vk != vj;
+            const double aj = I0b[vj], ak = I0b[vk];
+            const double pdj = Db[vj], pdk = Db[vk];
+            // the triangle's I0 in its own corner order (corner c is i)
+            const double c0 = c == 0 ? Ii0 : (c == 1 ? ak : aj);
+            const double c1 = c == 0 ? aj : (c == 1 ? Ii0 : ak);
+            const double c2 = c == 0 ? ak : (c == 1 ? aj : Ii0);
+            double gI[3];
 #pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                const double aj = I0b[k][vj], ak = I0b[k][vk];
-                const double pdj = Db[k][vj], pdk = Db[k][vk];
-                // the triangle's I0 in its own corner order (corner c is i)
-                const double c0 = c == 0 ? Ii0[k] : (c == 1 ? ak : aj);
-                const double c1 = c == 0 ? aj : (c == 1 ? Ii0[k] : ak);
-                const double c2 = c == 0 ? ak : (c == 1 ? aj : Ii0[k]);
-                double gI[3];
+            for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[d] + c1 * g[3 + d]) + c2 * g[6 + d];
+            const double ui0 = dot64(gI, ei), ui1 = dot64(gI, ei + 3);
+            const double po = hj ? (hk ? pdj + pdk : pdj) : (hk ? pdk : 0.0);
+            if (real) {  // f in the reference's triangle order
+                f0 += div12(ui0 * (2 * pdi + po) * At);
+                f1 += div12(ui1 * (2 * pdi + po) * At);
+            }
+            const float2 ui = make_float2((float)ui0, (float)ui1);
+            const float2 uj = make_float2((float)dot64(gI, ej), (float)dot64(gI, ej + 3));
+            const float2 uk = make_float2((float)dot64(gI, ek), (float)dot64(gI, ek + 3));
+            const float d4[4] = {ui.x * ui.x * wd, ui.x * ui.y * wd, ui.y * ui.x * wd, ui.y * ui.y * wd};
+            const float cj[4] = {ui.x * uj.x * wj, ui.x * uj.y * wj, ui.y * uj.x * wj, ui.y * uj.y * wj};
+            const float ck[4] = {ui.x * uk.x * wk, ui.x * uk.y * wk, ui.y * uk.x * wk, ui.y * uk.y * wk};
 #pragma unroll
-                for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[d] + c1 * g[3 + d]) + c2 * g[6 + d];
-                const double ui0 = dot64(gI, ei), ui1 = dot64(gI, ei + 3);
-                const double po = hj ? (hk ? pdj + pdk : pdj) : (hk ? pdk : 0.0);
-                if (real) {  // f in the reference's triangle order
-                    f0[k] += div12(ui0 * (2 * pdi[k] + po) * At);
-                    f1[k] += div12(ui1 * (2 * pdi[k] + po) * At);
-                }
-                const float2 ui = make_float2((float)ui0, (float)ui1);
-                const float2 uj = make_float2((float)dot64(gI, ej), (float)dot64(gI, ej + 3));
-                const float2 uk = make_float2((float)dot64(gI, ek), (float)dot64(gI, ek + 3));
-                const float d4[4] = {ui.x * ui.x * wd, ui.x * ui.y * wd, ui.y * ui.x * wd, ui.y * ui.y * wd};
-                const float cj[4] = {ui.x * uj.x * wj, ui.x * uj.y * wj, ui.y * uj.x * wj, ui.y * uj.y * wj};
-                const float ck[4] = {ui.x * uk.x * wk, ui.x * uk.y * wk, ui.y * uk.x * wk, ui.y * uk.y * wk};
+            for (int z = 0; z < WMAX; ++z) {
+                const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
 #pragma unroll
-                for (int z = 0; z < WMAX; ++z) {
-                    const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        float a = z == 0 ? acc[k][z][x] + d4[x] : acc[k][z][x];
-                        a = __builtin_fmaf(mj, cj[x], a);
-                        acc[k][z][x] = __builtin_fmaf(mk, ck[x], a);
-                    }
+                for (int x = 0; x < 4; ++x) {
+                    float a = z == 0 ? acc[z][x] + d4[x] : acc[z][x];
+                    a = __builtin_fmaf(mj, cj[x], a);
+                    acc[z][x] = __builtin_fmaf(mk, ck[x], a);
                 }
             }
         }
-        const int32_t deg = vptr[i + 1] - vptr[i];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const int32_t b = bq * NS + k;
-            if (b < B)
-                rows_store<WMAX>(acc[k], f0[k], f1[k], i, b, N, deg, sell_off[s] + l, sell_nb, sell_col, a2s,
-                                 block_jacobi, A, dinv32, rhs, Ah, Dh, nown, mir);
-        }
+        rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
+                         block_jacobi, A, dinv32, rhs, Ah, nown, mir);
     }
 }
 
@@ -1000,64 +869,43 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     }
     const double *J0 = w.Iint.p, *J1 = w.Iint.p + (I1 == I0 + ldI ? (int64_t)m->N : (int64_t)m->N * B);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
-    static const int rows_env = [] {
-        const char *v = std::getenv("MOF_ASM_ROWS");
-        return v ? std::atoi(v) : MOF_ASM_ROWS_DEFAULT;
-    }();
+    // row assembly (forming the triangle terms itself) when the widest row
+    // fits the register accumulators; otherwise k_tri_step + the per-block
+    // kernels (and the fp64 path)
     const int32_t W = m->pat.max_w;
-    const bool rows = precision == MOF_PREC_MIXED && rows_env && W <= 16;
-    // the row kernel forms the triangle terms itself (MOF_ASM_RC): no
-    // k_tri_step; otherwise the mixed path's residual still re-forms u from
-    // the I rows, so no u64 stores
-    const bool asm_rc = MOF_ASM_RC && rows;
-    const bool skip_u64 = MOF_RES_RECOMPUTE && precision == MOF_PREC_MIXED;
-    if (!asm_rc)
+    const bool rows = precision == MOF_PREC_MIXED && W <= 16;
+    const bool skip_u64 = precision == MOF_PREC_MIXED;  // the residual re-forms u from the I rows
+    if (!rows)
         k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
                                       skip_u64 ? nullptr : w.u64.p, w.fc.p,
                                       precision == MOF_PREC_MIXED ? w.u32.p : nullptr, w.dI.p);
-    w.u64_stale = skip_u64 || asm_rc;  // u64 (and with asm_rc fc) re-formed by the fp64 recovery if needed
+    w.u64_stale = skip_u64;  // u64 (and with the row assembly fc) re-formed by the fp64 recovery if needed
     w.J0 = J0;
     w.J1 = J1;
     w.JB = B;
-    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, J1, w.dt.p, w.dI.p};
+    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, w.dt.p, w.dI.p};
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
-    // multigrid: the level-0 smoother's bf16 operator and D^-1 come from here
-    AmgBf16 bf{nullptr, nullptr};
+    // multigrid: the level-0 smoother's bf16 operator comes from here
+    AmgBf16 bf{nullptr};
     if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
-    // row-wise assembly when the widest row fits the register accumulators
-    // (MOF_ASM_ROWS=0: the per-block kernel)
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
-    const dim3 gr(xcd_grid(nblk_rows, B, kGrpAsm));
-    const int32_t *mirw = m->sym_reads && MOF_SKIP_LOWER ? m->sell_mir.p : nullptr;
-#define MOF_ASM_ROWS_LAUNCH(WM)                                                                                   \
-    k_assemble_rows<WM><<<gr, kWG, 0, s>>>(m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p,   \
-                                           m->tsell_off.p, reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p,     \
-                                           m->w12_32.p, m->a2s32.p, w.u32.p, w.fc.p, bj, w.A32.p, w.dinv32.p,         \
-                                           w.rhs.p, bf.A0h, bf.D0h, m->n_own, mirw)
-#define MOF_ASM_RC_LAUNCH(WM, NS)                                                                                 \
-    k_assemble_rows_rc<WM, NS><<<xcd_grid(nblk_rows, (B + (NS)-1) / (NS), kGrpAsm), kWG, 0, s>>>(                 \
+    const int32_t *mirw = m->sym_reads ? m->sell_mir.p : nullptr;
+#define MOF_ASM_RC_LAUNCH(WM)                                                                                     \
+    k_assemble_rows_rc<WM><<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>(                                        \
         m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
         reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p, m->w12_32.p, m->a2s32.p, bj, w.A32.p, w.dinv32.p,   \
-        w.rhs.p, bf.A0h, bf.D0h, m->n_own, mirw, geo)
-    if (rows && W <= 8) {
-        if (asm_rc)
-            MOF_ASM_RC_LAUNCH(8, MOF_ASM_NS);
-        else
-            MOF_ASM_ROWS_LAUNCH(8);
-    } else if (rows) {
-        if (asm_rc)
-            MOF_ASM_RC_LAUNCH(16, (MOF_ASM_NS + 1) / 2);
-        else
-            MOF_ASM_ROWS_LAUNCH(16);
-    }
-#undef MOF_ASM_ROWS_LAUNCH
+        w.rhs.p, bf.A0h, m->n_own, mirw, geo)
+    if (rows && W <= 8)
+        MOF_ASM_RC_LAUNCH(8);
+    else if (rows)
+        MOF_ASM_RC_LAUNCH(16);
 #undef MOF_ASM_RC_LAUNCH
     else if (precision == MOF_PREC_MIXED)
         k_assemble_mixed<<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p, m->vcol.p,
                                             m->cptr.p, m->clist.p, m->w12_32.p, m->a2s32.p, w.u32.p,
-                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p, bf.A0h, bf.D0h, m->n_own);
+                                            w.fc.p, bj, w.A32.p, w.dinv32.p, w.rhs.p, bf.A0h, m->n_own);
     else
         k_assemble_blocks<double><<<gb, kWG, 0, s>>>(snb, m->N, m->M, B, m->sell_blk.p, m->blk_row.p,
                                                      m->vcol.p, m->cptr.p, m->clist.p, m->iw.p,

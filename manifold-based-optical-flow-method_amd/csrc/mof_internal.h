@@ -84,16 +84,9 @@ __host__ __device__ inline int32_t sell_block(int32_t slot, int32_t td) {
     return slot == 0 ? td : (slot <= td ? slot - 1 : slot);
 }
 
-// Symmetric reads of the fp32 / bf16 operators through the mirror table
-// (mof_rowkern.h spmv_row); 0 reads every block at its own position.
-#ifndef MOF_SYM_A
-#define MOF_SYM_A 1
-#endif
-// with symmetric reads, the assembly stores no lower blocks and the level-0
-// Galerkin lists read them as transposed upper ones (0: store everything)
-#ifndef MOF_SKIP_LOWER
-#define MOF_SKIP_LOWER 1
-#endif
+// Symmetric reads of the operators through the mirror table (mof_rowkern.h
+// spmv_row), chosen per mesh (sell_mirror): the assembly then stores no lower
+// blocks and the level-0 Galerkin lists read them as transposed upper ones.
 // sell_mirror entries: position | kMirT = read the block transposed
 constexpr int32_t kMirT = 1 << 30;
 constexpr int32_t kMirPos = kMirT - 1;
@@ -155,18 +148,14 @@ struct Workspace {
     DevArray<double> Iint;             // the batch's I rows in internal vertex order ([B+1] or [2B] rows)
     DevArray<double> dI;               // [B][N] (I1 - I0) / dt per system, internal order (k_gather_I)
     DevArray<double> Vbuf;             // [B][2N] planar output staging
-    // MOF_RES_RECOMPUTE: the mixed path's k_tri_step leaves u64 unwritten
-    // (the fp64 residual re-forms u from the batch's I rows); the fp64
-    // recovery re-runs k_tri_step from the rows below when it needs u64
+    // the mixed path leaves u64 unwritten (the fp64 residual re-forms u from
+    // the batch's I rows); the fp64 recovery re-runs k_tri_step from the rows
+    // below when it needs u64
     bool u64_stale = false;
     const double *J0 = nullptr, *J1 = nullptr;  // the batch's I0 / I1 rows (in Iint), row stride N
     int32_t JB = 0;                              // their systems
 };
 
-// the fp64 residual forms u from the I rows instead of reading u64
-#ifndef MOF_RES_RECOMPUTE
-#define MOF_RES_RECOMPUTE 1
-#endif
 
 // per-system scalar slots (Workspace::sysd / sysi)
 //  SD_RR0 / SD_BEST: |r|^2 at the start of the inner solve / smallest so far
@@ -359,8 +348,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_s
                 const RedArgs &rd, hipStream_t s, bool zh);
 // level-0 smoother data the PCG update / init write the pre-smoothing with
 struct AmgFine {
-    const void *D0h;  // bf16 2x2 D^-1 [B][N] (uint2 each)
-    const void *A0h;  // bf16 level-0 operator [B][sell_nb] (its diagonal blocks: MOF_DINV_FROM_A)
+    const void *A0h;  // bf16 level-0 operator [B][sell_nb] (its diagonal blocks give the smoother's D)
     int64_t sell_nb;
     const int32_t *sell_off;
     float *x0;        // smoother x
@@ -368,10 +356,10 @@ struct AmgFine {
     bool smoothed;    // level 0 has the smoothed prolongator (irregular mesh)
 };
 AmgFine amg_fine(mof_mesh *m);
-// bf16 level-0 A / D^-1 of the next batch, written by the assembly (marks
-// them fresh, so amg_setup_batch does not convert A32 again)
+// bf16 level-0 A of the next batch, written by the assembly (marks it
+// fresh, so amg_setup_batch does not convert A32 again)
 struct AmgBf16 {
-    uint2 *A0h, *D0h;
+    uint2 *A0h;
 };
 AmgBf16 amg_bf16_targets(mof_mesh *m, int32_t B);
 void amg_destroy(AmgDevice *g);

@@ -84,14 +84,16 @@ struct PcgArgs {
     int32_t ext;           // z and r.z come from an external preconditioner (AMG)
     V *x0;                 // ext: pre-smoothed x0 = omega D^-1 r for the V-cycle
     V omega;
-    const uint2 *dh;       // ext (multigrid, fp32): the smoother's 2x2 D^-1, 4 bf16 [B][N]
-    const uint2 *dA;       // ext, MOF_DINV_FROM_A: the smoother's bf16 operator (diagonal blocks)
+    const uint2 *dA;       // ext (multigrid, fp32): the smoother's bf16 operator (its diagonal
+                           // blocks give D for the pre-smoothing)
     int64_t dA_nb;
     const int32_t *dA_off;
     RedArgs red;           // partial-record layout; rows >= red.nown (ghosts) are not summed
     int32_t stall;         // stagnation window in iterations (0: off)
     double *sc;            // pre-reduced scalars (k_red_rzrr / k_red_pq), by iteration parity
-    int32_t zh;            // z stored as bf16 pairs (the multigrid cycle's output, MOF_Z_BF16)
+    int32_t zh;            // z stored as bf16 pairs: the multigrid cycle's output on a single
+                           // domain with the tentative prolongator (the decomposed path's
+                           // halo exchange moves float2 z)
 };
 
 // The per-system scalars every workgroup of the next launch needs, reduced
@@ -134,9 +136,8 @@ __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd
     block_sum<NV, NT>(out, lds);
 }
 
-#ifndef MOF_RES_U
-#define MOF_RES_U 4
-#endif
+// slots / incident triangles per load batch of the residual rows
+constexpr int kResU = 4, kRcU = 2;
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
 // U slots / incident triangles at a time as in spmv_row.
@@ -144,7 +145,7 @@ template <typename V>
 __device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int32_t i,
                                              const V *__restrict__ x, double &y0, double &y1) {
     using V2 = typename VT<V>::V2;
-    constexpr int U = MOF_RES_U;
+    constexpr int U = kResU;
     const int32_t s = i >> 6, l = i & 63;
     V a0 = 0, a1 = 0;
     // lambda a2 x
@@ -208,98 +209,15 @@ __device__ __forceinline__ void apply_row_mf(const OpArgs<V> &op, int32_t b, int
     y1 = a1;
 }
 
-// (a1_b x)_i with u re-formed per incident triangle from the system's I row
-// and the mesh geometry, in k_tri_step's exact arithmetic (grad I without
-// contraction, np.dot's fma chain), so r64 keeps its bits while the
-// 15.7 MB/system u64 array is neither written nor gathered three times
-// (once per incident row block); lambda a2 x as apply_row_mf.
-#ifndef MOF_RC_U
-#define MOF_RC_U 2
-#endif
+// (a1_b x)_i of two systems at once with u re-formed per incident triangle
+// from each system's I row and the mesh geometry, in k_tri_step's exact
+// arithmetic (grad I without contraction, np.dot's fma chain), so r64 keeps
+// its bits while the 15.7 MB/system u64 array is neither written nor
+// gathered three times (once per incident row block); lambda a2 x as
+// apply_row_mf. One system per thread was bound by the shared gathers (8.93
+// vs 6.72 ms per 512-system launch, round 2).
 __device__ __forceinline__ double dot3_np(const double *x, const double *y) {
     return fma(x[2], y[2], fma(x[1], y[1], __dmul_rn(x[0], y[0])));
-}
-__device__ __forceinline__ void apply_row_rc(const OpArgs<double> &op, int32_t b, int32_t i,
-                                             const double *__restrict__ x, double &y0, double &y1) {
-    constexpr int U = MOF_RC_U;
-    const int32_t s = i >> 6, l = i & 63;
-    double a0 = 0, a1 = 0;
-    {
-        const int32_t o = op.sell_off[s];
-        const int32_t w = (op.sell_off[s + 1] - o) >> 6;
-        for (int32_t t0 = 0; t0 < w; t0 += MOF_RES_U) {
-            int32_t j[MOF_RES_U];
-            double blk[MOF_RES_U][4];
-#pragma unroll
-            for (int u = 0; u < MOF_RES_U; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-#pragma unroll
-            for (int u = 0; u < MOF_RES_U; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
-#pragma unroll
-            for (int u = 0; u < MOF_RES_U; ++u) {
-                const double2 xj = ld2(x + 2 * (int64_t)j[u]);
-                const bool on = t0 + u < w;
-                a0 += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : 0.0;
-                a1 += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : 0.0;
-            }
-        }
-    }
-    {
-        const double *Ib = op.I0 + (int64_t)b * op.ldI;
-        const double2 xi = ld2(x + 2 * (int64_t)i);
-        const double Ii = Ib[i];
-        double ei[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ei[q] = op.e[6 * (int64_t)i + q];
-        const int32_t o = op.tsell_off[s];
-        const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
-        for (int32_t t0 = 0; t0 < w; t0 += U) {
-            int4 q[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) q[u] = op.tinc[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-            double g[U][9], ej[U][6], ek[U][6], Ij[U], Ik[U], wt[U];
-            double2 xj[U], xk[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t T = min(q[u].x, op.M - 1);  // padding entries (T = M): any triangle, weight 0
-#pragma unroll
-                for (int k = 0; k < 9; ++k) g[u][k] = op.gw[9 * T + k];
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    ej[u][k] = op.e[6 * (int64_t)q[u].z + k];
-                    ek[u][k] = op.e[6 * (int64_t)q[u].w + k];
-                }
-                Ij[u] = Ib[q[u].z];
-                Ik[u] = Ib[q[u].w];
-                xj[u] = ld2(x + 2 * (int64_t)q[u].z);
-                xk[u] = ld2(x + 2 * (int64_t)q[u].w);
-                wt[u] = op.w12[q[u].x];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c = q[u].y;
-                // the triangle's corner values in its own corner order
-                const double c0 = c == 0 ? Ii : (c == 1 ? Ik[u] : Ij[u]);
-                const double c1 = c == 0 ? Ij[u] : (c == 1 ? Ii : Ik[u]);
-                const double c2 = c == 0 ? Ik[u] : (c == 1 ? Ij[u] : Ii);
-                double gI[3];
-#pragma unroll
-                for (int d = 0; d < 3; ++d)
-                    gI[d] = __dadd_rn(__dadd_rn(__dmul_rn(c0, g[u][d]), __dmul_rn(c1, g[u][3 + d])),
-                                      __dmul_rn(c2, g[u][6 + d]));
-                const double2 ui = make_double2(dot3_np(gI, ei), dot3_np(gI, ei + 3));
-                const double2 uj = make_double2(dot3_np(gI, ej[u]), dot3_np(gI, ej[u] + 3));
-                const double2 uk = make_double2(dot3_np(gI, ek[u]), dot3_np(gI, ek[u] + 3));
-                const double si = ui.x * xi.x + ui.y * xi.y;
-                const double sj = uj.x * xj[u].x + uj.y * xj[u].y;
-                const double sk = uk.x * xk[u].x + uk.y * xk[u].y;
-                const double cc = (t0 + u < w) ? wt[u] * ((si + si) + sj + sk) : 0.0;
-                a0 += ui.x * cc;
-                a1 += ui.y * cc;
-            }
-        }
-    }
-    y0 = a0;
-    y1 = a1;
 }
 
 // apply_row_rc for two systems of the batch at once: every incident
@@ -310,22 +228,22 @@ __device__ __forceinline__ void apply_row_rc(const OpArgs<double> &op, int32_t b
 __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t b0, int32_t b1, int32_t i,
                                               const double *__restrict__ x64, double (&y)[2][2]) {
 #pragma clang fp contract(off)
-    constexpr int U = MOF_RC_U;
+    constexpr int U = kRcU;
     const int32_t s = i >> 6, l = i & 63;
     const int64_t vb[2] = {(int64_t)b0 * op.N, (int64_t)b1 * op.N};
     double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
     {
         const int32_t o = op.sell_off[s];
         const int32_t w = (op.sell_off[s + 1] - o) >> 6;
-        for (int32_t t0 = 0; t0 < w; t0 += MOF_RES_U) {
-            int32_t j[MOF_RES_U];
-            double blk[MOF_RES_U][4];
+        for (int32_t t0 = 0; t0 < w; t0 += kResU) {
+            int32_t j[kResU];
+            double blk[kResU][4];
 #pragma unroll
-            for (int u = 0; u < MOF_RES_U; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+            for (int u = 0; u < kResU; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
 #pragma unroll
-            for (int u = 0; u < MOF_RES_U; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
+            for (int u = 0; u < kResU; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
 #pragma unroll
-            for (int u = 0; u < MOF_RES_U; ++u) {
+            for (int u = 0; u < kResU; ++u) {
                 const bool on = t0 + u < w;
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
@@ -409,11 +327,6 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
 
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
 
-// The multigrid cycle's output z stored as a bf16 pair per vertex (single
-// domain; the decomposed path's halo exchange moves float2 z)
-#ifndef MOF_Z_BF16
-#define MOF_Z_BF16 1
-#endif
 
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__restrict__ rhs) {
@@ -441,8 +354,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
             if (i < a.red.nown) rz += (double)r0 * z0 + (double)r1 * z1;  // ghost rows: never summed
         } else if constexpr (sizeof(V) == 4) {
             // the smoother's D^-1 (bf16), as in every later sweep
-            const float2 d = MOF_DINV_FROM_A ? bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), r0, r1)
-                                             : bf16_mat2(a.dh[vi], r0, r1);
+            const float2 d = bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), r0, r1);
             st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
         }
         if (i < a.red.nown) rr += (double)r0 * r0 + (double)r1 * r1;
@@ -456,14 +368,11 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
     }
 }
 
-// MOF_PRS: the scalars of the PCG recurrences are reduced once per system
+// The scalars of the PCG recurrences are reduced once per system
 // (k_red_rzrr after the update / V-cycle, k_red_pq after the SpMV) and the
 // row kernels read two doubles instead of re-reducing every workgroup's
-// partial record -- which is what lets the row kernels use small
-// workgroups (MOF_KROWS).
-#ifndef MOF_PRS
-#define MOF_PRS 1
-#endif
+// partial record -- which is what lets the row kernels use small (256-row)
+// workgroups.
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
     __shared__ double lds[8];
@@ -518,19 +427,9 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, doub
     }
 }
 
-// fp32 SpMV workgroup: kRowsPerWG rows as kSpmvRows rows per thread (4: 256
-// threads, the other row kernels' shape; 1: 1024 threads, all rows of the
-// row block at once, so the neighbouring row blocks of a system run in step
-// and the transposed reads of the symmetric layout meet their lines in L2)
-#ifndef MOF_SPMV_ROWS
-#define MOF_SPMV_ROWS MOF_KROWS
-#endif
-constexpr int kSpmvRows = MOF_SPMV_ROWS;
-constexpr int kSpmvWG = kRowsPerWG / kSpmvRows;
-
-template <typename V, bool FIRST, int NT = kWG, bool ZH = false>
+template <typename V, bool FIRST, bool ZH = false>
 __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
-    constexpr int RPT = kRowsPerWG / NT;  // rows per thread
+    constexpr int NT = kWG, RPT = kRows;  // rows per thread
     __shared__ double lds[2 * (NT / 64)];
     int32_t rb, b;
     if (!xcd_map(a.nblk, a.B, rb, b, kGrpSpmv)) return;
@@ -541,17 +440,14 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     // x update below)
     const int32_t conv = a.sysi[b * kSysStride + SI_CONV];
     if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || (conv >= 0 && conv != it))) return;
-    const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;  // slot stride
-    const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;     // p.q slot stride
+    const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;  // p.q slot stride
     using V2 = typename VT<V>::V2;
     const int64_t vb = (int64_t)b * a.N;
     double cur[2];
-    if (MOF_PRS) {
+    {
         const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
         cur[0] = c[0];
         cur[1] = c[1];
-    } else {
-        reduce_sys<2, NT>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
     }
     // The previous iteration's x += alpha p, deferred to here: this launch
     // reads p anyway (p = z + beta p), so the update kernel reads neither p
@@ -559,21 +455,10 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     V alpha_prev = 0;
     double old[2] = {1.0, 1.0};  // the previous iteration's r.z, |r|^2
     if (!FIRST) {
-        if (MOF_PRS) {
-            const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
-            old[0] = o[0];
-            old[1] = o[1];
-        } else {
-            reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds);
-        }
-        if (!force) {
-            double pqp[1];
-            if (MOF_PRS)
-                pqp[0] = *sc_pq(a.sc, a.B, (it + 1) & 1, b);
-            else
-                reduce_sys<1, NT>(a.part_pq + ((it + 1) & 1) * pqs, a.red, a.B, b, pqp, lds);
-            alpha_prev = (V)(old[0] / pqp[0]);
-        }
+        const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
+        old[0] = o[0];
+        old[1] = o[1];
+        if (!force) alpha_prev = (V)(old[0] / *sc_pq(a.sc, a.B, (it + 1) & 1, b));
     }
     if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
         if (!FIRST) {
@@ -643,134 +528,11 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     if (threadIdx.x == 0) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, b, rb)] = v[0];
 }
 
-// The fp32 SpMV with two systems per thread (MOF_SPMV_NS = 2): each slot's
-// column index and mirror entry are loaded once for the pair (spmv_row_ns).
-// Both systems' products are always formed (a retired partner's are
-// discarded) with no fp contraction, so a system's bits do not depend on its
-// partner or slot; the per-system bookkeeping is pcg_spmv_body's.
-// Measured (same box, C3 B = 512, profiles/r02_ab/spmvns_*): the main launch
-// takes the same time (1624.8 vs 1625.5 us: bound by its bytes, not by the
-// index loads), the first-iteration one 1555 vs 1625 us; C3, C2 and R3 within
-// noise. Off by default.
-#ifndef MOF_SPMV_NS
-#define MOF_SPMV_NS 1
-#endif
-constexpr int kSpmvNS = MOF_SPMV_NS;
-template <bool FIRST, bool ZH>
-__device__ __forceinline__ void pcg_spmv_pair(const PcgArgs<float> &a, int32_t it, int32_t flags) {
-#pragma clang fp contract(off)
-    static_assert(MOF_PRS, "the paired SpMV reads the pre-reduced scalars");
-    constexpr int NS = 2, NT = kSpmvWG, RPT = kRowsPerWG / NT;
-    constexpr int U = MOF_SPMV_U >= 8 ? MOF_SPMV_U / 2 : MOF_SPMV_U;
-    __shared__ double lds[NS * (NT / 64)];
-    int32_t rb, bq;
-    if (!xcd_map(a.nblk, (a.B + NS - 1) / NS, rb, bq, kGrpSpmv > NS ? kGrpSpmv / NS : 1)) return;
-    const bool force = flags & kForce;
-    const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;  // p.q slot stride
-    int32_t bs[NS];
-    bool work[NS];
-    float alpha_prev[NS], beta[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        const int32_t b = bq * NS + t;
-        bs[t] = min(b, a.B - 1);
-        work[t] = false;
-        alpha_prev[t] = 0.f;
-        beta[t] = 0.f;
-        if (b >= a.B) continue;
-        const int32_t conv = a.sysi[b * kSysStride + SI_CONV];
-        if (!force && (!a.sysi[b * kSysStride + SI_ACTIVE] || (conv >= 0 && conv != it))) continue;
-        const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
-        const double cur[2] = {c[0], c[1]};
-        double old[2] = {1.0, 1.0};
-        if (!FIRST) {
-            const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
-            old[0] = o[0];
-            old[1] = o[1];
-            if (!force) alpha_prev[t] = (float)(old[0] / *sc_pq(a.sc, a.B, (it + 1) & 1, b));
-        }
-        if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {  // converged: finish x, retire
-            if (!FIRST) {
-                const int64_t vb = (int64_t)b * a.N;
-#pragma unroll
-                for (int r = 0; r < RPT; ++r) {
-                    const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
-                    if (i >= a.N) break;
-                    const int64_t vi = vb + i;
-                    const float2 p0 = *reinterpret_cast<const float2 *>(a.p + 2 * vi);
-                    float2 xi = *reinterpret_cast<const float2 *>(a.x + 2 * vi);
-                    xi.x += alpha_prev[t] * p0.x;
-                    xi.y += alpha_prev[t] * p0.y;
-                    *reinterpret_cast<float2 *>(a.x + 2 * vi) = xi;
-                }
-            }
-            if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
-                a.sysi[b * kSysStride + SI_CONV] = it;
-            continue;
-        }
-        if (!force && rb == 0 && threadIdx.x == 0 && cur[1] < a.sysd[b * kSysStride + SD_BEST]) {
-            a.sysd[b * kSysStride + SD_BEST] = cur[1];
-            a.sysi[b * kSysStride + SI_BEST_IT] = it;
-        }
-        if (!FIRST) beta[t] = (float)(cur[0] / old[0]);
-        work[t] = true;
-    }
-    if (!work[0] && !work[1]) return;
-    const float *xs[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t)
-        xs[t] = ZH ? reinterpret_cast<const float *>(reinterpret_cast<const uint32_t *>(a.z) + (int64_t)bs[t] * a.N)
-                   : a.z + 2 * (int64_t)bs[t] * a.N;
-    double pq[NS] = {0.0, 0.0};
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
-        if (i >= a.N) break;
-        float y[NS][2];
-        if (MOF_SYM_A && a.mat.sell_mir)
-            spmv_row_ns<(bool)MOF_SYM_A, NS, U, ZH>(a.mat, bs, i, xs, y);
-        else
-            spmv_row_ns<false, NS, U, ZH>(a.mat, bs, i, xs, y);
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            if (!work[t]) continue;
-            const int64_t vi = (int64_t)bs[t] * a.N + i;
-            float2 zi;
-            if constexpr (ZH) {
-                const uint32_t h = reinterpret_cast<const uint32_t *>(a.z)[vi];
-                zi = float2{bf16_lo(h), bf16_hi(h)};
-            } else {
-                zi = *reinterpret_cast<const float2 *>(a.z + 2 * vi);
-            }
-            float2 qi, pi;
-            if (FIRST) {
-                qi = float2{y[t][0], y[t][1]};
-                pi = zi;
-            } else {
-                const float2 q0 = *reinterpret_cast<const float2 *>(a.q + 2 * vi);
-                const float2 p0 = *reinterpret_cast<const float2 *>(a.p + 2 * vi);
-                qi = float2{y[t][0] + beta[t] * q0.x, y[t][1] + beta[t] * q0.y};
-                pi = float2{zi.x + beta[t] * p0.x, zi.y + beta[t] * p0.y};
-                if (!force) {
-                    float2 xi = *reinterpret_cast<const float2 *>(a.x + 2 * vi);
-                    xi.x += alpha_prev[t] * p0.x;
-                    xi.y += alpha_prev[t] * p0.y;
-                    *reinterpret_cast<float2 *>(a.x + 2 * vi) = xi;
-                }
-            }
-            *reinterpret_cast<float2 *>(a.q + 2 * vi) = qi;
-            *reinterpret_cast<float2 *>(a.p + 2 * vi) = pi;
-            if (i < a.red.nown) pq[t] += (double)pi.x * qi.x + (double)pi.y * qi.y;
-        }
-    }
-    block_sum<NS, NT>(pq, lds);
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int t = 0; t < NS; ++t)
-            if (work[t]) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, bs[t], rb)] = pq[t];
-    }
-}
-
+// Measured and not kept (round 2, profiles/r02_ab/spmvns_*): two systems
+// per thread sharing each slot's column index and mirror entry -- the main
+// launch took the same time (1624.8 vs 1625.5 us at C3, B = 512: bound by
+// its bytes, not by the index loads); 1024-thread workgroups running all
+// rows of a row block at once (1614 -> 2890 us: one workgroup per CU).
 // the fp32 instances run at >= 5 waves per SIMD (MOF_ROW_OCC: +1 % at C3);
 // the fp64 ones keep the compiler's choice (the hint costs C2 fp64 2.7 %)
 template <typename V, bool FIRST, bool ZH = false>
@@ -779,13 +541,10 @@ __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int3
 }
 #define MOF_SPMV_F32(FIRST, ZH)                                                                              \
     template <>                                                                                              \
-    __global__ __launch_bounds__(kSpmvWG) MOF_ROW_OCC void k_pcg_spmv<float, FIRST, ZH>(PcgArgs<float> a,   \
-                                                                                       int32_t it,          \
-                                                                                       int32_t flags) {     \
-        if constexpr (kSpmvNS == 2)                                                                          \
-            pcg_spmv_pair<FIRST, ZH>(a, it, flags);                                                          \
-        else                                                                                                 \
-            pcg_spmv_body<float, FIRST, kSpmvWG, ZH>(a, it, flags);                                          \
+    __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_pcg_spmv<float, FIRST, ZH>(PcgArgs<float> a,       \
+                                                                                   int32_t it,              \
+                                                                                   int32_t flags) {         \
+        pcg_spmv_body<float, FIRST, ZH>(a, it, flags);                                                       \
     }
 MOF_SPMV_F32(true, false)
 MOF_SPMV_F32(false, false)
@@ -794,15 +553,11 @@ MOF_SPMV_F32(false, true)
 #undef MOF_SPMV_F32
 // workgroup size of an SpMV launch
 template <typename V>
-constexpr int spmv_wg() { return sizeof(V) == 4 ? kSpmvWG : kWG; }
-// grid of an SpMV launch over (row block, system) -- or system pairs for the
-// paired fp32 kernel -- in the XCD order its body maps
+constexpr int spmv_wg() { return kWG; }
+// grid of an SpMV launch over (row block, system) in the XCD order its body maps
 template <typename V>
 dim3 spmv_grid(const PcgArgs<V> &a) {
-    if constexpr (sizeof(V) == 4 && kSpmvNS == 2)
-        return dim3(xcd_grid(a.nblk, (a.B + 1) / 2, kGrpSpmv > 2 ? kGrpSpmv / 2 : 1));
-    else
-        return dim3(xcd_grid(a.nblk, a.B, kGrpSpmv));
+    return dim3(xcd_grid(a.nblk, a.B, kGrpSpmv));
 }
 template <typename V>
 void launch_spmv(const PcgArgs<V> &a, bool first, dim3, hipStream_t s, int32_t it, int32_t flags) {
@@ -815,7 +570,7 @@ void launch_spmv(const PcgArgs<V> &a, bool first, dim3, hipStream_t s, int32_t i
              : k_pcg_spmv<V, false, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
 }
 
-constexpr int kUpdRB = kRows >= 4 ? 1 : 4 / kRows;  // row blocks per update workgroup
+constexpr int kUpdRB = 4;  // row blocks per update workgroup
 inline unsigned upd_blocks(int32_t nblk) { return (unsigned)((nblk + kUpdRB - 1) / kUpdRB); }
 
 template <typename V>
@@ -826,14 +581,11 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
     double cur[2], pqv[1];
-    if (MOF_PRS) {
+    {
         const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
         cur[0] = c[0];
         cur[1] = c[1];
         pqv[0] = *sc_pq(a.sc, a.B, it & 1, b);
-    } else {
-        reduce_sys<2>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds);
-        reduce_sys<1>(a.part_pq + (it & 1) * ((int64_t)a.red.P * a.B * a.red.nmax), a.red, a.B, b, pqv, lds);
     }
     if (cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) return;
     // Every workgroup of the system reduces the same partials, so all take
@@ -885,9 +637,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
                 if (i < a.red.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
             } else if constexpr (sizeof(V) == 4) {
                 // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
-                const float2 d = MOF_DINV_FROM_A
-                                     ? bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), ri.x, ri.y)
-                                     : bf16_mat2(a.dh[vi], ri.x, ri.y);
+                const float2 d = bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), ri.x, ri.y);
                 st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
             }
             if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
@@ -923,7 +673,6 @@ __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
 // partial |r|^2 and |f|^2.
-template <bool RC>
 __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                   const double *__restrict__ rhs,
                                                   const double *__restrict__ x64,
@@ -941,10 +690,7 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         double y0, y1;
-        if constexpr (RC)
-            apply_row_rc(op, b, i, x64 + 2 * vb, y0, y1);
-        else
-            apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
+        apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
         const double r0 = f.x - y0, r1 = f.y - y1;
         *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
@@ -965,9 +711,6 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
 // The re-forming residual, two systems per thread (apply_row_rc2): grid
 // over (row block, system pair) in the XCD-aware order; per-system partials
 // summed in the same tree as k_residual's.
-#ifndef MOF_RC_PAIR
-#define MOF_RC_PAIR 1
-#endif
 __global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
@@ -1100,11 +843,9 @@ OpArgs<double> op64(mof_mesh *m) {
 template <typename... Args>
 void launch_residual(const OpArgs<double> &op, int32_t nblk, int32_t B, hipStream_t s, Args... args) {
     if (op.u)
-        k_residual<false><<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
-    else if (MOF_RC_PAIR)
-        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
+        k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
     else
-        k_residual<true><<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
+        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
 }
 
 template <typename V>
@@ -1140,7 +881,6 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.ext = 0;
     a.x0 = nullptr;
     a.omega = (V)0;
-    a.dh = nullptr;
     a.dA = nullptr;
     a.dA_nb = 0;
     a.dA_off = nullptr;
@@ -1208,13 +948,12 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             AmgFine f = amg_fine(m);
             a.x0 = f.x0;
             a.omega = f.omega;
-            a.dh = static_cast<const uint2 *>(f.D0h);
             a.dA = static_cast<const uint2 *>(f.A0h);
             a.dA_nb = f.sell_nb;
             a.dA_off = f.sell_off;
             // bf16 z with the tentative prolongator (C3 +1 %, C2 mixed +2 %,
             // same iterations); R3 on the smoothed one: 63 vs 50 its
-            a.zh = MOF_Z_BF16 && !f.smoothed;
+            a.zh = !f.smoothed;
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
@@ -1227,7 +966,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol);
     if (amg) precond(0);
-    if (MOF_PRS) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, 0);
+    k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, 0);
     MOF_HIP(hipGetLastError());
     // systems active at the start of this solve: the host mirror is current
     // (reset by solve_batch, refreshed by every outer check)
@@ -1266,10 +1005,10 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             } else {
                 launch_spmv(a, it == 0, gx, s, it, 0);
             }
-            if (MOF_PRS) k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it & 1);
+            k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it & 1);
             k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), (unsigned)B), kWG, 0, s>>>(a, it);
             if (amg) precond((it + 1) & 1);
-            if (MOF_PRS) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, (it + 1) & 1);
+            k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, (it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -1501,8 +1240,7 @@ std::vector<PcgArgs<V>> dd_args(mof_dd *d, int32_t B, bool amg) {
                 a.ext = 1;
                 a.x0 = f.x0;
                 a.omega = f.omega;
-                a.dh = static_cast<const uint2 *>(f.D0h);
-                a.dA = static_cast<const uint2 *>(f.A0h);
+                    a.dA = static_cast<const uint2 *>(f.A0h);
                 a.dA_nb = f.sell_nb;
                 a.dA_off = f.sell_off;
             }
@@ -1534,8 +1272,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, const SolveP
                                d->parts[l]->ws.nblk, args[l].red, s, false);
         }
         dd_sync_partials(d, d->part_rzrr.p + slot * ps, 2 * rec, s);
-        if (MOF_PRS)
-            for (size_t l = 0; l < L; ++l) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], slot);
+        for (size_t l = 0; l < L; ++l) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], slot);
     };
     for (size_t l = 0; l < L; ++l) {
         Workspace &w = d->parts[l]->ws;
@@ -1548,7 +1285,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, const SolveP
     for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol, 0.0);
     if (amg)
         precond(0);
-    else if (MOF_PRS)
+    else
         for (size_t l = 0; l < L; ++l) k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], 0);
     MOF_HIP(hipGetLastError());
     std::vector<int32_t> was_active(B);
@@ -1563,8 +1300,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, const SolveP
             launch_spmv(args[l], first, gx, s, it_, 0);
         }
         dd_sync_partials(d, d->part_pq.p + (it_ & 1) * (int64_t)d->P * rec, rec, s);  // this parity's slot
-        if (MOF_PRS)
-            for (size_t l = 0; l < L; ++l) k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], it_ & 1);
+        for (size_t l = 0; l < L; ++l) k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], it_ & 1);
     };
     while (!done && it < max_iter) {
         const int32_t n = std::min(chunk, max_iter - it);
