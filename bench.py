@@ -47,6 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 CONFIG_NAMES = {
+    "C1": "642-vertex icosphere (n=8), T=16 (15 solves), the reference S3 path's parity case",
     "C2": "32k-vertex jittered icosphere (n=57, 32,492 vertices), fp64 Jacobi-PCG",
     "C3": "160k-vertex jittered icosphere (n=128, 163,842 vertices), fp32 PCG + fp64 refinement",
     "C5": "640k-vertex jittered icosphere (n=253, 640,092 vertices)",
@@ -170,7 +171,7 @@ def parity_check(geom, t, a, lam, samples):
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
-def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None):
+def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
     host on a bounded sample: Pool(C) runs per_core * C timesteps (SURVEY.md
     §8(d): 2 C); each assembles the first `frac` of the triangles with the
@@ -182,6 +183,9 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None):
     import reference_clone as clone
     C = clone.default_cores()
     K = per_core * C
+    if full_timesteps:  # C1 is timed in full (every timestep, the whole triangle loop)
+        K, frac = full_timesteps, 1.0
+        C = min(C, K)
     a2, gw, e, iw = geom if geom is not None else oracle.geometry(p, n, t, a)
     a2l = clone.as_lil(a2)
     T = K + 1
@@ -211,6 +215,9 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None):
 
 def main():
     args = parse()
+    if args.config == "C1":  # the whole T = 16 job is one step (one batch of 15 timesteps)
+        args.fixed_timesteps = args.fixed_timesteps or 15
+        args.batch = min(args.batch, args.fixed_timesteps)
     self_launch(args)
     from mofhip.dist import max_over_ranks, rank_env, rank_k_range, sum_over_ranks
     rank, world, local = rank_env()
@@ -447,7 +454,8 @@ def main():
         geom = oracle.geometry(p, n, t, a)
     parity = parity_check(geom, t, a, args.lambda_, samples) if samples else None
     if rank == 0 and not args.no_cpu_baseline and not dry:
-        cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom)
+        cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom,
+                           full_timesteps=args.fixed_timesteps if args.config == "C1" else 0)
 
     if rank == 0:
         line = {

@@ -470,10 +470,13 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
 
 // Row i's stores of one system: A blocks (+ lambda a2), the bf16 copies,
 // the diagonal block's inverse and f_i.
-template <int WMAX>
-__device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f0, double f1, int32_t i, int32_t b,
+// T = double: the a1 fold ran in fp64 (A64 = a1 + lambda a2, the
+// reference's operator, for the fp64 residual), A32 its fp32 rounding.
+template <int WMAX, typename T>
+__device__ __forceinline__ void rows_store(const T (&acc)[WMAX][4], double f0, double f1, int32_t i, int32_t b,
                                            int32_t N, int32_t deg, int64_t o, int64_t sell_nb,
                                            const int32_t *__restrict__ sell_col, const float *__restrict__ a2s,
+                                           const double *__restrict__ a2s64, double *__restrict__ A64,
                                            int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
                                            double *__restrict__ rhs, uint2 *__restrict__ Ah, int32_t nown,
                                            const int32_t *__restrict__ mir) {
@@ -484,9 +487,23 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
         // symmetric layout: lower blocks are read as transposed upper
         // ones and never leave the registers
         if (mir && (mir[pos] & kMirT)) continue;
-        const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
-        const float Av[4] = {acc[z][0] + s4.x, acc[z][1] + s4.y, acc[z][2] + s4.z, acc[z][3] + s4.w};
         const int64_t qq = (int64_t)b * sell_nb + pos;
+        float Av[4];
+        if constexpr (sizeof(T) == 8) {
+            const double2 s0 = reinterpret_cast<const double2 *>(a2s64)[2 * pos];
+            const double2 s1 = reinterpret_cast<const double2 *>(a2s64)[2 * pos + 1];
+            const double a64[4] = {acc[z][0] + s0.x, acc[z][1] + s0.y, acc[z][2] + s1.x, acc[z][3] + s1.y};
+            reinterpret_cast<double2 *>(A64)[2 * qq] = make_double2(a64[0], a64[1]);
+            reinterpret_cast<double2 *>(A64)[2 * qq + 1] = make_double2(a64[2], a64[3]);
+#pragma unroll
+            for (int x = 0; x < 4; ++x) Av[x] = (float)a64[x];
+        } else {
+            const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
+            Av[0] = acc[z][0] + s4.x;
+            Av[1] = acc[z][1] + s4.y;
+            Av[2] = acc[z][2] + s4.z;
+            Av[3] = acc[z][3] + s4.w;
+        }
         reinterpret_cast<float4 *>(A)[qq] = make_float4(Av[0], Av[1], Av[2], Av[3]);
         if (Ah) {
             const bool g = i >= nown || sell_col[pos] >= nown;
@@ -532,8 +549,10 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
 struct TriGeo {
     const double *gw, *e, *area, *J0, *dt;  // J0: the batch's I0 rows (internal order, stride N)
     const double *dI;                       // (I1 - I0) / dt per system (k_gather_I), stride N
+    const double *w12, *a2s64;              // F64: A_T / 12 and lambda a2 in fp64
+    double *A64;                            // F64: [B][sell_nb][4] fp64 A (stored blocks as A32)
 };
-template <int WMAX>
+template <int WMAX, bool F64>
 __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
@@ -548,7 +567,8 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         const int32_t s = i >> 6, l = i & 63;
-        float acc[WMAX][4];
+        using Acc = typename std::conditional<F64, double, float>::type;
+        Acc acc[WMAX][4];
         double ei[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) ei[k] = geo.e[6 * (int64_t)i + k];
@@ -575,9 +595,6 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             const double At = geo.area[T];
             const float wv = w12[q.x];
             const int32_t sj = sl & 0xff, sk = sl >> 8;
-            // a term on the diagonal block takes A/6 = 2 A/12 (a degenerate
-            // triangle's second corner at i included)
-            const float wd = 2.f * wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
             // set(T) - {i} in corner order: at most 2 distinct other corners
             const bool hj = vj != i, hk = vk != i && vk != vj;
             const double aj = I0b[vj], ak = I0b[vk];
@@ -595,25 +612,31 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
                 f0 += div12(ui0 * (2 * pdi + po) * At);
                 f1 += div12(ui1 * (2 * pdi + po) * At);
             }
-            const float2 ui = make_float2((float)ui0, (float)ui1);
-            const float2 uj = make_float2((float)dot64(gI, ej), (float)dot64(gI, ej + 3));
-            const float2 uk = make_float2((float)dot64(gI, ek), (float)dot64(gI, ek + 3));
-            const float d4[4] = {ui.x * ui.x * wd, ui.x * ui.y * wd, ui.y * ui.x * wd, ui.y * ui.y * wd};
-            const float cj[4] = {ui.x * uj.x * wj, ui.x * uj.y * wj, ui.y * uj.x * wj, ui.y * uj.y * wj};
-            const float ck[4] = {ui.x * uk.x * wk, ui.x * uk.y * wk, ui.y * uk.x * wk, ui.y * uk.y * wk};
+            // the a1 terms (u_i^a u_j^b) w (compute_a1's association), in
+            // fp32 -- or fp64 (F64: each slot a left fold in triangle order);
+            // a term on the diagonal block takes A/6 = 2 A/12 (a degenerate
+            // triangle's second corner at i included)
+            const Acc wvT = F64 ? (Acc)geo.w12[q.x] : (Acc)wv, wdT = wvT + wvT;
+            const Acc wjT = sj == 0 ? wdT : wvT, wkT = sk == 0 ? wdT : wvT;
+            const Acc ui[2] = {(Acc)ui0, (Acc)ui1};
+            const Acc uj[2] = {(Acc)dot64(gI, ej), (Acc)dot64(gI, ej + 3)};
+            const Acc uk[2] = {(Acc)dot64(gI, ek), (Acc)dot64(gI, ek + 3)};
+            const Acc d4[4] = {ui[0] * ui[0] * wdT, ui[0] * ui[1] * wdT, ui[1] * ui[0] * wdT, ui[1] * ui[1] * wdT};
+            const Acc cj[4] = {ui[0] * uj[0] * wjT, ui[0] * uj[1] * wjT, ui[1] * uj[0] * wjT, ui[1] * uj[1] * wjT};
+            const Acc ck[4] = {ui[0] * uk[0] * wkT, ui[0] * uk[1] * wkT, ui[1] * uk[0] * wkT, ui[1] * uk[1] * wkT};
 #pragma unroll
             for (int z = 0; z < WMAX; ++z) {
-                const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
+                const Acc mj = z == sj ? (Acc)1 : (Acc)0, mk = z == sk ? (Acc)1 : (Acc)0;
 #pragma unroll
                 for (int x = 0; x < 4; ++x) {
-                    float a = z == 0 ? acc[z][x] + d4[x] : acc[z][x];
-                    a = __builtin_fmaf(mj, cj[x], a);
-                    acc[z][x] = __builtin_fmaf(mk, ck[x], a);
+                    Acc a = z == 0 ? acc[z][x] + d4[x] : acc[z][x];
+                    a = fma(mj, cj[x], a);
+                    acc[z][x] = fma(mk, ck[x], a);
                 }
             }
         }
-        rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
-                         block_jacobi, A, dinv32, rhs, Ah, nown, mir);
+        rows_store<WMAX, Acc>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
+                            geo.a2s64, geo.A64, block_jacobi, A, dinv32, rhs, Ah, nown, mir);
     }
 }
 
@@ -883,7 +906,11 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     w.J0 = J0;
     w.J1 = J1;
     w.JB = B;
-    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, w.dt.p, w.dI.p};
+    // MOF_RES_A64 (A/B measurement): the row assembly folds a1 in fp64 and
+    // stores the fp64 A for an explicit fp64 residual SpMV
+    const bool a64 = rows && res_a64();
+    w.A64_valid = a64;
+    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, w.dt.p, w.dI.p, m->w12_64.p, m->a2s64.p, a64 ? w.A64.p : nullptr};
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
@@ -893,7 +920,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
     const int32_t *mirw = m->sym_reads ? m->sell_mir.p : nullptr;
 #define MOF_ASM_RC_LAUNCH(WM)                                                                                     \
-    k_assemble_rows_rc<WM><<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>(                                        \
+    (a64 ? k_assemble_rows_rc<WM, true> : k_assemble_rows_rc<WM, false>)<<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>( \
         m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
         reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p, m->w12_32.p, m->a2s32.p, bj, w.A32.p, w.dinv32.p,   \
         w.rhs.p, bf.A0h, m->n_own, mirw, geo)

@@ -708,10 +708,20 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
     }
 }
 
+// system pairs walked back to back per row block on an XCD (A/B knob
+// MOF_RES_GRP, read once)
+inline int32_t res_grp() {
+    static const int32_t g = [] {
+        const char *v = std::getenv("MOF_RES_GRP");
+        return v && *v ? std::atoi(v) : kGrpRes;
+    }();
+    return g;
+}
+
 // The re-forming residual, two systems per thread (apply_row_rc2): grid
 // over (row block, system pair) in the XCD-aware order; per-system partials
 // summed in the same tree as k_residual's.
-__global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
+__global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, int32_t grp, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
                                                       const int32_t *__restrict__ sysi,
@@ -719,7 +729,7 @@ __global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t
                                                       double *__restrict__ part) {
     __shared__ double lds[16];
     int32_t rb, bp;
-    if (!xcd_map(nblk, (B + 1) / 2, rb, bp, kGrpRes)) return;
+    if (!xcd_map(nblk, (B + 1) / 2, rb, bp, grp)) return;
     const int32_t b0 = 2 * bp, b1 = min(b0 + 1, B - 1);
     const bool act[2] = {sysi[b0 * kSysStride + SI_ACTIVE] != 0,
                          b0 + 1 < B && sysi[b1 * kSysStride + SI_ACTIVE] != 0};
@@ -754,6 +764,42 @@ __global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t
             o[0] = v[2 * t];
             o[1] = v[2 * t + 1];
         }
+    }
+}
+
+// r64 = f - A64 x64 with the fp64 A the row assembly stored (MOF_RES_A64):
+// a plain fp64 block SpMV (symmetric reads through the mirror table when the
+// mesh uses them), HBM-bound, instead of re-forming a1 per triangle.
+__global__ __launch_bounds__(kWG) void k_residual_a64(MatArgs<double> mt, int32_t N, int32_t nblk, int32_t B,
+                                                      RedArgs rd, const double *__restrict__ rhs,
+                                                      const double *__restrict__ x64,
+                                                      const int32_t *__restrict__ sysi, double *__restrict__ r64,
+                                                      double *__restrict__ part) {
+    __shared__ double lds[8];
+    int32_t rb, b;
+    if (!xcd_map(nblk, B, rb, b, kGrpSpmv) || !sysi[b * kSysStride + SI_ACTIVE]) return;
+    const int64_t vb = (int64_t)b * N;
+    double rr = 0.0, ff = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        if (i >= N) break;
+        double y0, y1;
+        spmv_row<double>(mt, b, i, x64 + 2 * vb, y0, y1);
+        const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
+        const double r0 = f.x - y0, r1 = f.y - y1;
+        *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
+        if (i < rd.nown) {
+            rr += r0 * r0 + r1 * r1;
+            ff += f.x * f.x + f.y * f.y;
+        }
+    }
+    double v[2] = {rr, ff};
+    block_sum<2>(v, lds);
+    if (threadIdx.x == 0) {
+        double *o = part + 2 * red_rec(rd, B, b, rb);
+        o[0] = v[0];
+        o[1] = v[1];
     }
 }
 
@@ -840,13 +886,6 @@ OpArgs<V> make_op(mof_mesh *m, const V *a2s, const V *w12, const V *u) {
 OpArgs<double> op64(mof_mesh *m) {
     return make_op<double>(m, m->a2s64.p, m->w12_64.p, m->ws.u64_stale ? nullptr : m->ws.u64.p);
 }
-template <typename... Args>
-void launch_residual(const OpArgs<double> &op, int32_t nblk, int32_t B, hipStream_t s, Args... args) {
-    if (op.u)
-        k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
-    else
-        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, kGrpRes)), kWG, 0, s>>>(op, nblk, B, args...);
-}
 
 template <typename V>
 MatArgs<V> make_mat(mof_mesh *m, const V *A) {
@@ -857,6 +896,24 @@ MatArgs<V> make_mat(mof_mesh *m, const V *A) {
     mt.sell_mir = m->sym_reads ? m->sell_mir.p : nullptr;
     mt.A = A;
     return mt;
+}
+
+// r64 = f - A x64 of the batch: the stored fp64 A (MOF_RES_A64), the u64
+// the fp64 path / recovery stored, or u re-formed from the I rows (two
+// systems per thread)
+template <typename... Args>
+void launch_residual(mof_mesh *m, int32_t nblk, int32_t B, hipStream_t s, RedArgs rd, Args... args) {
+    if (m->ws.A64_valid) {
+        k_residual_a64<<<dim3(xcd_grid(nblk, B, kGrpSpmv)), kWG, 0, s>>>(make_mat<double>(m, m->ws.A64.p), m->N, nblk,
+                                                                          B, rd, args...);
+        return;
+    }
+    const OpArgs<double> op = op64(m);
+    if (op.u)
+        k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
+    else
+        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, res_grp())), kWG, 0, s>>>(op, nblk, B, res_grp(), rd,
+                                                                                     args...);
 }
 
 template <typename V>
@@ -1080,7 +1137,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
         }
     };
     need_A(w.A32, precision == MOF_PREC_MIXED);
-    need_A(w.A64, precision == MOF_PREC_F64);
+    need_A(w.A64, precision == MOF_PREC_F64 || res_a64());
     if (w.cap >= B) {
         MOF_HIP(hipStreamSynchronize(m->stream));
         return;
@@ -1164,7 +1221,6 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
     int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
-    const OpArgs<double> o64 = op64(m);
     // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
     static const bool verbose = std::getenv("MOF_SOLVE_VERBOSE") != nullptr;
     for (; o < sp.max_outer; ++o) {
@@ -1183,7 +1239,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
-        launch_residual(o64, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
+        launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
                                                               w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
@@ -1404,7 +1460,7 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
             mof_mesh *m = d->parts[l];
             Workspace &w = m->ws;
             const RedArgs rd{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
-            launch_residual(op64(m), w.nblk, B, s, rd, w.rhs.p, w.x64.p,
+            launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p,
                                                                   w.sysi.p, w.r64.p, d->part_rr0.p);
         }
         dd_sync_partials(d, d->part_rr0.p, 2 * (int64_t)B * d->nmax, s);

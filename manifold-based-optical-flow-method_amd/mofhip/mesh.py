@@ -211,9 +211,18 @@ class DeviceMesh:
         o.stream = stream
         return o
 
-    def solve_range(self, I, t_k, k0, k1, lambda_, I2=None, device=None, raise_on_noconv=False,
+    def fingerprint(self) -> str:
+        """Digest of the mesh inputs (checkpoint keys, mofhip.solve)."""
+        fp = getattr(self, "_fp", None)
+        if fp is None:
+            from .solve import _digest
+            fp = self._fp = _digest(self._xyz, self._nrm, self._tri, self._area, self.f32_points)
+        return fp
+
+    def solve_range(self, I, t_k, k0, k1, lambda_, I2=None, device=None, raise_on_noconv=False, out=None,
                     **opts):
-        """V for k in [k0, k1): (k1-k0, 2N) float64 host array, plus stats."""
+        """V for k in [k0, k1): (k1-k0, 2N) float64 host array, plus stats.
+        ``out``: a C-contiguous float64 (k1-k0, 2N) array to write V into."""
         I = _f64(I)
         I2a = I if I2 is None else _f64(I2)
         tk = _f64(t_k)
@@ -222,7 +231,13 @@ class DeviceMesh:
             raise ValueError("I and I_2 must be (T, N)")
         if len(tk) < T:
             raise ValueError("t_k needs at least T entries")
-        V = np.empty((max(k1 - k0, 0), 2 * self.N))
+        shape = (max(k1 - k0, 0), 2 * self.N)
+        if out is None:
+            V = np.empty(shape)
+        else:
+            if out.shape != shape or out.dtype != np.float64 or not out.flags.c_contiguous:
+                raise ValueError("out must be a C-contiguous float64 %s array" % (shape,))
+            V = out
         st = L.MofStats()
         o = self.make_opts(**opts)
         h = self.handle(device)

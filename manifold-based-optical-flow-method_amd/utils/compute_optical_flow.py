@@ -58,13 +58,21 @@ SOLVER_OPTIONS = {
     "rtol": 1e-8,
     "batch": 0,
 }
+# compute_velocity_field checkpoint / resume: a directory for shard-granular
+# V chunks (mofhip.solve.Checkpoint; MOF_CHECKPOINT_DIR), "" for none
+RUN_OPTIONS = {
+    "checkpoint_dir": os.environ.get("MOF_CHECKPOINT_DIR", ""),
+    "checkpoint_chunk": int(os.environ.get("MOF_CHECKPOINT_CHUNK", "0") or 0),
+}
 
 
 def set_solver_options(**kw):
     """Update the PCG options (precision 'f64'|'mixed', precond 'amg'|'jacobi'
-    (default: amg for mixed, jacobi for f64), rtol, batch, ...)."""
-    SOLVER_OPTIONS.update(kw)
-    return dict(SOLVER_OPTIONS)
+    (default: amg for mixed, jacobi for f64), rtol, batch, ...) and the run
+    options (checkpoint_dir, checkpoint_chunk)."""
+    for k, v in kw.items():
+        (RUN_OPTIONS if k in RUN_OPTIONS else SOLVER_OPTIONS)[k] = v
+    return dict(SOLVER_OPTIONS, **RUN_OPTIONS)
 
 
 def _solver_options():
@@ -128,8 +136,9 @@ def compute_velocity_field(processes_num, time_steps, a2, grad_w, e, integral_wi
     # reference creates its Pool(processes_num) before start_time (:155-158)
     mesh.prepare(range(ndev))
     start = time.time()
-    V, stats = velocity_field_sharded(mesh, I, tk, 0, max(K, 0), lambda_, I2=I2,
-                                      devices=range(ndev), **_solver_options())
+    V, stats = velocity_field_sharded(mesh, I, tk, 0, max(K, 0), lambda_, I2=I2, devices=range(ndev),
+                                      checkpoint=RUN_OPTIONS["checkpoint_dir"] or None,
+                                      chunk=RUN_OPTIONS["checkpoint_chunk"], **_solver_options())
     execution_time = time.time() - start
     _warn_failed(sum(s["failed"] for s in stats))
     return [V[k] for k in range(V.shape[0])], execution_time

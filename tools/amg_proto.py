@@ -23,6 +23,11 @@ mixed solve -- for aggregation-multigrid variants:
               2 int8 + one scale per block, 3 fp8 e4m3 + one scale per block,
               4 int8 + one scale per row
   q0=F        the same for the level-0 sweeps (the PCG operator stays exact)
+              (formats 5: D^-1/2 A D^-1/2 with D = diag(A), entries in
+              [-1, 1] as int8 with the one fixed scale 1/127, rescaled)
+  s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
+              (from the copy's diagonal blocks) and the level-0 Galerkin
+              product all on the stored copy in format F (1 = bf16, today)
 
 The oracle is test infrastructure; this script is a design tool, never part
 of the product path.
@@ -185,6 +190,9 @@ def build(A, a2m, e, opts):
         L = Level()
         L.A, L.bs = Acur, bs
         L.D, L.Dinv = block_diag_inv(Acur, bs)
+        if lvl == 0 and "s0" in opts:  # the GPU's level 0: everything on the stored copy
+            L.Aq = quantize(Acur, bs, int(opts["s0"]))
+            L.D, L.Dinv = block_diag_inv(L.Aq, bs)
         if opts.get("l1"):
             G = block_graph(Acur, bs)  # |entries| summed per block
             Fr = sp.csr_matrix((Acur.tocoo().data ** 2, (Acur.tocoo().row // bs, Acur.tocoo().col // bs)),
@@ -237,7 +245,7 @@ def build(A, a2m, e, opts):
         pc = np.diff(Pb.indptr)
         rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
         L.gal_terms = int((pc[rows] * pc[Ab.indices]).sum())
-        Ac = (P.T @ Acur @ P).tocsr()
+        Ac = (P.T @ (L.Aq if hasattr(L, "Aq") else Acur) @ P).tocsr()
         dead = np.abs(Ac).sum(1).A1 == 0
         Ac = (Ac + sp.diags(dead * 1.0)).tocsr()
         Acur, bs, Bnull = Ac, 3, Bc
@@ -264,6 +272,12 @@ def quantize(A, bs, fmt):
         ex = np.floor(np.log2(np.maximum(np.abs(v), 2.0 ** -6)))
         q = 2.0 ** (ex - 3)
         d = np.round(v / q) * q * sc
+    elif fmt == 5:  # symmetric diagonal scaling, int8 with one global scale
+        s = np.sqrt(np.abs(A.diagonal()))
+        S = sp.diags(1.0 / s) @ A @ sp.diags(1.0 / s)
+        S = S.tocsr()
+        S.data = np.clip(np.round(S.data * 127.0), -127, 127) / 127.0
+        return (sp.diags(s) @ S @ sp.diags(s)).tocsr()
     elif fmt == 4:  # int8 with one scale per row block (row of blocks)
         rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
         m = np.zeros(Ab.shape[0] // bs)
@@ -280,7 +294,9 @@ def vcycle(levels, l, b, opts):
         return L.coarse @ b
     Aw = L.A
     qf = opts.get("q1") if l >= 1 else opts.get("q0")
-    if qf:
+    if hasattr(L, "Aq"):
+        Aw = L.Aq
+    elif qf:
         if not hasattr(L, "Aq"):
             L.Aq = quantize(L.A, L.bs, int(qf))
         Aw = L.Aq
