@@ -34,6 +34,10 @@ struct AmgParams {
     // (sell_mirror): level-0 gather entries of lower blocks then point at the
     // transposed upper block (| kMirT), which is all the assembly writes
     const int32_t *mirror = nullptr;
+    // level-0 aggregation visit order (internal node ids), or null: node
+    // order. A mesh renumbered within windows (mesh_prepare_host) passes its
+    // RCM order, so the aggregates are the RCM-ordered mesh's.
+    const int32_t *order = nullptr;
 };
 
 // One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser

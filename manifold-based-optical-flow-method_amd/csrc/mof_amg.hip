@@ -1221,6 +1221,7 @@ bool amg_build(mof_mesh *m) {
             MOF_HIP(hipStreamSynchronize(s));
             prm.a2 = a2.data();
         }
+        if (!m->agg_order.empty()) prm.order = m->agg_order.data();
         std::vector<int32_t> mir;
         if (m->sym_reads) {
             mir = sell_mirror(m->pat, m->n_own, 1, nullptr);

@@ -26,11 +26,14 @@ namespace mof {
 namespace {
 
 // greedy aggregation of a graph given as sorted adjacency with self loops
+// order (optional): the nodes in visit order (the aggregates then do not
+// depend on the node numbering, only on this order)
 int32_t aggregate(const std::vector<int32_t> &vptr, const std::vector<int32_t> &vcol, int32_t n,
-                  std::vector<int32_t> &agg) {
+                  std::vector<int32_t> &agg, const int32_t *order = nullptr) {
     agg.assign(n, -1);
     int32_t na = 0;
-    for (int32_t i = 0; i < n; ++i) {
+    for (int32_t oi = 0; oi < n; ++oi) {
+        const int32_t i = order ? order[oi] : oi;
         bool free_nb = true;
         for (int32_t q = vptr[i]; q < vptr[i + 1] && free_nb; ++q) free_nb = agg[vcol[q]] < 0;
         if (!free_nb) continue;
@@ -38,7 +41,8 @@ int32_t aggregate(const std::vector<int32_t> &vptr, const std::vector<int32_t> &
         ++na;
     }
     std::vector<int32_t> cnt;
-    for (int32_t i = 0; i < n; ++i) {
+    for (int32_t oi = 0; oi < n; ++oi) {
+        const int32_t i = order ? order[oi] : oi;
         if (agg[i] >= 0) continue;
         // most frequent aggregate among the neighbours (smallest id on ties)
         int32_t best = -1, best_c = 0;
@@ -238,7 +242,7 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         if (F.n * 3 <= prm.max_coarse_dofs) break;
         const int32_t bs = F.bs;
         std::vector<int32_t> agg;
-        const int32_t nc = aggregate(F.vptr, F.vcol, F.n, agg);
+        const int32_t nc = aggregate(F.vptr, F.vcol, F.n, agg, H.levels.size() == 1 ? prm.order : nullptr);
         if (nc >= F.n) break;  // no coarsening possible
         F.agg = agg;
         // members CSR

@@ -869,13 +869,32 @@ __global__ __launch_bounds__(kWG) void k_gather_I(int32_t N, int32_t R, int32_t 
     }
 }
 
+// The per-triangle term arrays ([cap][M+1][6]: u64, the fp32 u32, the f
+// terms fc; triangle slot M stays zero, the incidence lists' padding) only
+// the per-triangle paths use -- the fp64 solve, the mixed path on meshes too
+// wide for the row assembly, the fp64 recovery and mof_assemble -- so they
+// are allocated on first use at the workspace capacity (20 GB at C3, B = 512,
+// that the row-assembly path never touches).
+static void ensure_tri_terms(mof_mesh *m, bool u64, bool u32, hipStream_t s) {
+    Workspace &w = m->ws;
+    const size_t n = 6 * ((size_t)m->M + 1) * std::max(w.cap, 1);
+    auto need = [&](auto &arr) {
+        if (arr.n < n) {
+            arr.alloc(n);
+            arr.zero(s);
+        }
+    };
+    need(w.fc);
+    if (u64) need(w.u64);
+    if (u32) need(w.u32);
+}
+
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
                      bool block_jacobi, uint32_t precision, hipStream_t s, bool amg) {
     Workspace &w = m->ws;
     check_mesh_arrays(m);
-    const size_t nbs = (size_t)m->pat.sell_nb(), mu = 6 * ((size_t)m->M + 1) * B;
-    MOF_REQUIRE(B >= 1 && B <= w.cap && I0 && I1 && w.u64.n >= mu && w.fc.n >= mu &&
-                    w.dt.n >= (size_t)B && m->a2s_valid,
+    const size_t nbs = (size_t)m->pat.sell_nb();
+    MOF_REQUIRE(B >= 1 && B <= w.cap && I0 && I1 && w.dt.n >= (size_t)B && m->a2s_valid,
                 "assembly workspace / operator not prepared");
     MOF_REQUIRE(precision == MOF_PREC_MIXED ? w.A32.n >= 4 * nbs * B : w.A64.n >= 4 * nbs * B,
                 "assembly target A not allocated");
@@ -898,6 +917,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     const int32_t W = m->pat.max_w;
     const bool rows = precision == MOF_PREC_MIXED && W <= 16;
     const bool skip_u64 = precision == MOF_PREC_MIXED;  // the residual re-forms u from the I rows
+    if (!rows) ensure_tri_terms(m, !skip_u64, precision == MOF_PREC_MIXED, s);
     if (!rows)
         k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
                                       skip_u64 ? nullptr : w.u64.p, w.fc.p,
@@ -953,6 +973,7 @@ void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStr
             m->N, snb, m->diag_pos.p, w.A32.p, w.dinv32.p);
     } else {
         MOF_REQUIRE(w.A64.n >= 4 * (size_t)snb * B, "recovery: fp64 A not allocated");
+        ensure_tri_terms(m, true, false, s);
         if (w.u64_stale) {  // the batch's u64 was never stored: form it from the same I rows
             MOF_REQUIRE(w.J0 && w.J1 && w.JB >= B, "recovery: the batch's I rows are gone");
             k_tri_step<<<dim3((unsigned)((m->M + kWG - 1) / kWG)), kWG, 0, s>>>(
@@ -971,6 +992,7 @@ void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStr
 void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, double lambda,
                             hipStream_t s) {
     Workspace &w = m->ws;
+    ensure_tri_terms(m, true, false, s);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, 1, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
                                   w.u64.p, w.fc.p, nullptr, nullptr);

@@ -228,6 +228,10 @@ struct mof_mesh {
     std::vector<int32_t> perm, inv;
     // internal triangle order: tperm[internal] = caller's triangle index
     std::vector<int32_t> tperm, tinv;
+    // irregular meshes: the internal ids in RCM order (the vertices are
+    // degree-sorted within 256-row windows of it); the multigrid aggregation
+    // visits them in this order. Empty: the internal order is the RCM order.
+    std::vector<int32_t> agg_order;
     mof::DevArray<int32_t> perm_d;    // (N) old -> new, for the planar V gather
     mof::DevArray<int32_t> tri_orig;  // (M,3) caller's vertex ids, for gathers of I
     mof::DevArray<int32_t> icol;      // (N) internal vertex -> its column of the caller's I

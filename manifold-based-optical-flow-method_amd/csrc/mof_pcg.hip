@@ -1125,7 +1125,7 @@ double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) 
 
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     Workspace &w = m->ws;
-    const int64_t N = m->N, M = m->M, snb = m->pat.sell_nb();
+    const int64_t N = m->N, snb = m->pat.sell_nb();
     const int32_t cap = std::max(B, w.cap);
     // the materialised A of the requested precision (SELL padding stays zero);
     // an A of the other precision is kept only if it already exists
@@ -1144,13 +1144,10 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     }
     w.cap = B;
     w.nblk = (int32_t)((N + kRowsPerWG - 1) / kRowsPerWG);
-    // triangle slot M of u / fc stays zero: the padding of the incidence lists
-    w.u64.alloc(6 * (M + 1) * B);
-    w.u32.alloc(6 * (M + 1) * B);
-    w.fc.alloc(6 * (M + 1) * B);
-    w.u64.zero(m->stream);
-    w.u32.zero(m->stream);
-    w.fc.zero(m->stream);
+    // the per-triangle term arrays are sized on first use (ensure_tri_terms)
+    w.u64.release();
+    w.u32.release();
+    w.fc.release();
     w.dinv64.alloc(4 * N * B);
     w.dinv32.alloc(4 * N * B);
     w.rhs.alloc(2 * N * B);

@@ -278,6 +278,29 @@ def quantize(A, bs, fmt):
         S = S.tocsr()
         S.data = np.clip(np.round(S.data * 127.0), -127, 127) / 127.0
         return (sp.diags(s) @ S @ sp.diags(s)).tocsr()
+    elif fmt in (6, 7):  # 6: diagonal blocks bf16, off-diagonal blocks of the equilibrated
+        # Q = T^-1 D^-1/2 A D^-1/2 T^-1 (t_i^2 = the row's largest |off-diagonal|, so
+        # |Q| <= 1) as int8 with the one scale 1/127; 7: the same with fp8 e4m3 codes
+        s = np.sqrt(np.abs(A.diagonal()))
+        S = (sp.diags(1.0 / s) @ A @ sp.diags(1.0 / s)).tocoo()
+        same = (S.row // bs) == (S.col // bs)
+        m = np.zeros(A.shape[0])
+        np.maximum.at(m, S.row[~same], np.abs(S.data[~same]))
+        t = np.sqrt(np.where(m > 0, m, 1.0))
+        d = S.data.copy()
+        qv = d[~same] / (t[S.row[~same]] * t[S.col[~same]])
+        if fmt == 6:
+            qv = np.clip(np.round(qv * 127.0), -127, 127) / 127.0
+        else:
+            ex = np.floor(np.log2(np.maximum(np.abs(qv), 2.0 ** -6)))
+            q = 2.0 ** (ex - 3)
+            qv = np.round(qv / q) * q
+        d[~same] = qv * t[S.row[~same]] * t[S.col[~same]]
+        u = d[same].astype(np.float32).view(np.uint32).astype(np.uint64)
+        u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+        d[same] = u.astype(np.uint32).view(np.float32).astype(np.float64)
+        Sq = sp.csr_matrix((d, (S.row, S.col)), shape=A.shape)
+        return (sp.diags(s) @ Sq @ sp.diags(s)).tocsr()
     elif fmt == 4:  # int8 with one scale per row block (row of blocks)
         rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
         m = np.zeros(Ab.shape[0] // bs)
