@@ -313,29 +313,24 @@ __global__ __launch_bounds__(kWG) void k_galerkin(
 // 14.7 at 16 (the per-system fine-block gathers, not the shared gather
 // lists, bound it; more systems per thread only lower the occupancy); one
 // system per thread (k_galerkin<2>): 9.02 ms.
+// The system quads of a coarse tile run back to back on an XCD in groups of
+// kGrpGal (8 quads = 32 systems); 2 quads per group (fewer systems' fine
+// blocks in flight per tile) measured slower: C3 3424-3428 vs 3443-3446
+// timesteps/s (round 3, profiles/r03_ab/gal2_*).
 constexpr int kGalNS = 4;
-// system quads walked back to back per coarse tile on an XCD (A/B knob
-// MOF_GAL0_GRP, read once)
-inline int32_t gal0_grp() {
-    static const int32_t g = [] {
-        const char *v = std::getenv("MOF_GAL0_GRP");
-        return v && *v ? std::atoi(v) : kGrpGal;
-    }();
-    return g;
-}
 __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
-    const uint2 *__restrict__ Afh, int32_t grp) {
+    const uint2 *__restrict__ Afh) {
     // no fp contraction: every system slot of the unrolled loops rounds alike
     // (a system's bits must not depend on its slot, i.e. on the batch split)
 #pragma clang fp contract(off)
     int32_t tile, bq;
     const int32_t nq = (B + kGalNS - 1) / kGalNS;
-    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), nq, tile, bq, grp)) return;
+    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), nq, tile, bq, kGrpGal)) return;
     const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
     if (pos >= c_sell_nb) return;
     const int32_t I = c_sell_row[pos];
@@ -1392,12 +1387,13 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
         if (l == 0)
-            k_galerkin0_ns<<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGalNS - 1) / kGalNS, gal0_grp())),
+            k_galerkin0_ns<<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGalNS - 1) / kGalNS,
+                                           kGrpGal)),
                              kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p,
                                           F.Q.p, w.A32.p, m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
                                           F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
                                               ? nullptr
-                                              : reinterpret_cast<const uint2 *>(G.A0h.p), gal0_grp());
+                                              : reinterpret_cast<const uint2 *>(G.A0h.p));
         else
             k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
                                                               C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,

@@ -20,25 +20,6 @@ __device__ __forceinline__ double dot64(const double *x, const double *y) {
     return fma(x[2], y[2], fma(x[1], y[1], x[0] * y[0]));
 }
 
-// x / 12, correctly rounded, without the divide sequence (the f term's
-// "... * T_area / 12", compute_optical_flow.py:311): q0 = x c with
-// c = RN(1/12), the residual r = x - 12 q0 (exact in an fma: q0 is within an
-// ulp of x/12), q = RN(q0 + r c). Bit-identical to x / 12 for every x whose
-// quotient is a normal double: x/12 = (x/3)/4, and x/3 of a 53-bit
-// significand lies 0, 1/3 or 2/3 of an ulp past a double, at least 1/6 ulp
-// from every rounding midpoint, while q0 + r c is within 2^-53 ulp of it.
-// Quotients near or below the subnormal range (where the residual is no
-// longer exact), zeros and nan take the IEEE divide; infinities q0 (= x / 12).
-// Checked on the host against x / 12 (tests/test_div12.py: the same
-// operations in C over random bit patterns of every exponent).
-__device__ __forceinline__ double div12(double x) {
-    constexpr double c = 1.0 / 12.0;
-    const double q0 = x * c;
-    if (!(fabs(q0) >= 0x1p-1020)) return x / 12.0;
-    const double q = fma(fma(-q0, 12.0, x), c, q0);
-    return __builtin_isfinite(q0) ? q : q0;
-}
-
 // np.dot of two float32 3-vectors on scipy-openblas: float products summed
 // in double, rounded to float once.
 __device__ __forceinline__ float dot32(const float *x, const float *y) {
@@ -199,7 +180,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
                                                   const double *__restrict__ I1, int64_t ldI,
                                                   const double *__restrict__ dt,
                                                   double *__restrict__ u, double *__restrict__ fc,
-                                                  float *__restrict__ u32, const double *__restrict__ dI) {
+                                                  float *__restrict__ u32) {
     // one triangle per thread for all B systems: the geometry is read once
     const int32_t T = blockIdx.x * kWG + threadIdx.x;
     if (T >= M) return;
@@ -224,18 +205,8 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
         double gI[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) gI[d] = (a0 * g[d] + a1 * g[3 + d]) + a2 * g[6 + d];
-        double pd[3];
-        if (dI) {  // k_gather_I's (I1 - I0) / dt of the internal-order rows: the same bits
-            const double *db = dI + b * ldI;
-            pd[0] = db[vo[0]];
-            pd[1] = db[vo[1]];
-            pd[2] = db[vo[2]];
-        } else {
-            const double h = dt[b];
-            pd[0] = (i1[vo[0]] - a0) / h;
-            pd[1] = (i1[vo[1]] - a1) / h;
-            pd[2] = (i1[vo[2]] - a2) / h;
-        }
+        const double h = dt[b];
+        const double pd[3] = {(i1[vo[0]] - a0) / h, (i1[vo[1]] - a1) / h, (i1[vo[2]] - a2) / h};
         const int64_t base = 6 * ((int64_t)b * (M + 1) + T);
         double uo[6], fo[6];
 #pragma unroll
@@ -256,7 +227,7 @@ __global__ __launch_bounds__(kWG) void k_tri_step(int32_t M, int32_t B, const in
             for (int al = 0; al < 2; ++al) {
                 const double uu = dot64(gI, &ev[a][3 * al]);
                 uo[2 * a + al] = uu;
-                fo[2 * a + al] = div12(uu * (2 * pd[a] + po) * A);
+                fo[2 * a + al] = uu * (2 * pd[a] + po) * A / 12;
             }
         }
 #pragma unroll
@@ -470,13 +441,10 @@ __global__ __launch_bounds__(kWG) void k_assemble_mixed(
 
 // Row i's stores of one system: A blocks (+ lambda a2), the bf16 copies,
 // the diagonal block's inverse and f_i.
-// T = double: the a1 fold ran in fp64 (A64 = a1 + lambda a2, the
-// reference's operator, for the fp64 residual), A32 its fp32 rounding.
-template <int WMAX, typename T>
-__device__ __forceinline__ void rows_store(const T (&acc)[WMAX][4], double f0, double f1, int32_t i, int32_t b,
+template <int WMAX>
+__device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f0, double f1, int32_t i, int32_t b,
                                            int32_t N, int32_t deg, int64_t o, int64_t sell_nb,
                                            const int32_t *__restrict__ sell_col, const float *__restrict__ a2s,
-                                           const double *__restrict__ a2s64, double *__restrict__ A64,
                                            int block_jacobi, float *__restrict__ A, float *__restrict__ dinv32,
                                            double *__restrict__ rhs, uint2 *__restrict__ Ah, int32_t nown,
                                            const int32_t *__restrict__ mir) {
@@ -488,22 +456,8 @@ __device__ __forceinline__ void rows_store(const T (&acc)[WMAX][4], double f0, d
         // ones and never leave the registers
         if (mir && (mir[pos] & kMirT)) continue;
         const int64_t qq = (int64_t)b * sell_nb + pos;
-        float Av[4];
-        if constexpr (sizeof(T) == 8) {
-            const double2 s0 = reinterpret_cast<const double2 *>(a2s64)[2 * pos];
-            const double2 s1 = reinterpret_cast<const double2 *>(a2s64)[2 * pos + 1];
-            const double a64[4] = {acc[z][0] + s0.x, acc[z][1] + s0.y, acc[z][2] + s1.x, acc[z][3] + s1.y};
-            reinterpret_cast<double2 *>(A64)[2 * qq] = make_double2(a64[0], a64[1]);
-            reinterpret_cast<double2 *>(A64)[2 * qq + 1] = make_double2(a64[2], a64[3]);
-#pragma unroll
-            for (int x = 0; x < 4; ++x) Av[x] = (float)a64[x];
-        } else {
-            const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
-            Av[0] = acc[z][0] + s4.x;
-            Av[1] = acc[z][1] + s4.y;
-            Av[2] = acc[z][2] + s4.z;
-            Av[3] = acc[z][3] + s4.w;
-        }
+        const float4 s4 = reinterpret_cast<const float4 *>(a2s)[pos];
+        const float Av[4] = {acc[z][0] + s4.x, acc[z][1] + s4.y, acc[z][2] + s4.z, acc[z][3] + s4.w};
         reinterpret_cast<float4 *>(A)[qq] = make_float4(Av[0], Av[1], Av[2], Av[3]);
         if (Ah) {
             const bool g = i >= nown || sell_col[pos] >= nown;
@@ -535,7 +489,7 @@ __device__ __forceinline__ void rows_store(const T (&acc)[WMAX][4], double f0, d
 // triangle, forms grad_M I, u = grad_M I . e at (i, v_{a+1}, v_{a+2}) and
 // row i's f term in k_tri_step's exact arithmetic (the I0 values in the
 // triangle's own corner order, np.dot's fma chain, the f term's operation
-// order; dI from k_gather_I, the f term's "/ 12" by div12), then adds the
+// order), then adds the
 // triangle's three a1 terms of row i -- (i,i), (i,v_{a+1}), (i,v_{a+2}) --
 // to register accumulators of the row's SELL slots (tslot; WMAX >= the
 // widest row: fma by 0/1 slot masks, no dynamic register indexing). f folds
@@ -547,12 +501,9 @@ __device__ __forceinline__ void rows_store(const T (&acc)[WMAX][4], double f0, d
 // triangle's geometry (VGPRs 124 -> 290, 10.0 / 10.4 / 14.6 ms at 1 / 2 / 4),
 // a mul-add fold (11.9 ms), LDS slot accumulators (21.0 ms).
 struct TriGeo {
-    const double *gw, *e, *area, *J0, *dt;  // J0: the batch's I0 rows (internal order, stride N)
-    const double *dI;                       // (I1 - I0) / dt per system (k_gather_I), stride N
-    const double *w12, *a2s64;              // F64: A_T / 12 and lambda a2 in fp64
-    double *A64;                            // F64: [B][sell_nb][4] fp64 A (stored blocks as A32)
+    const double *gw, *e, *area, *J0, *J1, *dt;  // J0 / J1: the batch's I rows (internal order, stride N)
 };
-template <int WMAX, bool F64>
+template <int WMAX>
 __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
@@ -561,21 +512,21 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     double *__restrict__ rhs, uint2 *__restrict__ Ah, int32_t nown, const int32_t *__restrict__ mir, TriGeo geo) {
     int32_t rb, b;
     if (!xcd_map(nblk, B, rb, b, kGrpAsm)) return;
-    const double *I0b = geo.J0 + (int64_t)b * N, *Db = geo.dI + (int64_t)b * N;
+    const double *I0b = geo.J0 + (int64_t)b * N, *I1b = geo.J1 + (int64_t)b * N;
+    const double hb = geo.dt[b];
 #pragma unroll 1
     for (int r = 0; r < kRows; ++r) {
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         const int32_t s = i >> 6, l = i & 63;
-        using Acc = typename std::conditional<F64, double, float>::type;
-        Acc acc[WMAX][4];
+        float acc[WMAX][4];
         double ei[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) ei[k] = geo.e[6 * (int64_t)i + k];
 #pragma unroll
         for (int z = 0; z < WMAX; ++z) acc[z][0] = acc[z][1] = acc[z][2] = acc[z][3] = 0.f;
         double f0 = 0.0, f1 = 0.0;
-        const double Ii0 = I0b[i], pdi = Db[i];
+        const double Ii0 = I0b[i], pdi = (I1b[i] - Ii0) / hb;
         const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
         for (int32_t t = 0; t < tw; ++t) {
             const int64_t e = (int64_t)to + (int64_t)t * kSlice + l;
@@ -598,7 +549,7 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             // set(T) - {i} in corner order: at most 2 distinct other corners
             const bool hj = vj != i, hk = vk != i && vk != vj;
             const double aj = I0b[vj], ak = I0b[vk];
-            const double pdj = Db[vj], pdk = Db[vk];
+            const double pdj = (I1b[vj] - aj) / hb, pdk = (I1b[vk] - ak) / hb;
             // the triangle's I0 in its own corner order (corner c is i)
             const double c0 = c == 0 ? Ii0 : (c == 1 ? ak : aj);
             const double c1 = c == 0 ? aj : (c == 1 ? Ii0 : ak);
@@ -609,34 +560,32 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             const double ui0 = dot64(gI, ei), ui1 = dot64(gI, ei + 3);
             const double po = hj ? (hk ? pdj + pdk : pdj) : (hk ? pdk : 0.0);
             if (real) {  // f in the reference's triangle order
-                f0 += div12(ui0 * (2 * pdi + po) * At);
-                f1 += div12(ui1 * (2 * pdi + po) * At);
+                f0 += ui0 * (2 * pdi + po) * At / 12;
+                f1 += ui1 * (2 * pdi + po) * At / 12;
             }
-            // the a1 terms (u_i^a u_j^b) w (compute_a1's association), in
-            // fp32 -- or fp64 (F64: each slot a left fold in triangle order);
+            // the a1 terms (u_i^a u_j^b) w (compute_a1's association) in fp32;
             // a term on the diagonal block takes A/6 = 2 A/12 (a degenerate
             // triangle's second corner at i included)
-            const Acc wvT = F64 ? (Acc)geo.w12[q.x] : (Acc)wv, wdT = wvT + wvT;
-            const Acc wjT = sj == 0 ? wdT : wvT, wkT = sk == 0 ? wdT : wvT;
-            const Acc ui[2] = {(Acc)ui0, (Acc)ui1};
-            const Acc uj[2] = {(Acc)dot64(gI, ej), (Acc)dot64(gI, ej + 3)};
-            const Acc uk[2] = {(Acc)dot64(gI, ek), (Acc)dot64(gI, ek + 3)};
-            const Acc d4[4] = {ui[0] * ui[0] * wdT, ui[0] * ui[1] * wdT, ui[1] * ui[0] * wdT, ui[1] * ui[1] * wdT};
-            const Acc cj[4] = {ui[0] * uj[0] * wjT, ui[0] * uj[1] * wjT, ui[1] * uj[0] * wjT, ui[1] * uj[1] * wjT};
-            const Acc ck[4] = {ui[0] * uk[0] * wkT, ui[0] * uk[1] * wkT, ui[1] * uk[0] * wkT, ui[1] * uk[1] * wkT};
+            const float wd = wv + wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
+            const float ui[2] = {(float)ui0, (float)ui1};
+            const float uj[2] = {(float)dot64(gI, ej), (float)dot64(gI, ej + 3)};
+            const float uk[2] = {(float)dot64(gI, ek), (float)dot64(gI, ek + 3)};
+            const float d4[4] = {ui[0] * ui[0] * wd, ui[0] * ui[1] * wd, ui[1] * ui[0] * wd, ui[1] * ui[1] * wd};
+            const float cj[4] = {ui[0] * uj[0] * wj, ui[0] * uj[1] * wj, ui[1] * uj[0] * wj, ui[1] * uj[1] * wj};
+            const float ck[4] = {ui[0] * uk[0] * wk, ui[0] * uk[1] * wk, ui[1] * uk[0] * wk, ui[1] * uk[1] * wk};
 #pragma unroll
             for (int z = 0; z < WMAX; ++z) {
-                const Acc mj = z == sj ? (Acc)1 : (Acc)0, mk = z == sk ? (Acc)1 : (Acc)0;
+                const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
 #pragma unroll
                 for (int x = 0; x < 4; ++x) {
-                    Acc a = z == 0 ? acc[z][x] + d4[x] : acc[z][x];
-                    a = fma(mj, cj[x], a);
-                    acc[z][x] = fma(mk, ck[x], a);
+                    float a = z == 0 ? acc[z][x] + d4[x] : acc[z][x];
+                    a = __builtin_fmaf(mj, cj[x], a);
+                    acc[z][x] = __builtin_fmaf(mk, ck[x], a);
                 }
             }
         }
-        rows_store<WMAX, Acc>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
-                            geo.a2s64, geo.A64, block_jacobi, A, dinv32, rhs, Ah, nown, mir);
+        rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
+                         block_jacobi, A, dinv32, rhs, Ah, nown, mir);
     }
 }
 
@@ -843,30 +792,16 @@ void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
 // 256-system k_tri_step on C3, 5151 -> 2979 us with a random vertex order).
 // One XCD per row (workgroup w runs on XCD w mod 8): the row's gathers stay
 // in that XCD's L2. Row r < R0 comes from I0 + r ldI, the others from I1.
-// Rows r < B also write system r's time derivative dI = (I1 - I0) / dt in
-// the internal order (the row-assembly reads it instead of I1): the same IEEE
-// subtract and divide compute_f does per vertex (compute_optical_flow.py:
-// 303-309, k_tri_step's pd), once per vertex and system instead of once per
-// incidence -- two fp64 divides fewer per incident triangle.
 __global__ __launch_bounds__(kWG) void k_gather_I(int32_t N, int32_t R, int32_t R0, const double *__restrict__ I0,
                                                   const double *__restrict__ I1, int64_t ldI,
-                                                  const int32_t *__restrict__ icol, double *__restrict__ out,
-                                                  int32_t B, const double *__restrict__ dt,
-                                                  double *__restrict__ dI) {
+                                                  const int32_t *__restrict__ icol, double *__restrict__ out) {
     const int32_t w = blockIdx.x, q = w >> 3;
     const int32_t nbi = (N + kWG - 1) / kWG;
     const int32_t r = (w & 7) + 8 * (q / nbi);
     const int32_t i = (q % nbi) * kWG + threadIdx.x;
     if (r >= R || i >= N) return;
-    const int32_t c = icol[i];
     const double *src = r < R0 ? I0 + r * ldI : I1 + (int64_t)(r - R0) * ldI;
-    const double v0 = src[c];
-    out[(int64_t)r * N + i] = v0;
-    if (dI && r < B) {
-        // system r pairs I0 row r with I1 row r (in the shared layout I1 = I0 + ldI)
-        const double v1 = I1[(int64_t)r * ldI + c];
-        dI[(int64_t)r * N + i] = (v1 - v0) / dt[r];
-    }
+    out[(int64_t)r * N + i] = src[icol[i]];
 }
 
 // The per-triangle term arrays ([cap][M+1][6]: u64, the fp32 u32, the f
@@ -898,8 +833,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
                 "assembly workspace / operator not prepared");
     MOF_REQUIRE(precision == MOF_PREC_MIXED ? w.A32.n >= 4 * nbs * B : w.A64.n >= 4 * nbs * B,
                 "assembly target A not allocated");
-    MOF_REQUIRE(ldI >= 1 && m->icol.n >= (size_t)m->N && w.Iint.n >= 2 * (size_t)m->N * B &&
-                    w.dI.n >= (size_t)m->N * B,
+    MOF_REQUIRE(ldI >= 1 && m->icol.n >= (size_t)m->N && w.Iint.n >= 2 * (size_t)m->N * B,
                 "I permutation buffers not prepared");
     {
         // consecutive timesteps of one array share B-1 rows: B+1 rows then
@@ -907,7 +841,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
         const int32_t R = shared ? B + 1 : 2 * B, R0 = shared ? R : B;
         const int32_t nbi = (m->N + kWG - 1) / kWG;
         k_gather_I<<<dim3((unsigned)(8 * ((R + 7) / 8) * nbi)), kWG, 0, s>>>(m->N, R, R0, I0, I1, ldI, m->icol.p,
-                                                                            w.Iint.p, B, w.dt.p, w.dI.p);
+                                                                            w.Iint.p);
     }
     const double *J0 = w.Iint.p, *J1 = w.Iint.p + (I1 == I0 + ldI ? (int64_t)m->N : (int64_t)m->N * B);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG));
@@ -921,16 +855,12 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (!rows)
         k_tri_step<<<gt, kWG, 0, s>>>(m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, J0, J1, m->N, w.dt.p,
                                       skip_u64 ? nullptr : w.u64.p, w.fc.p,
-                                      precision == MOF_PREC_MIXED ? w.u32.p : nullptr, w.dI.p);
+                                      precision == MOF_PREC_MIXED ? w.u32.p : nullptr);
     w.u64_stale = skip_u64;  // u64 (and with the row assembly fc) re-formed by the fp64 recovery if needed
     w.J0 = J0;
     w.J1 = J1;
     w.JB = B;
-    // MOF_RES_A64 (A/B measurement): the row assembly folds a1 in fp64 and
-    // stores the fp64 A for an explicit fp64 residual SpMV
-    const bool a64 = rows && res_a64();
-    w.A64_valid = a64;
-    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, w.dt.p, w.dI.p, m->w12_64.p, m->a2s64.p, a64 ? w.A64.p : nullptr};
+    const TriGeo geo{m->gw.p, m->e.p, m->area.p, J0, J1, w.dt.p};
     const int64_t snb = m->pat.sell_nb();
     const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
     const int bj = block_jacobi ? 1 : 0;
@@ -940,7 +870,7 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
     const int32_t *mirw = m->sym_reads ? m->sell_mir.p : nullptr;
 #define MOF_ASM_RC_LAUNCH(WM)                                                                                     \
-    (a64 ? k_assemble_rows_rc<WM, true> : k_assemble_rows_rc<WM, false>)<<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>( \
+    k_assemble_rows_rc<WM><<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>(                                        \
         m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
         reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p, m->w12_32.p, m->a2s32.p, bj, w.A32.p, w.dinv32.p,   \
         w.rhs.p, bf.A0h, m->n_own, mirw, geo)
@@ -978,7 +908,7 @@ void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStr
             MOF_REQUIRE(w.J0 && w.J1 && w.JB >= B, "recovery: the batch's I rows are gone");
             k_tri_step<<<dim3((unsigned)((m->M + kWG - 1) / kWG)), kWG, 0, s>>>(
                 m->M, B, m->tri.p, m->tri.p, m->gw.p, m->e.p, m->area.p, w.J0, w.J1, m->N, w.dt.p, w.u64.p, w.fc.p,
-                nullptr, w.dI.p);
+                nullptr);
             w.u64_stale = false;
         }
         const dim3 gb(xcd_grid((int32_t)((snb + kWG - 1) / kWG), B, kGrpAsm));
@@ -995,7 +925,7 @@ void launch_assemble_export(mof_mesh *m, const double *I0, const double *I1, dou
     ensure_tri_terms(m, true, false, s);
     dim3 gt((unsigned)((m->M + kWG - 1) / kWG), 1u);
     k_tri_step<<<gt, kWG, 0, s>>>(m->M, 1, m->tri.p, m->tri_orig.p, m->gw.p, m->e.p, m->area.p, I0, I1, 0, w.dt.p,
-                                  w.u64.p, w.fc.p, nullptr, nullptr);
+                                  w.u64.p, w.fc.p, nullptr);
     const int64_t snb = m->pat.sell_nb();
     k_assemble_export<<<grid1(snb), kWG, 0, s>>>(snb, m->N, m->M, m->sell_blk.p, m->blk_row.p,
                                                  m->vcol.p, m->cptr.p, m->clist.p, m->iw.p, m->a2.p,

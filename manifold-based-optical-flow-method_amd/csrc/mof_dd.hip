@@ -804,8 +804,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                                 return solve_batch_dd(d, nb, rp, s, &outer_r, &st.max_iterations, on);
                             },
                             [&] {
-                                if (!res_a64())
-                                    for (mof_mesh *m : d->parts) m->ws.A64.release();
+                                for (mof_mesh *m : d->parts) m->ws.A64.release();
                             });
                     double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : Vbuf.p;
                     dd_gather_v(d, nb, Vdst, s);

@@ -147,15 +147,11 @@ struct Workspace {
     DevArray<double> dt;               // [B]
     DevArray<double> Ibuf;             // [B][N] I0 rows + [B][N] I1 rows (host-staged)
     DevArray<double> Iint;             // the batch's I rows in internal vertex order ([B+1] or [2B] rows)
-    DevArray<double> dI;               // [B][N] (I1 - I0) / dt per system, internal order (k_gather_I)
     DevArray<double> Vbuf;             // [B][2N] planar output staging
     // the mixed path leaves u64 unwritten (the fp64 residual re-forms u from
     // the batch's I rows); the fp64 recovery re-runs k_tri_step from the rows
     // below when it needs u64
     bool u64_stale = false;
-    // the batch's fp64 A in A64, written by the row assembly (MOF_RES_A64):
-    // the residual reads it
-    bool A64_valid = false;
     const double *J0 = nullptr, *J1 = nullptr;  // the batch's I0 / I1 rows (in Iint), row stride N
     int32_t JB = 0;                              // their systems
 };
@@ -169,17 +165,6 @@ enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST =
 enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_BEST_IT = 4, SI_FAIL_IT = 5, SI_FAIL_WHY = 6 };
 enum FailWhy { FW_BREAKDOWN = 1, FW_DIVERGED = 2, FW_STALLED = 3, FW_MAXITER = 4, FW_RESIDUAL = 5 };
 constexpr int kSysStride = 8;
-
-// MOF_RES_A64=1 (A/B measurement): the mixed path's row assembly also folds
-// a1 in fp64 and stores the fp64 A, and the fp64 residual is a plain SpMV on
-// it instead of re-forming a1 per incident triangle
-inline bool res_a64() {
-    static const bool on = [] {
-        const char *v = std::getenv("MOF_RES_A64");
-        return v && *v && std::atoi(v) != 0;
-    }();
-    return on;
-}
 
 struct AmgDevice;     // mof_amg.h
 struct AmgHierarchy;  // mof_amg.h

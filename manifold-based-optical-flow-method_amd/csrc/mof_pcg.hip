@@ -708,20 +708,10 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
     }
 }
 
-// system pairs walked back to back per row block on an XCD (A/B knob
-// MOF_RES_GRP, read once)
-inline int32_t res_grp() {
-    static const int32_t g = [] {
-        const char *v = std::getenv("MOF_RES_GRP");
-        return v && *v ? std::atoi(v) : kGrpRes;
-    }();
-    return g;
-}
-
 // The re-forming residual, two systems per thread (apply_row_rc2): grid
 // over (row block, system pair) in the XCD-aware order; per-system partials
 // summed in the same tree as k_residual's.
-__global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, int32_t grp, RedArgs rd,
+__global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
                                                       const int32_t *__restrict__ sysi,
@@ -729,7 +719,7 @@ __global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t
                                                       double *__restrict__ part) {
     __shared__ double lds[16];
     int32_t rb, bp;
-    if (!xcd_map(nblk, (B + 1) / 2, rb, bp, grp)) return;
+    if (!xcd_map(nblk, (B + 1) / 2, rb, bp, kGrpRes)) return;
     const int32_t b0 = 2 * bp, b1 = min(b0 + 1, B - 1);
     const bool act[2] = {sysi[b0 * kSysStride + SI_ACTIVE] != 0,
                          b0 + 1 < B && sysi[b1 * kSysStride + SI_ACTIVE] != 0};
@@ -764,42 +754,6 @@ __global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t
             o[0] = v[2 * t];
             o[1] = v[2 * t + 1];
         }
-    }
-}
-
-// r64 = f - A64 x64 with the fp64 A the row assembly stored (MOF_RES_A64):
-// a plain fp64 block SpMV (symmetric reads through the mirror table when the
-// mesh uses them), HBM-bound, instead of re-forming a1 per triangle.
-__global__ __launch_bounds__(kWG) void k_residual_a64(MatArgs<double> mt, int32_t N, int32_t nblk, int32_t B,
-                                                      RedArgs rd, const double *__restrict__ rhs,
-                                                      const double *__restrict__ x64,
-                                                      const int32_t *__restrict__ sysi, double *__restrict__ r64,
-                                                      double *__restrict__ part) {
-    __shared__ double lds[8];
-    int32_t rb, b;
-    if (!xcd_map(nblk, B, rb, b, kGrpSpmv) || !sysi[b * kSysStride + SI_ACTIVE]) return;
-    const int64_t vb = (int64_t)b * N;
-    double rr = 0.0, ff = 0.0;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
-        if (i >= N) break;
-        double y0, y1;
-        spmv_row<double>(mt, b, i, x64 + 2 * vb, y0, y1);
-        const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * (vb + i));
-        const double r0 = f.x - y0, r1 = f.y - y1;
-        *reinterpret_cast<double2 *>(r64 + 2 * (vb + i)) = make_double2(r0, r1);
-        if (i < rd.nown) {
-            rr += r0 * r0 + r1 * r1;
-            ff += f.x * f.x + f.y * f.y;
-        }
-    }
-    double v[2] = {rr, ff};
-    block_sum<2>(v, lds);
-    if (threadIdx.x == 0) {
-        double *o = part + 2 * red_rec(rd, B, b, rb);
-        o[0] = v[0];
-        o[1] = v[1];
     }
 }
 
@@ -898,22 +852,21 @@ MatArgs<V> make_mat(mof_mesh *m, const V *A) {
     return mt;
 }
 
-// r64 = f - A x64 of the batch: the stored fp64 A (MOF_RES_A64), the u64
-// the fp64 path / recovery stored, or u re-formed from the I rows (two
-// systems per thread)
+// r64 = f - A x64 of the batch: from the u64 the fp64 path / recovery
+// stored, or with u re-formed from the I rows (two systems per thread).
+// Measured and not kept (round 3, profiles/r03_ab/a64_*): the row assembly
+// folding a1 in fp64 and storing the fp64 A for a plain fp64 SpMV residual
+// -- the residuals went 2 x 5.7 -> 2 x 3.6 ms per 512-system batch, the
+// assembly 11.4 -> 15.6 ms (fp64 accumulators: 165 VGPRs, 3 waves, and
+// 10.7 GB of A64 stores): C3 3380-3383 vs 3378-3389 timesteps/s.
 template <typename... Args>
 void launch_residual(mof_mesh *m, int32_t nblk, int32_t B, hipStream_t s, RedArgs rd, Args... args) {
-    if (m->ws.A64_valid) {
-        k_residual_a64<<<dim3(xcd_grid(nblk, B, kGrpSpmv)), kWG, 0, s>>>(make_mat<double>(m, m->ws.A64.p), m->N, nblk,
-                                                                          B, rd, args...);
-        return;
-    }
     const OpArgs<double> op = op64(m);
     if (op.u)
         k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
     else
-        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, res_grp())), kWG, 0, s>>>(op, nblk, B, res_grp(), rd,
-                                                                                     args...);
+        // kGrpRes = 32 system pairs per group (16: equal, round 3)
+        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
 }
 
 template <typename V>
@@ -1137,7 +1090,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
         }
     };
     need_A(w.A32, precision == MOF_PREC_MIXED);
-    need_A(w.A64, precision == MOF_PREC_F64 || res_a64());
+    need_A(w.A64, precision == MOF_PREC_F64);
     if (w.cap >= B) {
         MOF_HIP(hipStreamSynchronize(m->stream));
         return;
@@ -1168,7 +1121,6 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.dt.alloc(B);
     w.Ibuf.alloc(2 * N * B);
     w.Iint.alloc(2 * N * B);
-    w.dI.alloc(N * B);
     w.Vbuf.alloc(2 * N * B);
     if (m->h_cap < B) {
         if (m->h_sysi) (void)hipHostFree(m->h_sysi);

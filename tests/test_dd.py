@@ -213,12 +213,20 @@ def test_dd_full_size_c3(precond):
 
 @pytest.mark.gpu
 def test_dd_nonconvergence_nan():
+    """A solve capped far below its need: NaN-filled and reported with
+    MOF_NO_RECOVERY; by default the decomposed path re-solves the failed
+    systems (fp64 block Jacobi, the full budget) as mof_solve_range does."""
     p, t, n, a, I = wave_case(n=12, T=3)
     tk = np.arange(len(I), dtype=np.float64)
     d = DecomposedMesh(p, n, t, a, 3)
-    V, st = d.solve_range(I, tk, 0, 2, 0.01, precision="f64", max_iter=2, max_outer=1)
+    V, st = d.solve_range(I, tk, 0, 2, 0.01, precision="f64", max_iter=2, max_outer=1, recovery=False)
     assert st["failed"] == 2 and np.isnan(V).all()
+    V, st = d.solve_range(I, tk, 0, 2, 0.01, precision="f64", max_iter=2, max_outer=1)
+    assert st["failed"] == 0 and st["recovered"] == 2 and st["recovered_f64"] == 2, st
     d.close()
+    m = DeviceMesh(p, n, t, a)
+    Vs, _ = m.solve_range(I, tk, 0, 2, 0.01, precision="f64")
+    assert np.abs(V - Vs).max() < 1e-6
 
 
 @pytest.mark.gpu

@@ -10,7 +10,7 @@ for rep in $(seq 1 ${AB_REPS:-2}); do
   for v in base "$@"; do
     lib=""
     [ "$v" != base ] && lib=$PWD/manifold-based-optical-flow-method_amd/mofhip/libmofhip_$v.so
-    MOFHIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline $AB_ARGS \
+    MOFHIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 0 --host-batches 0 $AB_ARGS \
         > $out/${v}_$rep.json 2> $out/${v}_$rep.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "[ab] $v rc=$rc"; [ $rc -ne 1 ] && exit 99; fi

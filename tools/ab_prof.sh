@@ -10,5 +10,5 @@ for v in base "$@"; do
   out=gpurun_out/abprof_$tag/$v
   mkdir -p $out
   MOFHIP_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o run -- \
-      python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline $AB_ARGS > $out/bench.json 2> $out/err.txt || exit 99
+      python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --parity-samples 0 --host-batches 0 $AB_ARGS > $out/bench.json 2> $out/err.txt || exit 99
 done
