@@ -263,6 +263,9 @@ void mesh_prepare_host(mof_mesh *m, const double *xyz, const double *nrm, const 
             // workgroup) of the RCM order, so a 64-row SELL slice holds rows
             // of like width -- R3: 1.72 M -> 1.32 M SELL slots for 1.15 M
             // blocks -- while every gather stays within the window's lines.
+            // Wider windows pad less (512 / 1024 / 2048 rows: ≈1.24 / 1.20 /
+            // 1.18 M slots) but scatter the gathers: R3 687 / 676 / 670 vs
+            // 696 timesteps/s (round 3, profiles/r03_ab/r3win*).
             // MOF_WINDOW_SORT=0/1 forces either.
             const char *ws = std::getenv("MOF_WINDOW_SORT");
             const bool wsort = ws && *ws ? std::atoi(ws) != 0 : mof::amg_auto_smooth(adj);
