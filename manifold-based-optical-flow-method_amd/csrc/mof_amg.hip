@@ -196,7 +196,9 @@ __device__ __forceinline__ void galerkin_block(
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
     // U entries at a time, every load of a chunk issued before use (entries
     // past the list re-load the last one and are masked out)
-    constexpr int U = 4;  // level 0 with 2 / 8: 5269 / 6032 vs 4654 us per 256-system launch
+    // level 0 (round 1) with 2 / 8: 5269 / 6032 vs 4654 us per 256-system
+    // launch; level 1 with 2 (80 instead of 148 VGPRs): equal (round 3)
+    constexpr int U = 4;
     for (int32_t t0 = g0; t0 < g1; t0 += U) {
         int32_t fp[U], ii[U], jj[U];
 #pragma unroll
@@ -338,7 +340,9 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     const int32_t b0 = bq * kGalNS;
     float Cm[kGalNS][3][3] = {};
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
-    constexpr int U = 2;
+    // one gather entry per load batch (92 VGPRs, 5 waves per SIMD) instead
+    // of 2 (140, 3 waves): 6.37 -> 5.92 ms per launch (round 3)
+    constexpr int U = 1;
     for (int32_t t0 = g0; t0 < g1; t0 += U) {
         int32_t fp[U], ii[U], jj[U];
 #pragma unroll

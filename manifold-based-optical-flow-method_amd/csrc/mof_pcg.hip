@@ -137,7 +137,10 @@ __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd
 }
 
 // slots / incident triangles per load batch of the residual rows
-constexpr int kResU = 4, kRcU = 2;
+// kRcU: incident triangles per load batch of the re-forming residual; 1
+// instead of 2 (round 3): 126 instead of 202 VGPRs, 4 instead of 2 waves
+// per SIMD, 5.73 -> 5.42 ms per 512-system launch (profiles/r03_ab/grp/)
+constexpr int kResU = 4, kRcU = 1;
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
 // U slots / incident triangles at a time as in spmv_row.
@@ -220,18 +223,23 @@ __device__ __forceinline__ double dot3_np(const double *x, const double *y) {
     return fma(x[2], y[2], fma(x[1], y[1], __dmul_rn(x[0], y[0])));
 }
 
-// apply_row_rc for two systems of the batch at once: every incident
-// triangle's geometry and every a2 block is loaded once for both (the
+// apply_row_rc for NS systems of the batch at once: every incident
+// triangle's geometry and every a2 block is loaded once for all of them (the
 // re-forming residual is bound by those shared gathers). No fp contraction,
-// so both system slots round alike (a system's bits must not depend on the
+// so every system slot rounds alike (a system's bits must not depend on the
 // slot it lands in, i.e. on the batch split).
-__device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t b0, int32_t b1, int32_t i,
-                                              const double *__restrict__ x64, double (&y)[2][2]) {
+template <int NS>
+__device__ __forceinline__ void apply_row_rcn(const OpArgs<double> &op, const int32_t (&bs)[NS], int32_t i,
+                                              const double *__restrict__ x64, double (&y)[NS][2]) {
 #pragma clang fp contract(off)
     constexpr int U = kRcU;
     const int32_t s = i >> 6, l = i & 63;
-    const int64_t vb[2] = {(int64_t)b0 * op.N, (int64_t)b1 * op.N};
-    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    int64_t vb[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) vb[t] = (int64_t)bs[t] * op.N;
+    double acc[NS][2];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.0;
     {
         const int32_t o = op.sell_off[s];
         const int32_t w = (op.sell_off[s + 1] - o) >> 6;
@@ -246,7 +254,7 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
             for (int u = 0; u < kResU; ++u) {
                 const bool on = t0 + u < w;
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
+                for (int t = 0; t < NS; ++t) {
                     const double2 xj = ld2(x64 + 2 * (vb[t] + j[u]));
                     acc[t][0] += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : 0.0;
                     acc[t][1] += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : 0.0;
@@ -255,11 +263,12 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
         }
     }
     {
-        const double *Ib[2] = {op.I0 + (int64_t)b0 * op.ldI, op.I0 + (int64_t)b1 * op.ldI};
-        double2 xi[2];
-        double Ii[2];
+        const double *Ib[NS];
+        double2 xi[NS];
+        double Ii[NS];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NS; ++t) {
+            Ib[t] = op.I0 + (int64_t)bs[t] * op.ldI;
             xi[t] = ld2(x64 + 2 * (vb[t] + i));
             Ii[t] = Ib[t][i];
         }
@@ -272,8 +281,8 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
             int4 q[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) q[u] = op.tinc[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-            double g[U][9], ej[U][6], ek[U][6], Ij[U][2], Ik[U][2], wt[U];
-            double2 xj[U][2], xk[U][2];
+            double g[U][9], ej[U][6], ek[U][6], Ij[U][NS], Ik[U][NS], wt[U];
+            double2 xj[U][NS], xk[U][NS];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t T = min(q[u].x, op.M - 1);  // padding entries (T = M): weight 0
@@ -285,7 +294,7 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
                     ek[u][k] = op.e[6 * (int64_t)q[u].w + k];
                 }
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
+                for (int t = 0; t < NS; ++t) {
                     Ij[u][t] = Ib[t][q[u].z];
                     Ik[u][t] = Ib[t][q[u].w];
                     xj[u][t] = ld2(x64 + 2 * (vb[t] + q[u].z));
@@ -298,7 +307,7 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
                 const int c = q[u].y;
                 const bool on = t0 + u < w;
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
+                for (int t = 0; t < NS; ++t) {
                     const double c0 = c == 0 ? Ii[t] : (c == 1 ? Ik[u][t] : Ij[u][t]);
                     const double c1 = c == 0 ? Ij[u][t] : (c == 1 ? Ii[t] : Ik[u][t]);
                     const double c2 = c == 0 ? Ik[u][t] : (c == 1 ? Ij[u][t] : Ii[t]);
@@ -319,7 +328,7 @@ __device__ __forceinline__ void apply_row_rc2(const OpArgs<double> &op, int32_t 
         }
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < NS; ++t) {
         y[t][0] = acc[t][0];
         y[t][1] = acc[t][1];
     }
@@ -708,33 +717,43 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
     }
 }
 
-// The re-forming residual, two systems per thread (apply_row_rc2): grid
-// over (row block, system pair) in the XCD-aware order; per-system partials
-// summed in the same tree as k_residual's.
-__global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
+// The re-forming residual, NS systems per thread (apply_row_rcn): grid
+// over (row block, system group of NS) in the XCD-aware order; per-system
+// partials summed in the same tree as k_residual's. NS = 2; 3 / 4 systems
+// per thread (140 / 160 VGPRs, 3 waves): 5.73 / 6.78 vs 5.73 ms per launch
+// (round 3, one incidence per load batch for 3 and 4).
+constexpr int kResNS = 2;
+template <int NS>
+__global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
                                                       const int32_t *__restrict__ sysi,
                                                       double *__restrict__ r64,
                                                       double *__restrict__ part) {
-    __shared__ double lds[16];
+    __shared__ double lds[8 * NS];
     int32_t rb, bp;
-    if (!xcd_map(nblk, (B + 1) / 2, rb, bp, kGrpRes)) return;
-    const int32_t b0 = 2 * bp, b1 = min(b0 + 1, B - 1);
-    const bool act[2] = {sysi[b0 * kSysStride + SI_ACTIVE] != 0,
-                         b0 + 1 < B && sysi[b1 * kSysStride + SI_ACTIVE] != 0};
-    if (!act[0] && !act[1]) return;
+    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bp, kGrpRes)) return;
+    int32_t bs[NS];
+    bool act[NS], any = false;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        bs[t] = min(NS * bp + t, B - 1);
+        act[t] = NS * bp + t < B && sysi[bs[t] * kSysStride + SI_ACTIVE] != 0;
+        any |= act[t];
+    }
+    if (!any) return;
     const int32_t N = op.N;
-    const int32_t bs[2] = {b0, b1};
-    double v[4] = {0.0, 0.0, 0.0, 0.0};  // rr, ff of each system
+    double v[2 * NS];  // rr, ff of each system
+#pragma unroll
+    for (int t = 0; t < 2 * NS; ++t) v[t] = 0.0;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
-        double y[2][2];
-        apply_row_rc2(op, b0, b1, i, x64, y);
+        double y[NS][2];
+        apply_row_rcn<NS>(op, bs, i, x64, y);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NS; ++t) {
             const int64_t vi = (int64_t)bs[t] * N + i;
             const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
             const double r0 = f.x - y[t][0], r1 = f.y - y[t][1];
@@ -745,10 +764,10 @@ __global__ __launch_bounds__(kWG) void k_residual_rc2(OpArgs<double> op, int32_t
             }
         }
     }
-    block_sum<4>(v, lds);
+    block_sum<2 * NS>(v, lds);
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NS; ++t) {
             if (!act[t]) continue;
             double *o = part + 2 * red_rec(rd, B, bs[t], rb);
             o[0] = v[2 * t];
@@ -865,8 +884,8 @@ void launch_residual(mof_mesh *m, int32_t nblk, int32_t B, hipStream_t s, RedArg
     if (op.u)
         k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
     else
-        // kGrpRes = 32 system pairs per group (16: equal, round 3)
-        k_residual_rc2<<<dim3(xcd_grid(nblk, (B + 1) / 2, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
+        k_residual_rcn<kResNS><<<dim3(xcd_grid(nblk, (B + kResNS - 1) / kResNS, kGrpRes)), kWG, 0, s>>>(
+            op, nblk, B, rd, args...);
 }
 
 template <typename V>

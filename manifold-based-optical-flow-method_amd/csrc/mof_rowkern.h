@@ -311,13 +311,11 @@ __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_
 // from the next row block are still in L2 when that row block comes up.
 // G per kernel family (C3, B=256, rocprof: SpMV -7 %, smoother sweeps -3 %,
 // level-0 Galerkin -13 %, residual -8 % against G = B; G = 0 means all B).
-#ifndef MOF_GRP_RES
-#define MOF_GRP_RES 32
-#endif
-#ifndef MOF_GRP_GAL
-#define MOF_GRP_GAL 8
-#endif
-constexpr int32_t kGrpSpmv = 8, kGrpSmooth = 8, kGrpRes = MOF_GRP_RES, kGrpGal = MOF_GRP_GAL, kGrpAsm = 8, kGrpProl = 0,
+// Round 3 (same box, profiles/r03_ab/grp/): the row assembly 32 -> 8
+// (10.2 -> 8.8 ms per 512-system batch), the residual 32 -> 8 system pairs
+// (5.73 -> 5.55 ms per launch); the Galerkin products at 1 instead of 8:
+// -0.7 % timesteps/s.
+constexpr int32_t kGrpSpmv = 8, kGrpSmooth = 8, kGrpRes = 8, kGrpGal = 8, kGrpAsm = 8, kGrpProl = 0,
                   kGrpRestr = 0;
 __host__ __device__ __forceinline__ int32_t sys_group(int32_t B, int32_t G) { return G > 0 && G < B ? G : B; }
 
