@@ -2,9 +2,10 @@
 //
 // Per batch of B systems (timesteps) the mesh-only hierarchy of
 // mof_amg_host.cpp gets its per-timestep values:
-//   k_galerkin<BSF>    A_{l+1} = Q^T A_l Q, one coarse block per thread, folded
-//                      over the pre-built gather lists (no atomics), plus the
-//                      3x3 block-Jacobi inverse of each coarse node;
+//   k_galerkin0_ns /   A_{l+1} = Q^T A_l Q, one coarse block of 4 systems per
+//   k_galerkin3_ns     thread, folded over the pre-built gather lists (no
+//                      atomics), plus the 3x3 block-Jacobi inverse of each
+//                      coarse node;
 //   k_coarse_inverse   the coarsest operator (<= 128 dofs) inverted by the
 //                      symmetric sweep operator in registers (fp64, one
 //                      workgroup per system).
@@ -178,139 +179,11 @@ __global__ __launch_bounds__(kWG) void k_to_h0(int64_t n, const float4 *__restri
     h0_st(H, q, v.x, v.y, v.z, v.w);
 }
 
-// Block (I, J) at coarse SELL position pos of A_{l+1} = Q^T A_l Q for system
-// b, summed over its gather list in list order; the diagonal block also gets
-// 1 on dead dofs and stores its 3x3 inverse for the smoother.
-template <int BSF>
-__device__ __forceinline__ void galerkin_block(
-    int64_t pos, int32_t b, int64_t c_sell_nb, int32_t nC, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
-    const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
-    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
-    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
-    const uint2 *__restrict__ Afh) {
-    const int32_t I = c_sell_row[pos];
-    if (I >= nC) return;  // rows past n in the last slice
-    const float *A = Af + (int64_t)b * f_sell_nb * bstride<BSF>();
-    float C[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-    const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
-    // U entries at a time, every load of a chunk issued before use (entries
-    // past the list re-load the last one and are masked out)
-    // level 0 (round 1) with 2 / 8: 5269 / 6032 vs 4654 us per 256-system
-    // launch; level 1 with 2 (80 instead of 148 VGPRs): equal (round 3)
-    constexpr int U = 4;
-    for (int32_t t0 = g0; t0 < g1; t0 += U) {
-        int32_t fp[U], ii[U], jj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t g = min(t0 + u, g1 - 1);
-            fp[u] = gent[3 * g];
-            ii[u] = gent[3 * g + 1];
-            jj[u] = gent[3 * g + 2];
-        }
-        float a[U][BSF][BSF], qi[U][BSF][3], qj[U][BSF][3];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            // fp -1 / -2: a decomposed part's ghost block, identity / zero
-            if constexpr (BSF == 2) {
-                // level 0 (symmetric layout: a lower block is the transpose of
-                // the upper block the entry points at)
-                const int32_t fq = fp[u] < 0 ? 0 : fp[u] & kMirPos;
-                if (Afh) {
-                    // level 0: the smoother's bf16 blocks (8 B per block; the
-                    // product's scattered gathers touch half the cache lines
-                    // of the fp32 A: 5.35 vs 6.78 ms per 256 systems, same
-                    // iteration counts) -- the coarse operator is then the
-                    // Galerkin product of the operator the smoother sweeps
-                    h0_dec(h0_ld(Afh, (int64_t)b * f_sell_nb + fq), a[u][0][0], a[u][0][1], a[u][1][0],
-                           a[u][1][1]);
-                } else {
-                    ldm<BSF>(A, fq, a[u]);
-                }
-                if (fp[u] >= 0 && (fp[u] & kMirT)) {
-                    const float t01 = a[u][0][1];
-                    a[u][0][1] = a[u][1][0];
-                    a[u][1][0] = t01;
-                }
-            } else {
-                // level >= 1: the fp32 operator (its bf16 sweep copy: 620 vs
-                // 731 us per launch, but 116 vs 110 PCG its/timestep on R3)
-                ldm<BSF>(A, max(fp[u], 0), a[u]);
-            }
-            if (fp[u] < 0) {
-#pragma unroll
-                for (int r = 0; r < BSF; ++r)
-#pragma unroll
-                    for (int k = 0; k < BSF; ++k) a[u][r][k] = (fp[u] == -1 && r == k) ? 1.f : 0.f;
-            }
-#pragma unroll
-            for (int k = 0; k < BSF; ++k)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    qi[u][k][c] = Q[((int64_t)ii[u] * BSF + k) * 3 + c];
-                    qj[u][k][c] = Q[((int64_t)jj[u] * BSF + k) * 3 + c];
-                }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float on = t0 + u < g1 ? 1.f : 0.f;
-            float T[BSF][3];  // A Q_j
-#pragma unroll
-            for (int r = 0; r < BSF; ++r)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    float sum = 0.f;
-#pragma unroll
-                    for (int k = 0; k < BSF; ++k) sum += a[u][r][k] * qj[u][k][c];
-                    T[r][c] = on * sum;
-                }
-#pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    float sum = 0.f;
-#pragma unroll
-                    for (int k = 0; k < BSF; ++k) sum += qi[u][k][r] * T[k][c];
-                    C[r][c] += sum;
-                }
-        }
-    }
-    if (pos == c_diag[I]) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-            if (c_dead[3 * (int64_t)I + d]) C[d][d] += 1.f;
-        float D[3][3];
-        inv3(C, D);
-        st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
-    }
-    st3(Ac, (int64_t)b * c_sell_nb + pos, C);
-    if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, C);  // sweep copy
-}
-
-// XCD-aware tiles: the B systems of a 256-position tile run back to back and
-// share its gather lists and Q in L2. (One coarse slice per workgroup, for L1
-// re-use of the fine blocks, measured equal.)
-template <int BSF>
-__global__ __launch_bounds__(kWG) void k_galerkin(
-    int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
-    const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
-    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
-    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
-    const uint2 *__restrict__ Afh) {
-    int32_t tile, b;
-    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), B, tile, b, kGrpGal)) return;
-    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
-    if (pos >= c_sell_nb) return;
-    galerkin_block<BSF>(pos, b, c_sell_nb, nC, c_sell_row, c_diag, c_dead, gptr, gent, Q, Af, f_sell_nb, Ac, Dh,
-                        Dh22, Ah, Ah22, Afh);
-}
-
 // Level 0's Galerkin product with kNS systems per thread: the gather entry
 // (fine position, P blocks of i and j) and both P blocks are loaded once and
 // applied to the fine blocks of every system (level 0 has 7.5x the entries
 // with a smoothed prolongator). Fine blocks from the smoother's bf16 copy
-// (Afh) or the fp32 A (Af); same fold order per system as galerkin_block.
+// (Afh) or the fp32 A (Af), folded per system in list order.
 // Systems per thread: C3 (512 systems) 6.08 ms per launch at 4, 8.06 at 8,
 // 14.7 at 16 (the per-system fine-block gathers, not the shared gather
 // lists, bound it; more systems per thread only lower the occupancy); one
@@ -402,6 +275,91 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     }
 #pragma unroll
     for (int t = 0; t < kGalNS; ++t) {
+        const int32_t b = b0 + t;
+        if (b >= B) continue;
+        if (pos == c_diag[I]) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                if (c_dead[3 * (int64_t)I + d]) Cm[t][d][d] += 1.f;
+            float D[3][3];
+            inv3(Cm[t], D);
+            st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
+        }
+        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm[t]);
+        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm[t]);
+    }
+}
+
+// Levels >= 1: the Galerkin product with NS systems per thread sharing each
+// gather entry and its two Q blocks (k_galerkin0_ns's scheme for the fp32
+// 3x3 blocks), folded per system in list order. Level 1 at C3 (512 systems):
+// 1217 us per launch with one system per thread (round 2's k_galerkin<3>,
+// 4 entries per load batch), 935 with 2, 851 with 4 (132 VGPRs, 3 waves);
+// C3 +0.5 %, R3 (denser level 1) within noise (round 3).
+constexpr int kGal3NS = 4;
+template <int NS>
+__global__ __launch_bounds__(kWG) void k_galerkin3_ns(
+    int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
+    const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
+    const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
+    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
+#pragma clang fp contract(off)
+    int32_t tile, bq;
+    if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), (B + NS - 1) / NS, tile, bq, kGrpGal)) return;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
+    if (pos >= c_sell_nb) return;
+    const int32_t I = c_sell_row[pos];
+    if (I >= nC) return;
+    const int32_t b0 = bq * NS;
+    float Cm[NS][3][3] = {};
+    const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
+    for (int32_t g = g0; g < g1; ++g) {
+        const int32_t fp = gent[3 * g], ii = gent[3 * g + 1], jj = gent[3 * g + 2];
+        float qi[3][3], qj[3][3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                qi[k][c] = Q[((int64_t)ii * 3 + k) * 3 + c];
+                qj[k][c] = Q[((int64_t)jj * 3 + k) * 3 + c];
+            }
+        float a[NS][3][3];
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            ldm<3>(Af + (int64_t)min(b0 + t, B - 1) * f_sell_nb * kB3, max(fp, 0), a[t]);
+            if (fp < 0) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) a[t][r][k] = (fp == -1 && r == k) ? 1.f : 0.f;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            float T[3][3];  // A Q_j
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) sum += a[t][r][k] * qj[k][c];
+                    T[r][c] = sum;
+                }
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) sum += qi[k][r] * T[k][c];
+                    Cm[t][r][c] += sum;
+                }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
         const int32_t b = b0 + t;
         if (b >= B) continue;
         if (pos == c_diag[I]) {
@@ -1167,7 +1125,6 @@ void launch_post0(int32_t nblk, int32_t B, hipStream_t s, Args... args) {
 }
 
 inline dim3 grid2(int64_t n, int32_t B) { return dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)B); }
-inline dim3 gtile(int64_t n, int32_t B) { return dim3(xcd_grid((int32_t)((n + kWG - 1) / kWG), B, kGrpGal)); }
 
 MatH level0_mat(mof_mesh *m) {
     MatH mt;
@@ -1399,10 +1356,10 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                               ? nullptr
                                               : reinterpret_cast<const uint2 *>(G.A0h.p));
         else
-            k_galerkin<3><<<gtile(C.sell_nb, B), kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p,
-                                                              C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
-                                                              F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
-                                                              nullptr);
+            k_galerkin3_ns<kGal3NS>
+                <<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGal3NS - 1) / kGal3NS, kGrpGal)), kWG,
+                   0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
+                           F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];
     k_coarse_inverse<<<dim3((unsigned)B), kInvWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
