@@ -105,6 +105,7 @@ struct AmgDevice {
     int32_t nc = 0;  // coarsest dofs (dense)
     float omega = 0.85f, omega1 = 1.05f;
     int32_t xm = 2;  // level 0's corrected iterate: 1 in the x0 format in place, 2 fp32 in lv[0].y
+    bool regular = false;  // tentative prolongator on a regular mesh: the bf16 iterates and omega1 1.1
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)

@@ -1204,11 +1204,16 @@ bool amg_build(mof_mesh *m) {
     G.built = true;
     // a mesh that does not coarsen (<= 42 vertices) keeps block Jacobi
     if (H.levels.size() < 2) return false;
-    G.xm = H.levels[0].smoothed ? 2 : 1;
-    // coarse-level damping: 1.1 with the tentative prolongator (round 2, C3
-    // 17.2 -> 17.0 its, +1.8 %; C2 mixed +2 %), 1.05 with the smoothed one
-    // (R3 as measured; 1.2 diverges there with the tentative P)
-    if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = H.levels[0].smoothed ? 1.05f : 1.1f;
+    // The bf16 iterates (x here, z in the PCG) and omega1 = 1.1 were tuned on
+    // the regular meshes; an irregular mesh keeps fp32 and 1.05 whichever
+    // prolongator it runs (round 3: R3 forced onto the tentative P took
+    // 146.5 PCG its/timestep with the regular meshes' choices)
+    G.regular = !H.levels[0].smoothed && !amg_auto_smooth(m->pat);
+    G.xm = G.regular ? 1 : 2;
+    // coarse-level damping: 1.1 on regular meshes (round 2, C3 17.2 -> 17.0
+    // its, +1.8 %; C2 mixed +2 %), 1.05 otherwise (R3 as measured; 1.2
+    // diverges there with the tentative P)
+    if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = G.regular ? 1.1f : 1.05f;
     if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
@@ -1328,6 +1333,7 @@ AmgFine amg_fine(mof_mesh *m) {
     f.x0 = G.lv[0].x.p;
     f.omega = G.omega;
     f.smoothed = G.lv[0].smoothed;
+    f.regular = G.regular;
     return f;
 }
 

@@ -980,9 +980,10 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             a.dA = static_cast<const uint2 *>(f.A0h);
             a.dA_nb = f.sell_nb;
             a.dA_off = f.sell_off;
-            // bf16 z with the tentative prolongator (C3 +1 %, C2 mixed +2 %,
-            // same iterations); R3 on the smoothed one: 63 vs 50 its
-            a.zh = !f.smoothed;
+            // bf16 z on regular meshes with the tentative prolongator (C3
+            // +1 %, C2 mixed +2 %, same iterations); R3 on the smoothed one:
+            // 63 vs 50 its
+            a.zh = f.regular;
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride

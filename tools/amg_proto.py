@@ -25,6 +25,8 @@ mixed solve -- for aggregation-multigrid variants:
   q0=F        the same for the level-0 sweeps (the PCG operator stays exact)
               (formats 5: D^-1/2 A D^-1/2 with D = diag(A), entries in
               [-1, 1] as int8 with the one fixed scale 1/127, rescaled)
+  amax=K      level-0 aggregates of at most K nodes (root + K-1 free
+              neighbours; design study)
   s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
               (from the copy's diagonal blocks) and the level-0 Galerkin
               product all on the stored copy in format F (1 = bf16, today)
@@ -94,15 +96,26 @@ def block_graph(A, bs):
     return Bg
 
 
-def aggregate(G):
+def aggregate(G, amax=0):
     """The library's greedy aggregation (mof_amg_host.cpp aggregate) on CSR
-    adjacency with self loops."""
+    adjacency with self loops. amax > 0 (design study): a root takes at most
+    amax - 1 of its free neighbours (smaller aggregates, more coarse nodes)."""
     n = G.shape[0]
     ptr, col = G.indptr, G.indices
     agg = -np.ones(n, dtype=np.int64)
     na = 0
     for i in range(n):
         nb = col[ptr[i]:ptr[i + 1]]
+        if amax > 0:
+            if agg[i] >= 0:
+                continue
+            free = nb[(agg[nb] < 0) & (nb != i)]
+            if len(free) < amax - 1:
+                continue
+            agg[i] = na
+            agg[free[:amax - 1]] = na
+            na += 1
+            continue
         if (agg[nb] < 0).all():
             agg[nb] = na
             na += 1
@@ -216,7 +229,7 @@ def build(A, a2m, e, opts):
             G = strength_graph(a2m, bs, opts["theta2"])
         G = (G + sp.eye(G.shape[0])).tocsr()
         G.sort_indices()
-        agg, na = aggregate(G)
+        agg, na = aggregate(G, int(opts.get("amax", 0)) if lvl == 0 else 0)
         if na >= n:
             L.coarse = np.linalg.inv(Acur.toarray())
             break
