@@ -1,0 +1,63 @@
+"""The committed measurements reproduce (CPU): the bench line's SpMV roofline
+from the committed rocprof trace, the PMC traffic summary from the committed
+FETCH_SIZE / WRITE_SIZE passes, and the round's headline line's own fields
+(DESIGN.md §4 Roofline, §8)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(REPO, "profiles")
+
+
+def _run(*args):
+    out = subprocess.run([sys.executable] + list(args), cwd=REPO, capture_output=True, text=True, check=True)
+    return out.stdout
+
+
+def test_roofline_reproduces_from_trace():
+    out = json.loads(_run("profiles/roofline_check.py", "profiles/r03_bench_c3_b512_under_rocprof.json",
+                          "profiles/r03_c3_mixed_amg_b512_kernel_trace.csv", "C3/mixed/amg/B512"))
+    assert abs(out["rel_diff"]) < 0.01, out
+    assert out["rocprof_frac"] >= 0.6
+    # measured HBM traffic per full launch within 10 % of the kernel's own bytes
+    line = json.loads(open(os.path.join(P, "r03_bench_c3_b512_under_rocprof.json")).readline())
+    rl = line["roofline"]
+    own = rl["kernel_bytes_per_system"] * 512 + rl["kernel_shared_bytes_per_launch"]
+    assert abs(out["pmc_hbm_bytes_median_launch"] / own - 1.0) < 0.10
+
+
+def test_pmc_summary_reproduces_committed_entry(tmp_path):
+    dst = tmp_path / "pmc.json"
+    _run("profiles/pmc_summary.py", "profiles/r03_pmc_fetch_c3_mixed_amg_b512.csv",
+         "profiles/r03_pmc_write_c3_mixed_amg_b512.csv", str(dst), "C3/mixed/amg/B512", "2048")
+    mine = json.load(open(dst))["C3/mixed/amg/B512"]
+    ref = json.load(open(os.path.join(P, "pmc_traffic.json")))["C3/mixed/amg/B512"]
+    assert mine["kernels"].keys() == ref["kernels"].keys()
+    for k, v in ref["kernels"].items():
+        assert mine["kernels"][k]["hbm_bytes_per_launch"] == pytest.approx(v["hbm_bytes_per_launch"])
+    assert mine["run"]["hbm_bytes_per_timestep"] == pytest.approx(ref["run"]["hbm_bytes_per_timestep"])
+
+
+def test_headline_line_contract():
+    line = json.loads(open(os.path.join(P, "r03_bench_c3_default.json")).readline())
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline",
+                "cpu_baseline", "parity", "host_io"):
+        assert key in line
+    assert line["parity"]["max_abs_err"] < line["parity"]["bar"] == 1e-6
+    assert line["solver"]["failed"] == 0 and line["solver"]["max_rel_residual"] <= 1e-8
+    # value = timed timesteps / (steps x ms_per_step)
+    t = line["config"]["timesteps_timed"] / (line["steps"] * line["ms_per_step"] * 1e-3)
+    assert line["value"] == pytest.approx(t, rel=1e-3)
+    cb = line["cpu_baseline"]
+    assert cb["cores"] >= 1 and cb["host_cpu_count"] >= cb["cores"] and cb["kind"] in ("port", "reference")
+
+
+def test_sq_summary_runs(tmp_path):
+    src = os.path.join(P, "r03_pmc_sq_c3_b512_final_summary.csv")
+    rows = open(src).read().splitlines()
+    assert rows[0].startswith("kernel,dispatches,SQ_WAVES")
+    assert any(r.startswith("k_residual_rcn<2>") for r in rows)
