@@ -584,7 +584,7 @@ inline unsigned upd_blocks(int32_t nblk) { return (unsigned)((nblk + kUpdRB - 1)
 
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
-    __shared__ double lds[8];
+    __shared__ double lds[(kWG / 64) * 2 * kUpdRB];
     const int32_t b = blockIdx.y;
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
@@ -622,41 +622,66 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     using V2 = typename VT<V>::V2;
     // kUpdRB row blocks per workgroup (one partial record each): the update
     // has no gathers, so 1024 rows per workgroup amortise its fixed costs
-    // whatever the row kernels' block size
-    for (int32_t q = 0; q < kUpdRB; ++q) {
-        const int32_t rbk = blockIdx.x * kUpdRB + q;
-        if (rbk >= a.nblk) break;
-        double rz = 0.0, rr = 0.0;
+    // whatever the row kernels' block size. Every load of the kUpdRB rows of
+    // a thread is issued before the first use and the 2 kUpdRB partial sums
+    // are formed by one block_sum (the same per-value order, so the same
+    // bits as one block_sum<2> per row block).
+    static_assert(kRows == 1, "one row per thread and row block");
+    constexpr int R = kUpdRB;
+    int32_t iv[R];
+    V2 qv[R], rv[R];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            const int32_t i = rbk * kRowsPerWG + r * kWG + threadIdx.x;
-            if (i >= a.N) break;
+    for (int q = 0; q < R; ++q) {
+        iv[q] = (blockIdx.x * R + q) * kRowsPerWG + threadIdx.x;
+        const int64_t vi = (int64_t)b * a.N + min(iv[q], a.N - 1);
+        qv[q] = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
+        rv[q] = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
+    }
+    V dv[R][4];
+    uint2 dh[R];
+    if (!a.ext) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) ld_blk(a.dinv, (int64_t)b * a.N + min(iv[q], a.N - 1), dv[q]);
+    } else if constexpr (sizeof(V) == 4) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) dh[q] = bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, min(iv[q], a.N - 1));
+    }
+    double v[2 * R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int32_t i = iv[q];
+        double rz = 0.0, rr = 0.0;
+        if (i < a.N) {
             const int64_t vi = (int64_t)b * a.N + i;
             // x += alpha p happens in the next SpMV launch (it reads p anyway)
-            const V2 qi = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
-            V2 ri = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
-            ri.x = i < a.red.nown ? ri.x - alpha * qi.x : (V)0;
-            ri.y = i < a.red.nown ? ri.y - alpha * qi.y : (V)0;
+            V2 ri = rv[q];
+            ri.x = i < a.red.nown ? ri.x - alpha * qv[q].x : (V)0;
+            ri.y = i < a.red.nown ? ri.y - alpha * qv[q].y : (V)0;
             *reinterpret_cast<V2 *>(a.r + 2 * vi) = ri;
             if (!a.ext) {
-                V d[4];
-                ld_blk(a.dinv, vi, d);
+                const V *d = dv[q];
                 const V z0 = d[0] * ri.x + d[1] * ri.y, z1 = d[2] * ri.x + d[3] * ri.y;
                 *reinterpret_cast<V2 *>(a.z + 2 * vi) = V2{z0, z1};
                 if (i < a.red.nown) rz += (double)ri.x * z0 + (double)ri.y * z1;
             } else if constexpr (sizeof(V) == 4) {
                 // pre-smoothing of the V-cycle with the smoother's D^-1 (bf16)
-                const float2 d = bf16_diag_solve(bf16_diag_block(a.dA, a.dA_nb, a.dA_off, b, i), ri.x, ri.y);
+                const float2 d = bf16_diag_solve(dh[q], ri.x, ri.y);
                 st_x0(a.x0, vi, a.omega * d.x, a.omega * d.y);
             }
             if (i < a.red.nown) rr += (double)ri.x * ri.x + (double)ri.y * ri.y;
         }
-        double v[2] = {rz, rr};
-        block_sum<2>(v, lds);
-        if (threadIdx.x == 0) {
+        v[2 * q] = rz;
+        v[2 * q + 1] = rr;
+    }
+    block_sum<2 * R>(v, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int32_t rbk = blockIdx.x * R + q;
+            if (rbk >= a.nblk) break;
             double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * red_rec(a.red, a.B, blockIdx.y, rbk);
-            o[0] = v[0];
-            o[1] = v[1];
+            o[0] = v[2 * q];
+            o[1] = v[2 * q + 1];
         }
     }
 }
