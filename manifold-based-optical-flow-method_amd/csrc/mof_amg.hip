@@ -1132,6 +1132,7 @@ MatH level0_mat(mof_mesh *m) {
     mt.sell_off = m->sell_off.p;
     mt.sell_col = m->sell_col.p;
     mt.sell_mir = m->sym_reads ? m->sell_mir.p : nullptr;
+    mt.vptr = m->sym_reads ? nullptr : m->vptr.p;
     mt.A = reinterpret_cast<const uint2 *>(m->amg->A0h.p);
     return mt;
 }

@@ -892,6 +892,7 @@ MatArgs<V> make_mat(mof_mesh *m, const V *A) {
     mt.sell_off = m->sell_off.p;
     mt.sell_col = m->sell_col.p;
     mt.sell_mir = m->sym_reads ? m->sell_mir.p : nullptr;
+    mt.vptr = m->sym_reads ? nullptr : m->vptr.p;
     mt.A = A;
     return mt;
 }

@@ -136,8 +136,20 @@ struct MatArgs {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;
     const int32_t *sell_mir;  // mirror table (symmetric reads), or null
+    const int32_t *vptr;      // plain reads: the adjacency row pointers (row i holds
+                              // vptr[i+1] - vptr[i] blocks), or null (slice width)
     const V *A;  // [B][sell_nb][4]
 };
+
+// The slots row i reads in a plain-read pass: its own block count, not the
+// slice width. A lane past its row's blocks re-loads its last block (already
+// in the wave's cache lines) and is masked, so the padding of a slice whose
+// rows are sorted by degree (irregular meshes, mesh_prepare_host) -- whole
+// 128-B lines of tail lanes -- is never fetched (R3: 1.32 M SELL slots for
+// 1.15 M blocks). Bit-identical: a padding slot only ever added 0.
+__device__ __forceinline__ int32_t row_width(const int32_t *vptr, int32_t i, int32_t w) {
+    return vptr ? min(w, vptr[i + 1] - vptr[i]) : w;
+}
 
 // Symmetric reads: the fp32 and bf16 operators read a lower
 // block (i, j), j < i, as the transpose of block (j, i) through the mirror
@@ -164,84 +176,22 @@ __device__ __forceinline__ typename VT<V>::V2 ld2(const V *p) {
 #define MOF_ROW_OCC __attribute__((amdgpu_waves_per_eu(5, 8)))
 constexpr int kSpmvU = 8, kSweepU = 8;
 
-// spmv_row_t for NS fp32 systems of one row per thread: each slot's column
-// index and mirror entry are loaded once for the NS systems (U slots per
-// load batch for each). No fp contraction: every system slot rounds alike.
-// x[t]: system t's operand (bf16 pairs with ZH).
-template <bool sym, int NS, int U, bool ZH>
-__device__ __forceinline__ void spmv_row_ns(const MatArgs<float> &mt, const int32_t (&bs)[NS], int32_t i,
-                                            const float *const (&x)[NS], float (&y)[NS][2]) {
-#pragma clang fp contract(off)
-    const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = mt.sell_off[s];
-    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
-    float acc[NS][2];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.f;
-    for (int32_t t0 = 0; t0 < w; t0 += U) {
-        int32_t j[U], mr[U];
-        int64_t pos[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            pos[u] = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
-            j[u] = mt.sell_col[pos[u]];
-            if constexpr (sym) mr[u] = mt.sell_mir[pos[u]];
-        }
-        if constexpr (sym) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) pos[u] = mir_pos(mr[u], (int64_t)o + l);
-        }
-        float blk[NS][U][4];
-        float2 xj[NS][U];
-#pragma unroll
-        for (int t = 0; t < NS; ++t)
-#pragma unroll
-            for (int u = 0; u < U; ++u) ld_blk(mt.A + 4 * (int64_t)bs[t] * mt.sell_nb, pos[u], blk[t][u]);
-#pragma unroll
-        for (int t = 0; t < NS; ++t)
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if constexpr (ZH) {
-                    const uint32_t h = reinterpret_cast<const uint32_t *>(x[t])[j[u]];
-                    xj[t][u] = float2{bf16_lo(h), bf16_hi(h)};
-                } else {
-                    xj[t][u] = reinterpret_cast<const float2 *>(x[t])[j[u]];
-                }
-            }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            bool on = t0 + u < w;
-            bool tr = false;
-            if constexpr (sym) {
-                on = on && mr[u] >= 0;
-                tr = (mr[u] & kMirT) != 0;
-            }
-#pragma unroll
-            for (int t = 0; t < NS; ++t) {
-                const float b1 = tr ? blk[t][u][2] : blk[t][u][1], b2 = tr ? blk[t][u][1] : blk[t][u][2];
-                acc[t][0] += on ? blk[t][u][0] * xj[t][u].x + b1 * xj[t][u].y : 0.f;
-                acc[t][1] += on ? b2 * xj[t][u].x + blk[t][u][3] * xj[t][u].y : 0.f;
-            }
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        y[t][0] = acc[t][0];
-        y[t][1] = acc[t][1];
-    }
-}
-
 // ZH: the operand is a bf16 pair per row (uint32 each; x points at the
 // system's first one) instead of V2
 template <bool sym, typename V, bool ZH = false>
 __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int32_t i,
                                            const V *__restrict__ x, V &y0, V &y1) {
+    // no fp contraction: the symmetric and the plain instance must round
+    // alike (the fp64 A is bit-symmetric, so both give the same bits), which
+    // contraction left to the code generator would not guarantee
+#pragma clang fp contract(off)
     using V2 = typename VT<V>::V2;
     constexpr int U = kSpmvU;  // fp64: 525 vs 536 us per C2 launch with 4
     const V *A = mt.A + 4 * (int64_t)b * mt.sell_nb;
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
     const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    const int32_t wl = sym ? w : row_width(mt.vptr, i, w);  // this row's slots
     V a0 = 0, a1 = 0;
     for (int32_t t0 = 0; t0 < w; t0 += U) {
         int32_t j[U], mr[U];
@@ -249,13 +199,13 @@ __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int3
         V2 xj[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int32_t t = min(t0 + u, w - 1);
+            const int32_t t = min(t0 + u, wl - 1);
             j[u] = mt.sell_col[(int64_t)o + t * kSlice + l];
             if constexpr (sym) mr[u] = mt.sell_mir[(int64_t)o + t * kSlice + l];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int32_t t = min(t0 + u, w - 1);
+            const int32_t t = min(t0 + u, wl - 1);
             if constexpr (sym)
                 ld_blk(A, mir_pos(mr[u], (int64_t)o + l), blk[u]);
             else
@@ -279,7 +229,7 @@ __device__ __forceinline__ void spmv_row_t(const MatArgs<V> &mt, int32_t b, int3
                 a0 += on ? blk[u][0] * xj[u].x + b1 * xj[u].y : (V)0;
                 a1 += on ? b2 * xj[u].x + blk[u][3] * xj[u].y : (V)0;
             } else {
-                const bool on = t0 + u < w;
+                const bool on = t0 + u < wl;
                 a0 += on ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : (V)0;
                 a1 += on ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : (V)0;
             }
@@ -343,53 +293,9 @@ struct MatH {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;
     const int32_t *sell_mir;  // mirror table (symmetric reads), or null
+    const int32_t *vptr;      // plain reads: row block counts (row_width), or null
     const uint2 *A;  // the level-0 sweep copy (h0_ld), [B][sell_nb] blocks
 };
-
-// spmv_row on the bf16 blocks; the operand of column j comes from
-// xload(j) (a plain gather, or a value formed on the fly); *diag (if given)
-// receives the row's slot 0, the diagonal block
-template <bool sym, int U = kSweepU, typename XL>
-__device__ __forceinline__ void spmv_row_hx_t(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
-                                              float &y1, uint2 *diag) {
-    const uint2 *A = mt.A;  // h0_ld index: system b's positions from b * sell_nb
-    const int32_t s = i >> 6, l = i & 63;
-    const int32_t o = mt.sell_off[s];
-    const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
-    float a0 = 0.f, a1 = 0.f;
-    for (int32_t t0 = 0; t0 < w; t0 += U) {
-        int32_t j[U], mr[U];
-        uint2 blk[U];
-        float2 xj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            j[u] = mt.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-            if constexpr (sym) mr[u] = mt.sell_mir[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            blk[u] = h0_ld(A, (int64_t)b * mt.sell_nb +
-                                  (sym ? mir_pos(mr[u], (int64_t)o + l) : (int64_t)o + min(t0 + u, w - 1) * kSlice + l));
-        if (diag && t0 == 0) *diag = blk[0];
-#pragma unroll
-        for (int u = 0; u < U; ++u) xj[u] = xload(j[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            bool on = t0 + u < w;
-            uint2 h = blk[u];
-            if constexpr (sym) {
-                on = on && mr[u] >= 0;
-                if (mr[u] & kMirT) h = h0_tr(h);  // transpose: swap the off-diagonal entries
-            }
-            float e00, e01, e10, e11;
-            h0_dec(h, e00, e01, e10, e11);
-            a0 += on ? e00 * xj[u].x + e01 * xj[u].y : 0.f;
-            a1 += on ? e10 * xj[u].x + e11 * xj[u].y : 0.f;
-        }
-    }
-    y0 = a0;
-    y1 = a1;
-}
 
 // spmv_row_hx_t for NS systems of one row per thread: the column and mirror
 // loads (shared by all systems) are issued once for the NS systems. No fp
@@ -403,6 +309,7 @@ __device__ __forceinline__ void spmv_row_hx_ns(const MatH &mt, const int32_t (&b
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = mt.sell_off[s];
     const int32_t w = (mt.sell_off[s + 1] - o) >> 6;
+    const int32_t wl = sym ? w : row_width(mt.vptr, i, w);  // this row's slots
     float acc[NS][2];
 #pragma unroll
     for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.f;
@@ -411,7 +318,7 @@ __device__ __forceinline__ void spmv_row_hx_ns(const MatH &mt, const int32_t (&b
         int64_t pos[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            pos[u] = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
+            pos[u] = (int64_t)o + min(t0 + u, wl - 1) * kSlice + l;
             j[u] = mt.sell_col[pos[u]];
             if constexpr (sym) mr[u] = mt.sell_mir[pos[u]];
         }
@@ -435,7 +342,7 @@ __device__ __forceinline__ void spmv_row_hx_ns(const MatH &mt, const int32_t (&b
             for (int u = 0; u < U; ++u) xj[t][u] = xload(t, j[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            bool on = t0 + u < w;
+            bool on = t0 + u < wl;
             bool tr = false;
             if constexpr (sym) {
                 on = on && mr[u] >= 0;
@@ -456,20 +363,6 @@ __device__ __forceinline__ void spmv_row_hx_ns(const MatH &mt, const int32_t (&b
         y[t][0] = acc[t][0];
         y[t][1] = acc[t][1];
     }
-}
-
-template <typename XL>
-__device__ __forceinline__ void spmv_row_hx(const MatH &mt, int32_t b, int32_t i, XL &&xload, float &y0,
-                                            float &y1, uint2 *diag = nullptr) {
-    if (mt.sell_mir)
-        spmv_row_hx_t<true>(mt, b, i, xload, y0, y1, diag);
-    else
-        spmv_row_hx_t<false>(mt, b, i, xload, y0, y1, diag);
-}
-
-__device__ __forceinline__ void spmv_row_h(const MatH &mt, int32_t b, int32_t i, const float *__restrict__ x,
-                                           float &y0, float &y1, uint2 *diag = nullptr) {
-    spmv_row_hx(mt, b, i, [x](int32_t j) { return reinterpret_cast<const float2 *>(x)[j]; }, y0, y1, diag);
 }
 
 // The V-cycle's level-0 iterate: the pre-smoothed x0 = w D^-1 r (written by
