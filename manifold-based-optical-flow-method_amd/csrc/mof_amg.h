@@ -85,9 +85,11 @@ struct AmgDevLevel {
     DevArray<uint8_t> dead;                          // level >= 1
     DevArray<int32_t> agg, mptr, mlist, apos, gptr, gent;  // transition to level + 1
     DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
+    DevArray<int32_t> ggrp;                         // level 0, tentative P: Galerkin groups (coarse
+                                                    // position ranges of <= kWG gather entries)
     bool smoothed = false;                          // level 0: smoothed prolongator
     DevArray<int32_t> pptr, pcol, rptr, rent;
-    int32_t ngrp = 0;
+    int32_t ngrp = 0, nggrp = 0;
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap
     DevArray<float> A;           // [B][sell_nb][12] (level >= 1)

@@ -290,6 +290,108 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     }
 }
 
+// Level 0's Galerkin product by gather entry (tentative prolongator): a
+// workgroup takes a range of coarse positions with at most kWG gather
+// entries in total (ggrp, built on the host), one entry per thread for
+// kGalNS systems -- the entry and its two Q rows loaded once, every fine block
+// of the systems gathered at once -- stages each term Q_i^T A_ij Q_j in LDS,
+// then one thread per (coarse position, system) sums its terms in list order.
+// The same terms in the same order as k_galerkin0_ns (bit-identical), with
+// two dependent loads per thread instead of two per entry of a position.
+// Systems per workgroup (C3, 512 systems, one box, round 3: 4 -> 5288 us per
+// launch, 4 with the first task's position data loaded beside the entry
+// 4978, 2 4670-4735, 1 5613, 8 6271; the old per-position kernel 5952, its
+// reads 32.5 -> 4.35 GB per launch). Spreading the sums over the 9 block
+// entries (every thread busy, a second barrier) took 9376 us.
+constexpr int kGalENS = 2;
+__global__ __launch_bounds__(kWG) void k_galerkin0_ent(
+    int32_t ngrp, const int32_t *__restrict__ ggrp, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ gent, const float *__restrict__ Q, const uint2 *__restrict__ Afh,
+    int64_t f_sell_nb, int64_t c_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
+    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
+    // no fp contraction: every system slot rounds alike, and as k_galerkin0_ns
+#pragma clang fp contract(off)
+    __shared__ float con[kGalENS][9][kWG];
+    int32_t g, bq;
+    const int32_t nq = (B + kGalENS - 1) / kGalENS;
+    if (!xcd_map(ngrp, nq, g, bq, kGrpGal)) return;
+    const int32_t b0 = bq * kGalENS;
+    const int32_t p0 = ggrp[g], p1 = ggrp[g + 1];
+    const int32_t e0 = gptr[p0], e1 = gptr[p1];
+    const int32_t e = e0 + (int32_t)threadIdx.x;
+    const int32_t np = p1 - p0;
+    // the first task's position data, loaded beside the entry's (the tasks
+    // run after the barrier; most groups have one task per thread or fewer)
+    int32_t tI = nC, tq0 = 0, tq1 = 0, tdg = -1;
+    if ((int32_t)threadIdx.x < np * kGalENS) {
+        const int32_t pos = p0 + (int32_t)threadIdx.x / kGalENS;
+        tI = c_sell_row[pos];
+        tq0 = gptr[pos];
+        tq1 = gptr[pos + 1];
+        if (tI < nC) tdg = c_diag[tI];
+    }
+    if (e < e1) {
+        const int32_t fp = gent[3 * (int64_t)e], ii = gent[3 * (int64_t)e + 1], jj = gent[3 * (int64_t)e + 2];
+        float qi[6], qj[6], a[kGalENS][4];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            qi[k] = Q[(int64_t)ii * 6 + k];
+            qj[k] = Q[(int64_t)jj * 6 + k];
+        }
+        const int32_t fq = fp < 0 ? 0 : fp & kMirPos;
+        const bool tr = fp >= 0 && (fp & kMirT);  // transposed upper block
+#pragma unroll
+        for (int t = 0; t < kGalENS; ++t) {
+            const int64_t bb = min(b0 + t, B - 1);
+            h0_dec(h0_ld(Afh, bb * f_sell_nb + fq), a[t][0], a[t][1], a[t][2], a[t][3]);
+            if (tr) {
+                const float t01 = a[t][1];
+                a[t][1] = a[t][2];
+                a[t][2] = t01;
+            }
+            if (fp < 0) {  // a decomposed part's ghost block: identity / zero
+                const float d = fp == -1 ? 1.f : 0.f;
+                a[t][0] = d; a[t][1] = 0.f; a[t][2] = 0.f; a[t][3] = d;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kGalENS; ++t) {
+            float T[2][3];  // A Q_j
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) T[r][c] = 1.f * (a[t][2 * r] * qj[c] + a[t][2 * r + 1] * qj[3 + c]);
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) con[t][3 * r + c][threadIdx.x] = qi[r] * T[0][c] + qi[3 + r] * T[1][c];
+        }
+    }
+    __syncthreads();
+    for (int32_t task = threadIdx.x; task < np * kGalENS; task += kWG) {
+        const int32_t pos = p0 + task / kGalENS, t = task % kGalENS, b = b0 + t;
+        const bool first = task == (int32_t)threadIdx.x;
+        const int32_t I = first ? tI : c_sell_row[pos];
+        if (I >= nC || b >= B) continue;
+        float Cm[3][3] = {};
+        const int32_t q0 = first ? tq0 : gptr[pos], q1 = first ? tq1 : gptr[pos + 1];
+        for (int32_t q = q0; q < q1; ++q)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Cm[k / 3][k % 3] += con[t][k][q - e0];
+        if (pos == (first ? tdg : c_diag[I])) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
+            float D[3][3];
+            inv3(Cm, D);
+            st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
+        }
+        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
+        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+    }
+}
+
 // Levels >= 1: the Galerkin product with NS systems per thread sharing each
 // gather entry and its two Q blocks (k_galerkin0_ns's scheme for the fp32
 // 3x3 blocks), folded per system in list order. Level 1 at C3 (512 systems):
@@ -1269,6 +1371,24 @@ bool amg_build(mof_mesh *m) {
             grp.push_back(na);
             D.ngrp = (int32_t)grp.size() - 1;
             put_i(D.rgrp, grp);
+            // level 0, tentative P: coarse position ranges of <= kWG gather
+            // entries for k_galerkin0_ent (unless a single position has more,
+            // or MOF_GAL_ENT=0)
+            const char *ge = std::getenv("MOF_GAL_ENT");
+            if (l == 0 && !L.smoothed && !(ge && *ge && std::atoi(ge) == 0)) {
+                const std::vector<int32_t> &gq = L.gptr;
+                const int32_t npos = (int32_t)gq.size() - 1;
+                bool ok = true;
+                for (int32_t p = 0; p < npos && ok; ++p) ok = gq[p + 1] - gq[p] <= kWG;
+                if (ok) {
+                    std::vector<int32_t> gg{0};
+                    for (int32_t p = 0; p < npos; ++p)
+                        if (gq[p + 1] - gq[gg.back()] > kWG || p - gg.back() >= kWG) gg.push_back(p);
+                    gg.push_back(npos);
+                    D.nggrp = (int32_t)gg.size() - 1;
+                    put_i(D.ggrp, gg);
+                }
+            }
         }
     }
     G.nc = H.coarse_dofs;
@@ -1354,7 +1474,12 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     G.bf16_fresh = false;
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
-        if (l == 0)
+        if (l == 0 && F.nggrp > 0)
+            k_galerkin0_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
+                F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
+                reinterpret_cast<const uint2 *>(G.A0h.p), m->pat.sell_nb(), C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C),
+                ah22(C));
+        else if (l == 0)
             k_galerkin0_ns<<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGalNS - 1) / kGalNS,
                                            kGrpGal)),
                              kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p,

@@ -214,3 +214,23 @@ def test_smoothed_aggregation_irregular_mesh(monkeypatch):
         Vo = oracle.worker(k, a2, gw, e, iw, t, list(tk), a, 0.01, I[k], I[k + 1])
         for smooth in ("auto", "0"):
             assert np.abs(out[smooth][0][k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), (smooth, k)
+
+
+@pytest.mark.parametrize("case", ["G1_ico642", "G2_cap641"])
+def test_galerkin_by_entry_bit_identical(case, monkeypatch):
+    """The level-0 Galerkin product by gather entry (k_galerkin0_ent, the
+    tentative prolongator's default) forms the same terms in the same order
+    as the per-position kernel (MOF_GAL_ENT=0): the same bits, batch split
+    into partial system quads."""
+    g = load_golden(case)
+    I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    out = []
+    for ent in ("1", "0"):
+        monkeypatch.setenv("MOF_GAL_ENT", ent)
+        m = mesh_of(g)
+        V, st = m.solve_range(I, tk, 0, len(I) - 2, lam, precision="mixed", precond="amg", batch=7)
+        assert st["failed"] == 0 and st["recovered"] == 0
+        out.append((V, st["iterations"]))
+        m.close()
+    assert out[0][1] == out[1][1]
+    assert np.array_equal(out[0][0], out[1][0])
