@@ -223,108 +223,130 @@ __device__ __forceinline__ double dot3_np(const double *x, const double *y) {
     return fma(x[2], y[2], fma(x[1], y[1], __dmul_rn(x[0], y[0])));
 }
 
-// apply_row_rc for NS systems of the batch at once: every incident
-// triangle's geometry and every a2 block is loaded once for all of them (the
-// re-forming residual is bound by those shared gathers). No fp contraction,
-// so every system slot rounds alike (a system's bits must not depend on the
-// slot it lands in, i.e. on the batch split).
+// The re-forming residual's row pieces for NS systems of the batch at once:
+// every a2 block and incident triangle's geometry is loaded once for all of
+// them (the residual is bound by those shared gathers). No fp contraction, so
+// every system slot rounds alike (a system's bits must not depend on the slot
+// it lands in, i.e. on the batch split).
+// rcn_a2: acc += (lambda a2 x)_i, slots in order, kResU per load batch.
+template <int NS>
+__device__ __forceinline__ void rcn_a2(const OpArgs<double> &op, const int32_t (&bs)[NS], int32_t i,
+                                       const double *__restrict__ x64, double (&acc)[NS][2]) {
+#pragma clang fp contract(off)
+    const int32_t s = i >> 6, l = i & 63;
+    const int32_t o = op.sell_off[s];
+    const int32_t w = (op.sell_off[s + 1] - o) >> 6;
+    for (int32_t t0 = 0; t0 < w; t0 += kResU) {
+        int32_t j[kResU];
+        double blk[kResU][4];
+#pragma unroll
+        for (int u = 0; u < kResU; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
+#pragma unroll
+        for (int u = 0; u < kResU; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
+#pragma unroll
+        for (int u = 0; u < kResU; ++u) {
+            const bool on = t0 + u < w;
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                const double2 xj = ld2(x64 + 2 * ((int64_t)bs[t] * op.N + j[u]));
+                acc[t][0] += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : 0.0;
+                acc[t][1] += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : 0.0;
+            }
+        }
+    }
+}
+// The row's own data the incidence terms need.
+template <int NS>
+struct RcnRow {
+    double2 xi[NS];
+    double Ii[NS];
+    double ei[6];
+};
+template <int NS>
+__device__ __forceinline__ void rcn_row(const OpArgs<double> &op, const int32_t (&bs)[NS], int32_t i,
+                                        const double *__restrict__ x64, RcnRow<NS> &R) {
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        R.xi[t] = ld2(x64 + 2 * ((int64_t)bs[t] * op.N + i));
+        R.Ii[t] = op.I0[(int64_t)bs[t] * op.ldI + i];
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) R.ei[q] = op.e[6 * (int64_t)i + q];
+}
+// rcn_tri: the term of incidence q (triangle, corner, the corner's two other
+// vertices) of row i, (a1_T x)_i = u_{T,i} (A_T/12) (2 s_i + s_j + s_k) with
+// u re-formed from the I row in k_tri_step's exact arithmetic (grad I
+// without contraction, np.dot's fma chain); padding entries (T = M) have
+// weight 0.
+template <int NS>
+__device__ __forceinline__ void rcn_tri(const OpArgs<double> &op, const int32_t (&bs)[NS], int4 q,
+                                        const double *__restrict__ x64, const RcnRow<NS> &R,
+                                        double (&val)[NS][2]) {
+#pragma clang fp contract(off)
+    double g[9], ej[6], ek[6], Ij[NS], Ik[NS], wt;
+    double2 xj[NS], xk[NS];
+    const int64_t T = min(q.x, op.M - 1);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g[k] = op.gw[9 * T + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        ej[k] = op.e[6 * (int64_t)q.z + k];
+        ek[k] = op.e[6 * (int64_t)q.w + k];
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const double *Ib = op.I0 + (int64_t)bs[t] * op.ldI;
+        const int64_t vb = (int64_t)bs[t] * op.N;
+        Ij[t] = Ib[q.z];
+        Ik[t] = Ib[q.w];
+        xj[t] = ld2(x64 + 2 * (vb + q.z));
+        xk[t] = ld2(x64 + 2 * (vb + q.w));
+    }
+    wt = op.w12[q.x];
+    const int c = q.y;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const double c0 = c == 0 ? R.Ii[t] : (c == 1 ? Ik[t] : Ij[t]);
+        const double c1 = c == 0 ? Ij[t] : (c == 1 ? R.Ii[t] : Ik[t]);
+        const double c2 = c == 0 ? Ik[t] : (c == 1 ? Ij[t] : R.Ii[t]);
+        double gI[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[d] + c1 * g[3 + d]) + c2 * g[6 + d];
+        const double2 ui = make_double2(dot3_np(gI, R.ei), dot3_np(gI, R.ei + 3));
+        const double2 uj = make_double2(dot3_np(gI, ej), dot3_np(gI, ej + 3));
+        const double2 uk = make_double2(dot3_np(gI, ek), dot3_np(gI, ek + 3));
+        const double si = ui.x * R.xi[t].x + ui.y * R.xi[t].y;
+        const double sj = uj.x * xj[t].x + uj.y * xj[t].y;
+        const double sk = uk.x * xk[t].x + uk.y * xk[t].y;
+        const double cc = wt * ((si + si) + sj + sk);
+        val[t][0] = ui.x * cc;
+        val[t][1] = ui.y * cc;
+    }
+}
+
+// (A x)_i of NS systems: the a2 slots, then the incident triangles in
+// triangle order, one incidence per load batch (kRcU = 1).
 template <int NS>
 __device__ __forceinline__ void apply_row_rcn(const OpArgs<double> &op, const int32_t (&bs)[NS], int32_t i,
                                               const double *__restrict__ x64, double (&y)[NS][2]) {
 #pragma clang fp contract(off)
-    constexpr int U = kRcU;
+    static_assert(kRcU == 1, "one incidence per load batch");
     const int32_t s = i >> 6, l = i & 63;
-    int64_t vb[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) vb[t] = (int64_t)bs[t] * op.N;
     double acc[NS][2];
 #pragma unroll
     for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.0;
-    {
-        const int32_t o = op.sell_off[s];
-        const int32_t w = (op.sell_off[s + 1] - o) >> 6;
-        for (int32_t t0 = 0; t0 < w; t0 += kResU) {
-            int32_t j[kResU];
-            double blk[kResU][4];
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) j[u] = op.sell_col[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) ld_blk(op.a2s, (int64_t)o + min(t0 + u, w - 1) * kSlice + l, blk[u]);
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {
-                const bool on = t0 + u < w;
-#pragma unroll
-                for (int t = 0; t < NS; ++t) {
-                    const double2 xj = ld2(x64 + 2 * (vb[t] + j[u]));
-                    acc[t][0] += on ? blk[u][0] * xj.x + blk[u][1] * xj.y : 0.0;
-                    acc[t][1] += on ? blk[u][2] * xj.x + blk[u][3] * xj.y : 0.0;
-                }
-            }
-        }
-    }
-    {
-        const double *Ib[NS];
-        double2 xi[NS];
-        double Ii[NS];
+    rcn_a2<NS>(op, bs, i, x64, acc);
+    RcnRow<NS> R;
+    rcn_row<NS>(op, bs, i, x64, R);
+    const int32_t o = op.tsell_off[s];
+    const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
+    for (int32_t t0 = 0; t0 < w; ++t0) {
+        double val[NS][2];
+        rcn_tri<NS>(op, bs, op.tinc[(int64_t)o + t0 * kSlice + l], x64, R, val);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
-            Ib[t] = op.I0 + (int64_t)bs[t] * op.ldI;
-            xi[t] = ld2(x64 + 2 * (vb[t] + i));
-            Ii[t] = Ib[t][i];
-        }
-        double ei[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ei[q] = op.e[6 * (int64_t)i + q];
-        const int32_t o = op.tsell_off[s];
-        const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
-        for (int32_t t0 = 0; t0 < w; t0 += U) {
-            int4 q[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) q[u] = op.tinc[(int64_t)o + min(t0 + u, w - 1) * kSlice + l];
-            double g[U][9], ej[U][6], ek[U][6], Ij[U][NS], Ik[U][NS], wt[U];
-            double2 xj[U][NS], xk[U][NS];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t T = min(q[u].x, op.M - 1);  // padding entries (T = M): weight 0
-#pragma unroll
-                for (int k = 0; k < 9; ++k) g[u][k] = op.gw[9 * T + k];
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    ej[u][k] = op.e[6 * (int64_t)q[u].z + k];
-                    ek[u][k] = op.e[6 * (int64_t)q[u].w + k];
-                }
-#pragma unroll
-                for (int t = 0; t < NS; ++t) {
-                    Ij[u][t] = Ib[t][q[u].z];
-                    Ik[u][t] = Ib[t][q[u].w];
-                    xj[u][t] = ld2(x64 + 2 * (vb[t] + q[u].z));
-                    xk[u][t] = ld2(x64 + 2 * (vb[t] + q[u].w));
-                }
-                wt[u] = op.w12[q[u].x];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c = q[u].y;
-                const bool on = t0 + u < w;
-#pragma unroll
-                for (int t = 0; t < NS; ++t) {
-                    const double c0 = c == 0 ? Ii[t] : (c == 1 ? Ik[u][t] : Ij[u][t]);
-                    const double c1 = c == 0 ? Ij[u][t] : (c == 1 ? Ii[t] : Ik[u][t]);
-                    const double c2 = c == 0 ? Ik[u][t] : (c == 1 ? Ij[u][t] : Ii[t]);
-                    double gI[3];
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[u][d] + c1 * g[u][3 + d]) + c2 * g[u][6 + d];
-                    const double2 ui = make_double2(dot3_np(gI, ei), dot3_np(gI, ei + 3));
-                    const double2 uj = make_double2(dot3_np(gI, ej[u]), dot3_np(gI, ej[u] + 3));
-                    const double2 uk = make_double2(dot3_np(gI, ek[u]), dot3_np(gI, ek[u] + 3));
-                    const double si = ui.x * xi[t].x + ui.y * xi[t].y;
-                    const double sj = uj.x * xj[u][t].x + uj.y * xj[u][t].y;
-                    const double sk = uk.x * xk[u][t].x + uk.y * xk[u][t].y;
-                    const double cc = on ? wt[u] * ((si + si) + sj + sk) : 0.0;
-                    acc[t][0] += ui.x * cc;
-                    acc[t][1] += ui.y * cc;
-                }
-            }
+            acc[t][0] += val[t][0];
+            acc[t][1] += val[t][1];
         }
     }
 #pragma unroll
@@ -746,7 +768,11 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
 // over (row block, system group of NS) in the XCD-aware order; per-system
 // partials summed in the same tree as k_residual's. NS = 2; 3 / 4 systems
 // per thread (140 / 160 VGPRs, 3 waves): 5.73 / 6.78 vs 5.73 ms per launch
-// (round 3, one incidence per load batch for 3 and 4).
+// (round 3, one incidence per load batch for 3 and 4). Measured and not kept
+// (round 3, profiles/r03_ab/res_slot/): a row block's incidence slots spread
+// over 4 / 2 thread groups of a 1024 / 512-thread workgroup, the terms
+// staged in LDS and added by the row's thread in slot order (bit-identical):
+// 8421 / 5539 vs 5093 us per launch.
 constexpr int kResNS = 2;
 template <int NS>
 __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
