@@ -19,12 +19,12 @@ def _run(*args):
 
 
 def test_roofline_reproduces_from_trace():
-    out = json.loads(_run("profiles/roofline_check.py", "profiles/r03_bench_c3_b512_under_rocprof.json",
-                          "profiles/r03_c3_mixed_amg_b512_kernel_trace.csv", "C3/mixed/amg/B512"))
+    out = json.loads(_run("profiles/roofline_check.py", "profiles/r03b_bench_c3_b512_under_rocprof.json",
+                          "profiles/r03b_c3_mixed_amg_b512_kernel_trace.csv", "C3/mixed/amg/B512"))
     assert abs(out["rel_diff"]) < 0.01, out
     assert out["rocprof_frac"] >= 0.6
     # measured HBM traffic per full launch within 10 % of the kernel's own bytes
-    line = json.loads(open(os.path.join(P, "r03_bench_c3_b512_under_rocprof.json")).readline())
+    line = json.loads(open(os.path.join(P, "r03b_bench_c3_b512_under_rocprof.json")).readline())
     rl = line["roofline"]
     own = rl["kernel_bytes_per_system"] * 512 + rl["kernel_shared_bytes_per_launch"]
     assert abs(out["pmc_hbm_bytes_median_launch"] / own - 1.0) < 0.10
@@ -32,8 +32,8 @@ def test_roofline_reproduces_from_trace():
 
 def test_pmc_summary_reproduces_committed_entry(tmp_path):
     dst = tmp_path / "pmc.json"
-    _run("profiles/pmc_summary.py", "profiles/r03_pmc_fetch_c3_mixed_amg_b512.csv",
-         "profiles/r03_pmc_write_c3_mixed_amg_b512.csv", str(dst), "C3/mixed/amg/B512", "2048")
+    _run("profiles/pmc_summary.py", "profiles/r03b_pmc_fetch_c3_mixed_amg_b512.csv",
+         "profiles/r03b_pmc_write_c3_mixed_amg_b512.csv", str(dst), "C3/mixed/amg/B512", "4608")
     mine = json.load(open(dst))["C3/mixed/amg/B512"]
     ref = json.load(open(os.path.join(P, "pmc_traffic.json")))["C3/mixed/amg/B512"]
     assert mine["kernels"].keys() == ref["kernels"].keys()
@@ -43,7 +43,7 @@ def test_pmc_summary_reproduces_committed_entry(tmp_path):
 
 
 def test_headline_line_contract():
-    line = json.loads(open(os.path.join(P, "r03_bench_c3_default.json")).readline())
+    line = json.loads(open(os.path.join(P, "r03b_bench_c3_default.json")).readline())
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline",
                 "cpu_baseline", "parity", "host_io"):
         assert key in line

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o run -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $out/bench_under_rocprof.json 2> $out/stats.err || exit 99
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $out/fetch.out 2> $out/fetch.err || exit 99
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-batches 0 --parity-samples 0 "$@" > $out/fetch.out 2> $out/fetch.err || exit 99
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $out/write.out 2> $out/write.err || exit 99
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-batches 0 --parity-samples 0 "$@" > $out/write.out 2> $out/write.err || exit 99
 find $out -name "*.csv" | head -20
