@@ -733,7 +733,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                             int32_t outer_r = 0;
                             return mof::solve_batch(m, nb, rp, s, &outer_r, &st.max_iterations, nullptr, on);
                         },
-                        [&] { m->ws.A64.release(); });
+                        [&] { mof::release_f64_terms(m); });
                 double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[sl].p;
                 mof::launch_to_planar(m, nb, Vdst, s);
                 if (!dev_io) MOF_HIP(hipEventRecord(m->hev[4 + sl], s));

@@ -824,6 +824,19 @@ static void ensure_tri_terms(mof_mesh *m, bool u64, bool u32, hipStream_t s) {
     if (u32) need(w.u32);
 }
 
+// After a mixed solve's fp64 recovery: the fp64 A and the per-triangle term
+// arrays it allocated at the workspace capacity (≈8 GB each at C3, B = 512)
+// go back, so the row-assembly path keeps its headroom (the residual re-forms
+// u when u64 is absent).
+void release_f64_terms(mof_mesh *m) {
+    Workspace &w = m->ws;
+    w.A64.release();
+    w.u64.release();
+    w.u32.release();
+    w.fc.release();
+    w.u64_stale = false;
+}
+
 void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1, int64_t ldI,
                      bool block_jacobi, uint32_t precision, hipStream_t s, bool amg) {
     Workspace &w = m->ws;

@@ -100,6 +100,7 @@ struct mof_dd {
     mof::DevArray<double> vgather;      // [P][B][nmax_own][2] owned V of every part
     int32_t nmax_own = 0;
     mof::DevArray<int32_t> all_l2g;     // [P][nmax_own] owned caller vertices (-1: none)
+    mof::DevArray<double> agree;        // (P) one status word per rank (dd_all_ok), allocated at setup
     double ms_setup = 0.0;
 };
 
@@ -119,5 +120,9 @@ void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s);
 void dd_halo(mof_dd *d, int32_t B, bool f32, int which, hipStream_t s);
 // planar V (B, 2N) in the caller's order from the owned rows of all parts
 void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s);
+// true on every rank iff `ok` on every rank (one all-gather of a status
+// word; in-process: `ok`). Used where one rank can fail alone (a workspace
+// allocation) before collectives every rank must enter.
+bool dd_all_ok(mof_dd *d, bool ok, hipStream_t s);
 
 }  // namespace mof

@@ -225,6 +225,25 @@ void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s) {
                "ncclAllGather(partials)");
 }
 
+bool dd_all_ok(mof_dd *d, bool ok, hipStream_t s) {
+    if (d->rank < 0 || d->P == 1) return ok;
+    const double mine = ok ? 1.0 : 0.0;
+    MOF_HIP(hipMemcpyAsync(d->agree.p + d->rank, &mine, sizeof(double), hipMemcpyHostToDevice, s));
+    if (d->hosted)
+        host_allgather(d, d->agree.p, 1, sizeof(double), s);
+    else
+        nccl_check(d->nccl,
+                   d->nccl->all_gather(d->agree.p + d->rank, d->agree.p, 1, ncclFloat64,
+                                       static_cast<ncclComm_t>(d->comm), s),
+                   "ncclAllGather(status)");
+    std::vector<double> all(d->P);
+    MOF_HIP(hipMemcpyAsync(all.data(), d->agree.p, sizeof(double) * d->P, hipMemcpyDeviceToHost, s));
+    MOF_HIP(hipStreamSynchronize(s));
+    for (double v : all)
+        if (v != 1.0) return false;
+    return true;
+}
+
 // The pack -> exchange -> unpack path: the RCCL transport, or in-process
 // parts with MOF_DD_STAGED (the same kernels and segment offsets, the
 // exchange done by device copies).
@@ -513,6 +532,7 @@ void dd_setup(mof_dd *d, const double *xyz, const double *nrm, const int32_t *tr
             for (int32_t i = 0; i < d->plan.parts[q].n_own; ++i) all[(size_t)q * nmo + i] = d->plan.parts[q].l2g[i];
         d->all_l2g.alloc(all.size());
         d->all_l2g.upload(all.data(), all.size(), d->stream);
+        d->agree.alloc((size_t)P);
     }
     MOF_HIP(hipStreamSynchronize(d->stream));
     d->ms_setup = dd_now_ms() - t0;
@@ -796,7 +816,26 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                         recover_systems(
                             nb, sp, o.max_iter, d->parts[0]->h_sysi, only, st,
                             [&](uint32_t prec) {
-                                dd_ensure(d, nb, prec);
+                                // a workspace allocation can fail on one rank
+                                // only: every rank learns of it before the
+                                // pass's collectives, and all skip the pass
+                                // (its systems stay failed, NaN-filled)
+                                bool ok = true;
+                                Error err{MOF_E_HIP, ""};
+                                try {
+                                    dd_ensure(d, nb, prec);
+                                } catch (const Error &e) {
+                                    if (e.code != MOF_E_HIP) throw;
+                                    (void)hipGetLastError();
+                                    ok = false;
+                                    err = e;
+                                }
+                                if (env_int_dd("MOF_DD_TEST_OOM_RANK", -1) == d->rank && prec == MOF_PREC_F64) {
+                                    ok = false;  // test hook: this rank's fp64 workspace "fails"
+                                    err = Error{MOF_E_HIP, "injected allocation failure"};
+                                }
+                                if (!dd_all_ok(d, ok, s))
+                                    throw ok ? Error{MOF_E_HIP, "workspace allocation failed on another rank"} : err;
                                 for (mof_mesh *m : d->parts) launch_recovery_operator(m, nb, prec, s);
                             },
                             [&](const SolveParams &rp, const uint8_t *on) {
@@ -804,7 +843,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                                 return solve_batch_dd(d, nb, rp, s, &outer_r, &st.max_iterations, on);
                             },
                             [&] {
-                                for (mof_mesh *m : d->parts) m->ws.A64.release();
+                                for (mof_mesh *m : d->parts) release_f64_terms(m);
                             });
                     double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : Vbuf.p;
                     dd_gather_v(d, nb, Vdst, s);

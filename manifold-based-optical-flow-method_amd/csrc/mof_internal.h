@@ -340,6 +340,8 @@ void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, c
 // A (the multigrid assembly keeps D^-1 in bf16 only); with MOF_PREC_F64 the
 // fp64 A and D^-1 (from the u / f terms the assembly left in the workspace).
 void launch_recovery_operator(mof_mesh *m, int32_t B, uint32_t precision, hipStream_t s);
+// the fp64 A and per-triangle term arrays of a recovery pass, released (mof_assemble.hip)
+void release_f64_terms(mof_mesh *m);
 void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision);
 // aggregation multigrid preconditioner (mof_amg.hip)
 bool amg_build(mof_mesh *m);  // hierarchy from the mesh (once); false: mesh too small

@@ -568,7 +568,9 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
 // the fp64 ones keep the compiler's choice (the hint costs C2 fp64 2.7 %)
 template <typename V, bool FIRST, bool ZH = false>
 __global__ __launch_bounds__(kWG) void k_pcg_spmv(PcgArgs<V> a, int32_t it, int32_t flags) {
-    pcg_spmv_body<V, FIRST>(a, it, flags);
+    // bf16 z exists for the fp32 inner solve only (the float specialisations)
+    static_assert(!ZH || sizeof(V) == 4, "bf16 z needs the fp32 SpMV");
+    pcg_spmv_body<V, FIRST, ZH>(a, it, flags);
 }
 #define MOF_SPMV_F32(FIRST, ZH)                                                                              \
     template <>                                                                                              \
@@ -593,12 +595,19 @@ dim3 spmv_grid(const PcgArgs<V> &a) {
 template <typename V>
 void launch_spmv(const PcgArgs<V> &a, bool first, dim3, hipStream_t s, int32_t it, int32_t flags) {
     const dim3 g = spmv_grid(a);
-    if (first)
-        a.zh ? k_pcg_spmv<V, true, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags)
-             : k_pcg_spmv<V, true, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
-    else
-        a.zh ? k_pcg_spmv<V, false, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags)
-             : k_pcg_spmv<V, false, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+    constexpr bool zh_ok = sizeof(V) == 4;
+    if (zh_ok && a.zh) {
+        if constexpr (zh_ok) {
+            if (first)
+                k_pcg_spmv<V, true, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+            else
+                k_pcg_spmv<V, false, true><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+        }
+    } else if (first) {
+        k_pcg_spmv<V, true, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+    } else {
+        k_pcg_spmv<V, false, false><<<g, spmv_wg<V>(), 0, s>>>(a, it, flags);
+    }
 }
 
 constexpr int kUpdRB = 4;  // row blocks per update workgroup
@@ -1081,8 +1090,9 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 // events stamped by the kernel's own dispatch packet (start
                 // and end of its execution, as rocprof's kernel trace), not
                 // separate marker packets around it
-                auto kf = it == 0 ? (a.zh ? k_pcg_spmv<V, true, true> : k_pcg_spmv<V, true, false>)
-                                  : (a.zh ? k_pcg_spmv<V, false, true> : k_pcg_spmv<V, false, false>);
+                constexpr bool zh_ok = sizeof(V) == 4;
+                auto kf = it == 0 ? (zh_ok && a.zh ? k_pcg_spmv<V, true, zh_ok> : k_pcg_spmv<V, true, false>)
+                                  : (zh_ok && a.zh ? k_pcg_spmv<V, false, zh_ok> : k_pcg_spmv<V, false, false>);
                 hipExtLaunchKernelGGL(kf, spmv_grid(a), dim3(spmv_wg<V>()), 0, s, ev[2 * c], ev[2 * c + 1], 0, a, it, 0);
             } else {
                 launch_spmv(a, it == 0, gx, s, it, 0);

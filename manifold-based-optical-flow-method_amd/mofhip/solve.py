@@ -9,9 +9,12 @@ concatenated in k order (:190-191). No collective is involved.
 Checkpoint / resume (``checkpoint=`` a directory): each device's range is
 solved in chunks of ``chunk`` timesteps, every finished chunk is written as
 ``V_<k0>_<k1>.npy`` (atomically, with a fingerprint of the mesh, the
-chunk's I rows, t_k, lambda and the solver options), and a rerun loads the
-chunks whose fingerprint matches instead of solving them again -- the
-shard-granular counterpart of S3's stage outputs (S3…py:122-137).
+chunk's I rows, t_k, lambda, the solver options, the library version and
+the MOF_* environment switches that change V or convergence), and a rerun
+loads the chunks whose fingerprint matches instead of solving them again --
+the shard-granular counterpart of S3's stage outputs (S3…py:122-137). A
+chunk with failed (NaN-filled) systems is written but never reused: a rerun
+solves it again, so a resume cannot hide a failure.
 """
 from __future__ import annotations
 
@@ -54,12 +57,28 @@ def _digest(*parts) -> str:
     return h.hexdigest()
 
 
+def _library_key() -> tuple:
+    """Library version and ABI, and the MOF_* environment switches (sorted):
+    a rebuilt library or another solver setting must not reuse old chunks."""
+    try:
+        from . import _lib as L
+        lib = L.lib()
+        ver = (lib.mof_version().decode(), int(lib.mof_abi_version()))
+    except Exception:  # no library (CPU tests with a stand-in mesh)
+        ver = ("", 0)
+    env = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("MOF_")
+                       and k != "MOF_CHECKPOINT_DIR"))
+    return ver, env
+
+
 def chunk_fingerprint(mesh, I, I2, t_k, a, b, lambda_, opts) -> str:
-    """What a saved chunk's V depends on: the mesh, timesteps [a, b)'s I rows
-    (I[a:b] and I2[a+1:b+1]), t_k[a:b+1], lambda and the solver options."""
+    """What a saved chunk's V depends on: the mesh (and its device vertex
+    order), timesteps [a, b)'s I rows (I[a:b] and I2[a+1:b+1]), t_k[a:b+1],
+    lambda, the solver options and the library / environment key."""
     I2 = I if I2 is None else I2
-    return _digest(mesh.fingerprint(), np.asarray(I[a:b]), np.asarray(I2[a + 1:b + 1]),
-                   np.asarray(t_k[a:b + 1], dtype=np.float64), float(lambda_), sorted(opts.items()))
+    return _digest(mesh.fingerprint(), bool(getattr(mesh, "reorder", True)), np.asarray(I[a:b]),
+                   np.asarray(I2[a + 1:b + 1]), np.asarray(t_k[a:b + 1], dtype=np.float64), float(lambda_),
+                   sorted(opts.items()), _library_key())
 
 
 class Checkpoint:
@@ -73,20 +92,26 @@ class Checkpoint:
         stem = os.path.join(self.path, "V_%09d_%09d" % (a, b))
         return stem + ".npy", stem + ".json"
 
-    def load(self, a, b, fp, out) -> bool:
+    def load(self, a, b, fp, out):
+        """The saved chunk's stats (its V copied into ``out``), or None when
+        there is no usable chunk: missing, another fingerprint, another shape,
+        or one with failed systems (those are solved again)."""
         vf, mf = self._files(a, b)
         try:
             with open(mf) as f:
                 meta = json.load(f)
             if meta.get("fingerprint") != fp:
-                return False
+                return None
+            stats = dict(meta.get("stats") or {})
+            if int(stats.get("failed", 0)) > 0:
+                return None
             arr = np.load(vf, mmap_mode="r", allow_pickle=False)
             if arr.shape != out.shape:
-                return False
+                return None
             out[...] = arr
-            return True
-        except (OSError, ValueError):
-            return False
+            return stats
+        except (OSError, ValueError, TypeError):
+            return None
 
     def save(self, a, b, fp, V, stats):
         vf, mf = self._files(a, b)
@@ -129,8 +154,11 @@ def velocity_field_sharded(mesh, I, t_k, k0, k1, lambda_, I2=None, devices=(0,),
                 c1 = min(b, c0 + csize)
                 dst = V[c0 - k0:c1 - k0]
                 fp = chunk_fingerprint(mesh, I, I2, t_k, c0, c1, lambda_, opts)
-                if ck.load(c0, c1, fp, dst):
-                    st = {"systems": 0, "failed": 0, "resumed": c1 - c0}
+                saved = ck.load(c0, c1, fp, dst)
+                if saved is not None:
+                    # the saved run's counts (systems, iterations, ...) carry
+                    # over; nothing was solved now
+                    st = dict(saved, resumed=c1 - c0)
                 else:
                     _, st = mesh.solve_range(I, t_k, c0, c1, lambda_, I2=I2, device=dev, out=dst, **opts)
                     ck.save(c0, c1, fp, dst, st)

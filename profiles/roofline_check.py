@@ -7,9 +7,12 @@ processed (bytes_per_launch = bytes_per_system x systems_per_launch +
 the shared column indices of every launch with work, averaged over the
 timed launches) and times each launch with events stamped by the kernel's
 own dispatch packet. This script divides the same bytes by rocprof's
-average duration of the same launches -- from a kernel trace, the last
-`launches` SpMV launches of the run (the timed region follows the warmup,
-whose first batch has more early-exit launches); from a kernel summary, all
+average duration of the same launches -- from a kernel trace, the SpMV
+launches of the timed region: every batch starts with one `k_gather_I`
+launch, so the timed batches are those from batch `warmup * b` to batch
+`(warmup + steps) * b` (b batches per step), and the SpMV launches between
+those two `k_gather_I` starts are the timed ones (the host-IO leg and the
+parity solves after the clock are excluded); from a kernel summary, all
 SpMV launches (both template instances) -- and prints both fractions of the
 8 TB/s peak, and the full-launch durations side by side.
 With a pmc_traffic.json key it also prints measured HBM bytes per launch
@@ -22,6 +25,22 @@ import sys
 PEAK_GBS = 8000.0
 
 
+def timed_launches(rows, line, prefix):
+    """Durations (us) of the SpMV launches inside the bench line's timed
+    region of a rocprofv3 kernel trace, bounded by the batches' k_gather_I
+    launches (see the module docstring)."""
+    cfg = line["config"]
+    per_step = -(-int(cfg["timesteps_per_step"]) // int(cfg.get("batch_effective") or cfg["batch"]))
+    first, last = line["warmup"] * per_step, (line["warmup"] + line["steps"]) * per_step
+    marks = sorted(int(r["Start_Timestamp"]) for r in rows if "k_gather_I(" in r["Kernel_Name"])
+    if len(marks) < last:
+        raise SystemExit("trace holds %d batches, the line's timed region ends at batch %d" % (len(marks), last))
+    t0 = marks[first]
+    t1 = marks[last] if len(marks) > last else float("inf")
+    return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
+            if prefix in r["Kernel_Name"] and t0 <= int(r["Start_Timestamp"]) < t1]
+
+
 def main():
     line = json.loads(open(sys.argv[1]).readline())
     rl = line["roofline"]
@@ -29,8 +48,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[2])))
     full_us = None
     if rows and "Start_Timestamp" in rows[0]:
-        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
-             if prefix in r["Kernel_Name"]][-rl["launches"]:]
+        d = timed_launches(rows, line, prefix)
         n, us = len(d), sum(d) / len(d)
         full = sorted(d)[-rl["full_launches"]:] if rl.get("full_launches") else []
         full_us = sum(full) / len(full) if full else None

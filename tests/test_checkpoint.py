@@ -82,3 +82,45 @@ def test_no_checkpoint_writes_in_place():
     assert [c[1:] for c in m.calls] == [(3, 9), (9, 15), (15, 20)]
     ref = np.stack([np.concatenate([I[k] * 2.0, I[k + 1] + tk[k]]) for k in range(3, 20)])
     assert np.array_equal(V, ref)
+
+
+class _FailingMesh(_Mesh):
+    """Reports one failed (NaN-filled) system in every chunk containing k = 5."""
+
+    def solve_range(self, I, t_k, k0, k1, lam, I2=None, device=None, out=None, **opts):
+        out, st = super().solve_range(I, t_k, k0, k1, lam, I2=I2, device=device, out=out, **opts)
+        if k0 <= 5 < k1:
+            out[5 - k0] = np.nan
+            st = dict(st, failed=1)
+        return out, st
+
+
+def test_failed_chunks_are_solved_again(tmp_path):
+    I, tk = _inputs()
+    m = _FailingMesh()
+    _, st1 = velocity_field_sharded(m, I, tk, 0, 12, 0.5, checkpoint=str(tmp_path), chunk=4)
+    assert sum(s["failed"] for s in st1) == 1
+    n1 = len(m.calls)
+    # the rerun reuses the clean chunks (with their saved counts) and solves
+    # the failed one again, whose failure is reported again
+    V2, st2 = velocity_field_sharded(m, I, tk, 0, 12, 0.5, checkpoint=str(tmp_path), chunk=4)
+    assert m.calls[n1:] == [(0, 4, 8)]
+    assert st2[0]["failed"] == 1
+    assert st2[0]["resumed"] == 8
+    assert st2[0]["systems"] == 12  # saved 4 + 4, solved 4
+    assert np.isnan(V2[5]).all()
+
+
+def test_environment_switches_invalidate_chunks(tmp_path, monkeypatch):
+    I, tk = _inputs()
+    m = _Mesh()
+    monkeypatch.delenv("MOF_PCG_STALL", raising=False)
+    velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
+    velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
+    assert len(m.calls) == 1
+    monkeypatch.setenv("MOF_PCG_STALL", "32")  # a solver switch: the chunk is stale
+    velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
+    assert len(m.calls) == 2
+    m.reorder = False  # another device vertex order: stale as well
+    velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
+    assert len(m.calls) == 3

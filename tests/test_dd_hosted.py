@@ -33,8 +33,9 @@ def _case():
     return p, t, n, a, synth.travelling_wave(p, 6)
 
 
-def _rank_worker(rank, world, port, part, opts, out):
+def _rank_worker(rank, world, port, part, opts, out, env=None):
     import sys
+    os.environ.update(env or {})
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     sys.path.insert(0, os.path.join(repo, "manifold-based-optical-flow-method_amd"))
@@ -83,3 +84,43 @@ def test_host_transport_ranks_match_in_process(P, opts):
         assert local == 1 and r == rank, V
         assert failed == 0 and its == sr["iterations"]
         assert np.array_equal(V, Vr)  # every rank receives the whole V, bit for bit
+
+
+@pytest.mark.parametrize("oom_rank", [-1, 1])
+def test_recovery_allocation_failure_agreed_by_all_ranks(oom_rank):
+    """The fp64 recovery pass allocates its workspace per rank; a failure on
+    one rank (injected: MOF_DD_TEST_OOM_RANK) is agreed by an all-gather of a
+    status word before the pass's collectives, so every rank skips the pass
+    and returns its systems NaN-filled instead of hanging in the halo
+    exchange. Without the failure the same pass recovers
+    every system. The first solve fails by construction (2 inner iterations,
+    one refinement step)."""
+    import torch.multiprocessing as mp
+    from mofhip import DecomposedMesh
+    p, t, n, a, I = _case()
+    P = 2
+    part = np.random.default_rng(5).integers(0, P, len(p)).astype(np.int32)
+    opts = {"precision": "mixed", "batch": 3, "max_iter": 2, "max_outer": 1}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env = {"MOF_DD_TEST_OOM_RANK": str(oom_rank)}
+    procs = [ctx.Process(target=_rank_worker, args=(r, P, port, part, opts, q, env)) for r in range(P)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(P)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    T = len(I) - 1
+    for rank, local, r, V, its, failed in res:
+        assert local == 1 and r == rank, V
+        if oom_rank < 0:
+            assert failed == 0 and np.isfinite(V).all()
+        else:
+            assert failed == T and np.isnan(V).all()
+    if oom_rank < 0:
+        ref = DecomposedMesh(p, n, t, a, P, part=part, staged=True)
+        Vr, _ = ref.solve_range(I, np.arange(len(I), dtype=np.float64), 0, T, 0.01, precision="f64", batch=3)
+        ref.close()
+        assert np.max(np.abs(res[0][3] - Vr)) < 1e-6

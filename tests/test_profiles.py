@@ -23,6 +23,11 @@ def test_roofline_reproduces_from_trace():
                           "profiles/r03b_c3_mixed_amg_b512_kernel_trace.csv", "C3/mixed/amg/B512"))
     assert abs(out["rel_diff"]) < 0.01, out
     assert out["rocprof_frac"] >= 0.6
+    # the timed region's launches, bounded by the batches' k_gather_I launches
+    # (batches 2-6 of this trace: not the host-IO leg after the clock)
+    line0 = json.loads(open(os.path.join(P, "r03b_bench_c3_b512_under_rocprof.json")).readline())
+    assert out["rocprof_launches"] == line0["roofline"]["launches"] == 95
+    assert 1760.0 < out["rocprof_us_per_launch"] < 1770.0
     # measured HBM traffic per full launch within 10 % of the kernel's own bytes
     line = json.loads(open(os.path.join(P, "r03b_bench_c3_b512_under_rocprof.json")).readline())
     rl = line["roofline"]
