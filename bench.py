@@ -53,7 +53,12 @@ CONFIG_NAMES = {
     "C5": "640k-vertex jittered icosphere (n=253, 640,092 vertices)",
     "R3": "163,842-vertex irregular random-hull sphere (valence 3-14, random vertex order)",
     "P3": "C3 mesh with randomly relabelled vertices (no index locality)",
+    "S1": "160,801-vertex S1-like reconstructed patch (51 x 51 electrode grid, Delaunay, butterfly x3, smoothed)",
+    "S1s": "3,249-vertex S1-like reconstructed patch (8 x 8 electrode grid), T=98 (97 solves), the reference's "
+           "real workload size (config.yaml:5, find_singularity_point.py:19-20)",
 }
+# small jobs timed whole: one step = every timestep of the job (one batch)
+SMALL_JOBS = {"C1": 15, "S1s": 97}
 
 
 def parse():
@@ -81,6 +86,8 @@ def parse():
                     help="device: I/V resident in HBM; host: pageable numpy in and out (drop-in path)")
     ap.add_argument("--parity-samples", type=int, default=2,
                     help="timesteps of the last timed batch checked against the oracle + spsolve (0: none)")
+    ap.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
+                    help="fp64: the one-launch fused solve per batch (auto: the library's choice, small meshes)")
     ap.add_argument("--host-batches", type=int, default=4,
                     help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
                          "the device-resident region (0: none)")
@@ -215,8 +222,8 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0)
 
 def main():
     args = parse()
-    if args.config == "C1":  # the whole T = 16 job is one step (one batch of 15 timesteps)
-        args.fixed_timesteps = args.fixed_timesteps or 15
+    if args.config in SMALL_JOBS:  # the whole job is one step (one batch: C1 15, S1s 97 timesteps)
+        args.fixed_timesteps = args.fixed_timesteps or SMALL_JOBS[args.config]
         args.batch = min(args.batch, args.fixed_timesteps)
     self_launch(args)
     from mofhip.dist import max_over_ranks, rank_env, rank_k_range, sum_over_ranks
@@ -293,7 +300,8 @@ def main():
     tk = np.arange(K_rank + 1, dtype=np.float64)
     sync()
     precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
-    opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol)
+    opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol,
+                fused={"auto": None, "on": True, "off": False}[args.fused])
 
     kept = []  # host V of the timed calls, freed after the clock stops (the caller keeps its result)
 
@@ -302,7 +310,8 @@ def main():
         if dry:
             return dict.fromkeys(("iterations", "failed", "recovered", "ms_spmv", "spmv_bytes", "spmv_launches",
                                   "spmv_systems", "spmv_full_launches", "ms_spmv_full", "ms_assembly",
-                                  "ms_solve", "max_rel_residual", "outer_steps"), 0) | {"systems": b - a}
+                                  "ms_solve", "max_rel_residual", "outer_steps", "fused_launches",
+                                  "ms_fused"), 0) | {"systems": b - a}
         if host_io:
             V, st = mesh.solve_range(I_host, tk, a, b, args.lambda_, device=local, time_spmv=timed, **opts)
             if timed:
@@ -341,11 +350,12 @@ def main():
     t0 = time.perf_counter()
     agg = {"iterations": 0, "failed": 0, "recovered": 0, "ms_spmv": 0.0, "spmv_bytes": 0.0, "spmv_launches": 0,
            "spmv_systems": 0, "spmv_full_launches": 0, "ms_spmv_full": 0.0, "max_rel_residual": 0.0,
-           "ms_assembly": 0.0, "ms_solve": 0.0, "systems": 0}
+           "ms_assembly": 0.0, "ms_solve": 0.0, "systems": 0, "fused_launches": 0, "ms_fused": 0.0}
     for a_, b_ in timed_calls:
         st = solve(a_, b_, True)
         for k in ("iterations", "failed", "recovered", "ms_spmv", "spmv_bytes", "spmv_launches", "spmv_systems",
-                  "spmv_full_launches", "ms_spmv_full", "ms_assembly", "ms_solve", "systems"):
+                  "spmv_full_launches", "ms_spmv_full", "ms_assembly", "ms_solve", "systems", "fused_launches",
+                  "ms_fused"):
             agg[k] += st[k]
         agg["max_rel_residual"] = max(agg["max_rel_residual"], st["max_rel_residual"])
         agg["max_outer_steps"] = max(agg.get("max_outer_steps", 0), st["outer_steps"])
@@ -455,7 +465,7 @@ def main():
     parity = parity_check(geom, t, a, args.lambda_, samples) if samples else None
     if rank == 0 and not args.no_cpu_baseline and not dry:
         cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom,
-                           full_timesteps=args.fixed_timesteps if args.config == "C1" else 0)
+                           full_timesteps=args.fixed_timesteps if args.config in SMALL_JOBS else 0)
 
     if rank == 0:
         line = {
@@ -487,7 +497,12 @@ def main():
                        "ms_assembly_per_timestep": round(agg["ms_assembly"] / n_local, 4),
                        "ms_solve_per_timestep": round(agg["ms_solve"] / n_local, 4),
                        "mesh_build_s": round(mesh_s, 3), "mesh_geometry_ms": round(info["ms_geometry"], 3),
-                       "mesh_pattern_ms": round(info["ms_pattern"], 3)},
+                       "mesh_pattern_ms": round(info["ms_pattern"], 3),
+                       # the one-launch fp64 solve per batch (small meshes): its
+                       # launches and kernel time (no per-SpMV timing there)
+                       "fused_launches": agg["fused_launches"],
+                       "ms_fused_per_launch": round(agg["ms_fused"] / agg["fused_launches"], 4)
+                       if agg["fused_launches"] else None},
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -33,7 +33,7 @@ extern "C" {
  * mof_mesh_info blocks_read; mof_mesh_clone). A binding checks
  * mof_abi_version() == MOF_ABI_VERSION of the header it was built against:
  * the library writes whole structs, so a stale header would be overrun. */
-#define MOF_ABI_VERSION 2
+#define MOF_ABI_VERSION 3
 
 /* status codes */
 #define MOF_OK 0
@@ -87,6 +87,15 @@ extern "C" {
                                   fp64 workspace cannot be allocated leaves
                                   its systems NaN-filled (MOF_E_NOCONV)
                                   rather than failing the call */
+#define MOF_SOLVE_FUSED 128u   /* MOF_PREC_F64: solve each batch in one launch,
+                                  one workgroup per system (the eager
+                                  kernels' bodies run row block by row block;
+                                  bit-identical V, flags and iteration
+                                  counts). Default: on for meshes of at most
+                                  16 row blocks of 256 vertices
+                                  (MOF_FUSED_MAX_BLK), where the eager
+                                  launches are latency-bound */
+#define MOF_SOLVE_EAGER 256u   /* never the fused solve */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */
@@ -136,6 +145,8 @@ typedef struct mof_stats {
     int32_t recovered;        /* systems the first solve failed and a recovery
                                  solve (block Jacobi, then fp64) solved */
     int32_t recovered_f64;    /* of those, solved by the fp64 recovery */
+    int64_t fused_launches;   /* MOF_TIME_SPMV: fused solves (one per batch) ... */
+    double ms_fused;          /* ... and their summed kernel time */
 } mof_stats;
 
 typedef struct mof_mesh_info {

@@ -614,6 +614,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         sp.stall = sp.amg ? env_int("MOF_PCG_STALL", 64) : 0;
         sp.fail_at_max_iter = sp.amg;
         sp.adaptive_inner = env_int("MOF_FIXED_INNER_RTOL", 0) == 0;
+        sp.fused = (o.flags & MOF_SOLVE_EAGER) ? 0 : ((o.flags & MOF_SOLVE_FUSED) ? 1 : -1);
         const bool recovery = !(o.flags & MOF_NO_RECOVERY);
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
         if (!I2) I2 = I;
@@ -768,6 +769,8 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         st.spmv_systems = timing.systems;
         st.spmv_full_launches = timing.full_launches;
         st.ms_spmv_full = timing.ms_full;
+        st.fused_launches = timing.fused_launches;
+        st.ms_fused = timing.ms_fused;
         if (stats) *stats = st;
         if (st.failed) {
             nonconv = 1;

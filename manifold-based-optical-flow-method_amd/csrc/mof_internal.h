@@ -161,8 +161,12 @@ struct Workspace {
 //  SD_RR0 / SD_BEST: |r|^2 at the start of the inner solve / smallest so far
 //  SI_BEST_IT: iteration of SD_BEST (stagnation detector)
 //  SI_FAIL_IT / SI_FAIL_WHY: inner iteration and reason (FailWhy) of a failure
-enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST = 5 };
-enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_BEST_IT = 4, SI_FAIL_IT = 5, SI_FAIL_WHY = 6 };
+//  SI_ITSUM / SI_ITMAX / SD_OUTER: the fused solve's (k_solve_fused) inner
+//  iterations summed over its refinement steps, the largest inner solve, and
+//  the refinement steps taken (the eager path counts these on the host)
+enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST = 5, SD_OUTER = 6 };
+enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_ITSUM = 3, SI_BEST_IT = 4, SI_FAIL_IT = 5, SI_FAIL_WHY = 6,
+            SI_ITMAX = 7 };
 enum FailWhy { FW_BREAKDOWN = 1, FW_DIVERGED = 2, FW_STALLED = 3, FW_MAXITER = 4, FW_RESIDUAL = 5 };
 constexpr int kSysStride = 8;
 
@@ -300,6 +304,8 @@ struct SpmvTiming {
     int64_t full_launches = 0;   // launches in which every system of the solve worked
     double ms = 0.0, bytes = 0.0;
     double ms_full = 0.0;        // their summed time
+    int64_t fused_launches = 0;  // fused solves (k_solve_fused), one per batch ...
+    double ms_fused = 0.0;       // ... and their summed time
 };
 
 // Algorithmic bytes of one k_pcg_spmv launch over `active` systems
@@ -322,6 +328,10 @@ struct SolveParams {
     // refinement steps after the first: per-system inner tolerance from the
     // outer residual still missing (k_pcg_tol); MOF_FIXED_INNER_RTOL=1: off
     bool adaptive_inner = true;
+    // the whole fp64 solve of a batch in one launch, one workgroup per system
+    // (k_solve_fused): 0 never, 1 when the batch is eligible, -1 auto (small
+    // meshes: row blocks <= MOF_FUSED_MAX_BLK)
+    int32_t fused = -1;
 };
 // Solve the B assembled systems in the workspace; fills sysd/sysi.
 // Returns total inner iterations; sets *outer to the refinement steps used.

@@ -359,16 +359,20 @@ __device__ __forceinline__ void apply_row_rcn(const OpArgs<double> &op, const in
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
 
 
+// The row kernels' bodies take their (row block, system) as arguments: the
+// __global__ wrappers map blockIdx to them, and the fused small-mesh solve
+// (k_solve_fused) runs the same bodies over every row block of its system in
+// one workgroup -- the same arithmetic in the same order, so the same bits.
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__restrict__ rhs) {
+__device__ __forceinline__ void pcg_init_rows(const PcgArgs<V> &a, const double *__restrict__ rhs, int32_t rb,
+                                              int32_t b) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.y;
     if (!a.sysi[b * kSysStride + SI_ACTIVE]) return;
     using V2 = typename VT<V>::V2;
     double rz = 0.0, rr = 0.0;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-        const int32_t i = blockIdx.x * kRowsPerWG + r * kWG + threadIdx.x;
+        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= a.N) break;
         const int64_t vi = (int64_t)b * a.N + i;
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
@@ -393,10 +397,14 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
     double v[2] = {rz, rr};
     block_sum<2>(v, lds);
     if (threadIdx.x == 0) {
-        double *o = a.part_rzrr + 2 * red_rec(a.red, a.B, b, blockIdx.x);  // slot 0
+        double *o = a.part_rzrr + 2 * red_rec(a.red, a.B, b, rb);  // slot 0
         o[0] = v[0];
         o[1] = v[1];
     }
+}
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__restrict__ rhs) {
+    pcg_init_rows<V>(a, rhs, blockIdx.x, blockIdx.y);
 }
 
 // The scalars of the PCG recurrences are reduced once per system
@@ -405,9 +413,8 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
 // partial record -- which is what lets the row kernels use small (256-row)
 // workgroups.
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
+__device__ __forceinline__ void red_rzrr_sys(const PcgArgs<V> &a, int32_t slot, int32_t b) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.x;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
     double v[2];
     reduce_sys<2>(a.part_rzrr + slot * ps, a.red, a.B, b, v, lds);
@@ -418,13 +425,20 @@ __global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
     }
 }
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
+__global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
+    red_rzrr_sys<V>(a, slot, blockIdx.x);
+}
+template <typename V>
+__device__ __forceinline__ void red_pq_sys(const PcgArgs<V> &a, int32_t slot, int32_t b) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.x;
     const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;
     double v[1];
     reduce_sys<1>(a.part_pq + slot * pqs, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) *sc_pq(a.sc, a.B, slot, b) = v[0];
+}
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
+    red_pq_sys<V>(a, slot, blockIdx.x);
 }
 
 // One workgroup per system: tolerance from |rhs|^2, reset the convergence word.
@@ -434,9 +448,8 @@ __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
 // steps: the fp32 operator's rounding limits a step to ~3e-4 there) takes a
 // short inner solve, not a full 1e-4 one.
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, double outer_rtol) {
+__device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, double outer_rtol, int32_t b) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.x;
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) {
         if (threadIdx.x == 0) si[SI_CONV] = 0;
@@ -457,13 +470,15 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, doub
         si[SI_CONV] = -1;
     }
 }
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, double outer_rtol) {
+    pcg_tol_sys<V>(a, rtol, outer_rtol, blockIdx.x);
+}
 
 template <typename V, bool FIRST, bool ZH = false>
-__device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
+__device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, int32_t flags, int32_t rb, int32_t b) {
     constexpr int NT = kWG, RPT = kRows;  // rows per thread
     __shared__ double lds[2 * (NT / 64)];
-    int32_t rb, b;
-    if (!xcd_map(a.nblk, a.B, rb, b, kGrpSpmv)) return;
     const bool force = flags & kForce;
     // retired systems: inactive, or converged in an earlier iteration (the
     // word is sticky, so no later launch re-reads a stale partial slot)
@@ -558,6 +573,12 @@ __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, i
     block_sum<1, NT>(v, lds);
     if (threadIdx.x == 0) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, b, rb)] = v[0];
 }
+template <typename V, bool FIRST, bool ZH = false>
+__device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
+    int32_t rb, b;
+    if (!xcd_map(a.nblk, a.B, rb, b, kGrpSpmv)) return;
+    pcg_spmv_rows<V, FIRST, ZH>(a, it, flags, rb, b);
+}
 
 // Measured and not kept (round 2, profiles/r02_ab/spmvns_*): two systems
 // per thread sharing each slot's column index and mirror entry -- the main
@@ -613,10 +634,10 @@ void launch_spmv(const PcgArgs<V> &a, bool first, dim3, hipStream_t s, int32_t i
 constexpr int kUpdRB = 4;  // row blocks per update workgroup
 inline unsigned upd_blocks(int32_t nblk) { return (unsigned)((nblk + kUpdRB - 1) / kUpdRB); }
 
+// g: the group of kUpdRB row blocks
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
+__device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it, int32_t g, int32_t b) {
     __shared__ double lds[(kWG / 64) * 2 * kUpdRB];
-    const int32_t b = blockIdx.y;
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
@@ -641,7 +662,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     else if (a.stall > 0 && it - si[SI_BEST_IT] > a.stall)
         why = FW_STALLED;
     if (why) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (g == 0 && threadIdx.x == 0) {
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
             si[SI_FAIL_IT] = it;
@@ -663,7 +684,7 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     V2 qv[R], rv[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-        iv[q] = (blockIdx.x * R + q) * kRowsPerWG + threadIdx.x;
+        iv[q] = (g * R + q) * kRowsPerWG + threadIdx.x;
         const int64_t vi = (int64_t)b * a.N + min(iv[q], a.N - 1);
         qv[q] = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
         rv[q] = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
@@ -708,24 +729,26 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
-            const int32_t rbk = blockIdx.x * R + q;
+            const int32_t rbk = g * R + q;
             if (rbk >= a.nblk) break;
-            double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * red_rec(a.red, a.B, blockIdx.y, rbk);
+            double *o = a.part_rzrr + ((it + 1) & 1) * ps + 2 * red_rec(a.red, a.B, b, rbk);
             o[0] = v[2 * q];
             o[1] = v[2 * q + 1];
         }
     }
 }
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
+    pcg_update_rows<V>(a, it, blockIdx.x, blockIdx.y);
+}
 
 // x64 (+)= x_inner for systems active in the inner solve.
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
-                                                      const V *__restrict__ xin,
-                                                      const int32_t *__restrict__ sysi,
-                                                      double *__restrict__ x64) {
-    const int32_t b = blockIdx.y;
+__device__ __forceinline__ void outer_update_rows(int32_t N, int32_t first, const V *__restrict__ xin,
+                                                  const int32_t *__restrict__ sysi, double *__restrict__ x64,
+                                                  int32_t blk, int32_t b) {
     if (!sysi[b * kSysStride + SI_ACTIVE]) return;
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
+    const int32_t i = blk * kWG + threadIdx.x;
     if (i >= N) return;
     const int64_t vi = (int64_t)b * N + i;
     using V2 = typename VT<V>::V2;
@@ -735,18 +758,20 @@ __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first,
     x.y += (double)d.y;
     *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
 }
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first, const V *__restrict__ xin,
+                                                      const int32_t *__restrict__ sysi, double *__restrict__ x64) {
+    outer_update_rows<V>(N, first, xin, sysi, x64, blockIdx.x, blockIdx.y);
+}
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
 // partial |r|^2 and |f|^2.
-__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
-                                                  const double *__restrict__ rhs,
-                                                  const double *__restrict__ x64,
-                                                  const int32_t *__restrict__ sysi,
-                                                  double *__restrict__ r64,
-                                                  double *__restrict__ part) {
+__device__ __forceinline__ void residual_rows(const OpArgs<double> &op, int32_t B, const RedArgs &rd,
+                                              const double *__restrict__ rhs, const double *__restrict__ x64,
+                                              const int32_t *__restrict__ sysi, double *__restrict__ r64,
+                                              double *__restrict__ part, int32_t rb, int32_t b) {
     __shared__ double lds[8];
-    int32_t rb, b;  // XCD-aware: the systems of a row block share its a2 blocks in L2
-    if (!xcd_map(nblk, B, rb, b, kGrpRes) || !sysi[b * kSysStride + SI_ACTIVE]) return;
+    if (!sysi[b * kSysStride + SI_ACTIVE]) return;
     const int32_t N = op.N;
     const int64_t vb = (int64_t)b * N;
     double rr = 0.0, ff = 0.0;
@@ -771,6 +796,16 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
         o[0] = v[0];
         o[1] = v[1];
     }
+}
+__global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
+                                                  const double *__restrict__ rhs,
+                                                  const double *__restrict__ x64,
+                                                  const int32_t *__restrict__ sysi,
+                                                  double *__restrict__ r64,
+                                                  double *__restrict__ part) {
+    int32_t rb, b;  // XCD-aware: the systems of a row block share its a2 blocks in L2
+    if (!xcd_map(nblk, B, rb, b, kGrpRes)) return;
+    residual_rows(op, B, rd, rhs, x64, sysi, r64, part, rb, b);
 }
 
 // The re-forming residual, NS systems per thread (apply_row_rcn): grid
@@ -837,11 +872,10 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t
 }
 
 // One workgroup per system: relative true residual; retire converged systems.
-__global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, const double *__restrict__ part,
-                                                     double rtol, double *__restrict__ sysd,
-                                                     int32_t *__restrict__ sysi) {
+__device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, const double *__restrict__ part,
+                                                double rtol, double *__restrict__ sysd, int32_t *__restrict__ sysi,
+                                                int32_t b) {
     __shared__ double lds[8];
-    const int32_t b = blockIdx.x;
     int32_t *si = sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) return;
     double v[2];
@@ -859,6 +893,11 @@ __global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, cons
             si[SI_ACTIVE] = 0;
         }
     }
+}
+__global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, const double *__restrict__ part,
+                                                     double rtol, double *__restrict__ sysd,
+                                                     int32_t *__restrict__ sysi) {
+    outer_check_sys(rd, B, part, rtol, sysd, sysi, blockIdx.x);
 }
 
 __global__ void k_sys_reset(int32_t B, int32_t *__restrict__ sysi, double *__restrict__ sysd) {
@@ -1143,6 +1182,118 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     return total;
 }
 
+// ---- the fused small-mesh solve ---------------------------------------------
+// On a small mesh every launch of the eager solve is a few microseconds of
+// work behind a few microseconds of launch and dependency latency: C1 (642
+// vertices, 15 systems) needs ~300 launches per batch and is launch-bound
+// (SURVEY.md §7 hard part 4). k_solve_fused runs the whole fp64 block-Jacobi
+// solve of one system -- every refinement step's inner PCG (init, tolerance,
+// SpMV / p.q / update / r.z iterations, the max_iter check launch), the x64
+// update, the fp64 residual and the outer check -- in one workgroup, calling
+// the eager kernels' bodies for each of its row blocks in turn with a
+// workgroup barrier where the eager path has a launch boundary. Same bodies,
+// same row blocks, same partial records and reduction order: V, the flags and
+// the iteration counts are bit-identical to the eager path
+// (tests/test_gpu_fused.py). One launch and one flag fetch per batch.
+struct FusedArgs {
+    const double *rhs;  // f of every system
+    double *x64, *r64, *part_rr0;
+    double rtol, inner_rtol;
+    int32_t max_iter, max_outer, adaptive;
+};
+
+// flags written by other threads of the workgroup before a barrier: a
+// workgroup-scope load (never the scalar cache)
+__device__ __forceinline__ int32_t ld_flag(const int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ __launch_bounds__(kWG) void k_solve_fused(PcgArgs<double> a, OpArgs<double> op, FusedArgs f) {
+    const int32_t b = blockIdx.x;
+    int32_t *si = a.sysi + b * kSysStride;
+    double *sd = a.sysd + b * kSysStride;
+    if (threadIdx.x == 0) {  // k_sys_reset
+        for (int k = 0; k < kSysStride; ++k) {
+            si[k] = 0;
+            sd[k] = 0.0;
+        }
+        si[SI_ACTIVE] = 1;
+        si[SI_CONV] = -1;
+    }
+    __syncthreads();
+    const int32_t nvb = (a.N + kWG - 1) / kWG;              // k_outer_update's blocks
+    const int32_t nug = (a.nblk + kUpdRB - 1) / kUpdRB;     // k_pcg_update's row-block groups
+    int32_t itsum = 0, itmax = 0, o = 0;
+    for (; o < f.max_outer; ++o) {
+        // pcg<double>: the first step to 0.5 rtol, later ones to inner_rtol
+        const double *rhs = o == 0 ? f.rhs : f.r64;
+        for (int32_t rb = 0; rb < a.nblk; ++rb) pcg_init_rows<double>(a, rhs, rb, b);
+        __syncthreads();
+        pcg_tol_sys<double>(a, o == 0 ? 0.5 * f.rtol : f.inner_rtol, o > 0 && f.adaptive ? f.rtol : 0.0, b);
+        __syncthreads();
+        red_rzrr_sys<double>(a, 0, b);
+        __syncthreads();
+        int32_t it = 0;
+        bool fin = false;
+        for (; it < f.max_iter; ++it) {
+            for (int32_t rb = 0; rb < a.nblk; ++rb) {
+                if (it == 0)
+                    pcg_spmv_rows<double, true>(a, it, 0, rb, b);
+                else
+                    pcg_spmv_rows<double, false>(a, it, 0, rb, b);
+            }
+            __syncthreads();
+            if (ld_flag(si + SI_CONV) >= 0 || !ld_flag(si + SI_ACTIVE)) {
+                fin = true;
+                break;
+            }
+            red_pq_sys<double>(a, it & 1, b);
+            __syncthreads();
+            for (int32_t g = 0; g < nug; ++g) pcg_update_rows<double>(a, it, g, b);
+            __syncthreads();
+            if (!ld_flag(si + SI_ACTIVE)) {  // breakdown / divergence / stagnation
+                fin = true;
+                break;
+            }
+            red_rzrr_sys<double>(a, (it + 1) & 1, b);
+            __syncthreads();
+        }
+        if (!fin) {  // the check launch after max_iter (SI_CONV of a system converged there)
+            for (int32_t rb = 0; rb < a.nblk; ++rb) pcg_spmv_rows<double, false>(a, it, 0, rb, b);
+            __syncthreads();
+        }
+        // this inner solve's iterations, counted as pcg() counts them
+        const int32_t c = ld_flag(si + SI_CONV);
+        const int32_t its = c >= 0 ? c
+                                   : (ld_flag(si + SI_FAILED) && ld_flag(si + SI_FAIL_WHY) != FW_MAXITER
+                                          ? ld_flag(si + SI_FAIL_IT) + 1
+                                          : it);
+        itsum += its;
+        itmax = max(itmax, its);
+        for (int32_t blk = 0; blk < nvb; ++blk) outer_update_rows<double>(a.N, o == 0, a.x, a.sysi, f.x64, blk, b);
+        __syncthreads();
+        for (int32_t rb = 0; rb < a.nblk; ++rb)
+            residual_rows(op, a.B, a.red, f.rhs, f.x64, a.sysi, f.r64, f.part_rr0, rb, b);
+        __syncthreads();
+        outer_check_sys(a.red, a.B, f.part_rr0, f.rtol, a.sysd, a.sysi, b);
+        __syncthreads();
+        if (!ld_flag(si + SI_ACTIVE)) {
+            ++o;
+            break;
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (si[SI_ACTIVE]) {  // k_mark_unconverged
+            si[SI_FAILED] = 1;
+            si[SI_ACTIVE] = 0;
+            si[SI_FAIL_WHY] = FW_MAXITER;
+        }
+        si[SI_ITSUM] = itsum;
+        si[SI_ITMAX] = itmax;
+        sd[SD_OUTER] = (double)o;
+    }
+}
+
 }  // namespace
 
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
@@ -1216,10 +1367,64 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     MOF_HIP(hipStreamSynchronize(m->stream));
 }
 
+// The fused solve covers the fp64 solve of a whole batch from x = 0 with a
+// stored u64 (the fp64 path's residual); auto (sp.fused < 0) on meshes of at
+// most MOF_FUSED_MAX_BLK row blocks (default 16: 4096 vertices), where the
+// eager path is launch-bound.
+bool fused_eligible(const mof_mesh *m, const SolveParams &sp, const uint8_t *only) {
+    if (sp.fused == 0 || only || sp.precision != MOF_PREC_F64 || sp.amg || sp.fail_at_max_iter) return false;
+    if (m->ws.u64_stale || !m->ws.u64.p || m->n_own != m->N) return false;
+    if (sp.fused > 0) return true;
+    static const int max_blk = [] {
+        const char *v = std::getenv("MOF_FUSED_MAX_BLK");
+        return v && *v ? std::atoi(v) : 16;
+    }();
+    return m->ws.nblk <= max_blk;
+}
+
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
                     int32_t *max_iters, SpmvTiming *timing, const uint8_t *only) {
     SpmvTiming *tm = sp.time_spmv ? timing : nullptr;
     Workspace &w = m->ws;
+    if (fused_eligible(m, sp, only)) {
+        // the whole solve in one launch (k_solve_fused), bit-identical to the
+        // eager loop below
+        PcgArgs<double> a = make_args<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p);
+        a.stall = sp.stall;
+        const FusedArgs fa{w.rhs.p, w.x64.p, w.r64.p, w.part_rr0.p, sp.rtol, sp.inner_rtol,
+                           sp.max_iter, sp.max_outer, sp.adaptive_inner ? 1 : 0};
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (tm) {
+            if (m->spmv_events.size() < 2) {
+                const size_t old_n = m->spmv_events.size();
+                m->spmv_events.resize(64);
+                for (size_t q = old_n; q < m->spmv_events.size(); ++q) MOF_HIP(hipEventCreate(&m->spmv_events[q]));
+            }
+            e0 = m->spmv_events[0];
+            e1 = m->spmv_events[1];
+            hipExtLaunchKernelGGL(k_solve_fused, dim3((unsigned)B), dim3(kWG), 0, s, e0, e1, 0, a, op64(m), fa);
+        } else {
+            k_solve_fused<<<dim3((unsigned)B), kWG, 0, s>>>(a, op64(m), fa);
+        }
+        MOF_HIP(hipGetLastError());
+        fetch_flags(m, B, s);
+        int64_t iters = 0;
+        int32_t o = 0;
+        for (int32_t b = 0; b < B; ++b) {
+            const int32_t *si = m->h_sysi + b * kSysStride;
+            iters += si[SI_ITSUM];
+            *max_iters = std::max(*max_iters, si[SI_ITMAX]);
+            o = std::max(o, (int32_t)m->h_sysd[b * kSysStride + SD_OUTER]);
+        }
+        *outer = o;
+        if (tm) {
+            float ms = 0.f;
+            MOF_HIP(hipEventElapsedTime(&ms, e0, e1));
+            tm->fused_launches++;
+            tm->ms_fused += ms;
+        }
+        return iters;
+    }
     if (!only) {
         k_sys_reset<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p, w.sysd.p);
         MOF_HIP(hipGetLastError());

@@ -20,7 +20,7 @@ CSRC_DIR = os.path.join(ROOT_DIR, "csrc")
 LIB_PATH = os.environ.get("MOFHIP_LIB") or os.path.join(PKG_DIR, "libmofhip.so")
 
 # include/mof.h MOF_ABI_VERSION this binding's structs follow
-MOF_ABI_VERSION = 2
+MOF_ABI_VERSION = 3
 
 MOF_OK = 0
 MOF_E_ARG = -1
@@ -37,6 +37,8 @@ MOF_NO_BLOCK_JACOBI = 2
 MOF_TIME_SPMV = 4
 MOF_PRECOND_AMG = 8
 MOF_NO_RECOVERY = 16
+MOF_SOLVE_FUSED = 128
+MOF_SOLVE_EAGER = 256
 MOF_CSV_ROUND_TRIP = 1
 MOF_COORDS_F32 = 32
 MOF_DD_STAGED = 64
@@ -87,7 +89,8 @@ class MofStats(ctypes.Structure):
         ("ms_spmv", ctypes.c_double), ("spmv_bytes", ctypes.c_double),
         ("spmv_systems", ctypes.c_int64), ("spmv_full_launches", ctypes.c_int64),
         ("ms_spmv_full", ctypes.c_double), ("recovered", ctypes.c_int32),
-        ("recovered_f64", ctypes.c_int32),
+        ("recovered_f64", ctypes.c_int32), ("fused_launches", ctypes.c_int64),
+        ("ms_fused", ctypes.c_double),
     ]
 
     def as_dict(self):

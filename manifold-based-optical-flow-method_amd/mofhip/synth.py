@@ -26,6 +26,7 @@ __all__ = [
     "vertex_normals",
     "triangle_areas",
     "travelling_wave",
+    "electrode_surface",
     "mesh_for_config",
     "CONFIG_FREQ",
 ]
@@ -167,6 +168,145 @@ def spherical_cap(n: int = 16, radius: float = 10.0, zcut: float = 0.5):
     return p[used].copy(), remap[t].astype(np.int32)
 
 
+def _edges_with_opposites(tri):
+    """{(a, b) a < b: [opposite vertices]} in first-seen order."""
+    opp = {}
+    for a, b, c in tri.tolist():
+        for u, v, w in ((a, b, c), (b, c, a), (c, a, b)):
+            opp.setdefault((u, v) if u < v else (v, u), []).append(w)
+    return opp
+
+
+def _laplacian_smooth(p, tri, n_iter=100, relax=0.01):
+    """vtkSmoothPolyDataFilter-like (pyvista ``smooth``): n_iter Laplacian
+    steps p += relax (mean of neighbours - p); boundary vertices move along
+    the boundary (their boundary-edge neighbours only)."""
+    opp = _edges_with_opposites(tri)
+    nbr = [[] for _ in range(len(p))]
+    bnb = [[] for _ in range(len(p))]
+    for (a, b), o in opp.items():
+        nbr[a].append(b)
+        nbr[b].append(a)
+        if len(o) == 1:
+            bnb[a].append(b)
+            bnb[b].append(a)
+    src, dst = [], []
+    for i in range(len(p)):
+        ns = bnb[i] if bnb[i] else nbr[i]
+        src.extend(ns)
+        dst.extend([i] * len(ns))
+    src, dst = np.asarray(src), np.asarray(dst)
+    cnt = np.bincount(dst, minlength=len(p)).astype(np.float64)[:, None]
+    p = p.copy()
+    for _ in range(n_iter):
+        acc = np.zeros_like(p)
+        np.add.at(acc, dst, p[src])
+        p += relax * (acc / cnt - p)
+    return p
+
+
+def _butterfly(p, tri):
+    """One butterfly subdivision step (vtkButterflySubdivisionFilter-like):
+    every triangle splits in four; an interior edge (a, b) with opposite
+    vertices c, d gets 1/2 (a + b) + 1/8 (c + d) - 1/16 (the four wing
+    vertices opposite the edges a-c, b-c, a-d, b-d), a boundary edge the
+    four-point rule 9/16 (a + b) - 1/16 (its boundary neighbours); a missing
+    wing falls back to the edge's far corner. New vertices follow the old
+    ones in edge order."""
+    opp = _edges_with_opposites(tri)
+    bnext = {}
+    for (a, b), o in opp.items():
+        if len(o) == 1:
+            bnext.setdefault(a, []).append(b)
+            bnext.setdefault(b, []).append(a)
+
+    def wing(u, v, notw):
+        o = opp[(u, v) if u < v else (v, u)]
+        for w in o:
+            if w != notw:
+                return w
+        return None
+
+    eid = {}
+    new = []
+    N = len(p)
+    for (a, b), o in opp.items():
+        if len(o) == 2:
+            c, d = o
+            q = 0.5 * (p[a] + p[b]) + 0.125 * (p[c] + p[d])
+            for u, v, far in ((a, c, b), (b, c, a), (a, d, b), (b, d, a)):
+                w = wing(u, v, far)
+                q -= 0.0625 * p[w if w is not None else far]
+        else:
+            pa = [x for x in bnext.get(a, []) if x != b]
+            pb = [x for x in bnext.get(b, []) if x != a]
+            qa = p[pa[0]] if pa else p[a]
+            qb = p[pb[0]] if pb else p[b]
+            q = 0.5625 * (p[a] + p[b]) - 0.0625 * (qa + qb)
+        eid[(a, b)] = N + len(new)
+        new.append(q)
+    e = lambda u, v: eid[(u, v) if u < v else (v, u)]  # noqa: E731
+    out = []
+    for a, b, c in tri.tolist():
+        ab, bc, ca = e(a, b), e(b, c), e(c, a)
+        out += [(a, ab, ca), (ab, b, bc), (ca, bc, c), (ab, bc, ca)]
+    return np.vstack([p, np.asarray(new)]), np.asarray(out, dtype=np.int64)
+
+
+def electrode_surface(n_side: int, spacing: float = 10.0, jitter: float = 0.15, radius: float = 70.0,
+                      subdivisions: int = 3, seed: int = 0):
+    """S1-like reconstructed cortical patch (S1_reconstruct_surface.py:82-97):
+    an ``n_side`` x ``n_side`` ECoG electrode grid (``spacing`` mm, positions
+    jittered by ``jitter`` x spacing) lying on a sphere of ``radius`` mm (the
+    cortex's curvature), a 2-D Delaunay triangulation of it (pyvista
+    ``delaunay_2d``), 100 Laplacian smoothing steps, ``subdivisions``
+    butterfly subdivision steps, and 100 more smoothing steps. An open,
+    mostly valence-6 surface whose original grid vertices keep the
+    Delaunay valences (4-8). Returns (points (V,3) f64, triangles (M,3) int32)
+    with consistently oriented triangles (normals towards +z)."""
+    from scipy.spatial import Delaunay
+    rng = np.random.default_rng(seed)
+    g = (np.arange(n_side) - 0.5 * (n_side - 1)) * spacing
+    x, y = np.meshgrid(g, g, indexing="ij")
+    xy = np.stack([x.ravel(), y.ravel()], axis=1)
+    xy += jitter * spacing * rng.uniform(-1.0, 1.0, size=xy.shape)
+    z = np.sqrt(np.maximum(radius ** 2 - (xy ** 2).sum(axis=1), 0.0)) - radius
+    p = np.column_stack([xy, z])
+    tri = Delaunay(xy).simplices.astype(np.int64)
+    # the hull of a jittered grid closes with slivers over nearly collinear
+    # boundary electrodes, which the smoothing folds over: peel boundary
+    # triangles with an angle under 20 degrees
+    while True:
+        opp = _edges_with_opposites(tri)
+        bd = {e for e, o in opp.items() if len(o) == 1}
+        e0 = xy[tri[:, 1]] - xy[tri[:, 0]]
+        e1 = xy[tri[:, 2]] - xy[tri[:, 1]]
+        e2 = xy[tri[:, 0]] - xy[tri[:, 2]]
+
+        def angle(u, v):
+            return np.degrees(np.arccos(np.clip(-(u * v).sum(1) / np.linalg.norm(u, axis=1)
+                                                / np.linalg.norm(v, axis=1), -1.0, 1.0)))
+        amin = np.minimum(np.minimum(angle(e2, e0), angle(e0, e1)), angle(e1, e2))
+        onb = np.array([any(((min(u, v), max(u, v)) in bd) for u, v in ((a, b), (b, c), (c, a)))
+                        for a, b, c in tri.tolist()])
+        drop = onb & (amin < 20.0)
+        if not drop.any():
+            break
+        tri = tri[~drop]
+    used = np.unique(tri)
+    remap = -np.ones(len(p), dtype=np.int64)
+    remap[used] = np.arange(len(used))
+    p, tri = p[used], remap[tri]
+    c = np.cross(p[tri[:, 1]] - p[tri[:, 0]], p[tri[:, 2]] - p[tri[:, 0]])
+    flip = c[:, 2] < 0
+    tri[flip] = tri[flip][:, [0, 2, 1]]
+    p = _laplacian_smooth(p, tri)
+    for _ in range(subdivisions):
+        p, tri = _butterfly(p, tri)
+    p = _laplacian_smooth(p, tri)
+    return p, tri.astype(np.int32)
+
+
 def vertex_normals(points: np.ndarray, triangles: np.ndarray) -> np.ndarray:
     """VTK-like point normals: normalised sum of the unit normals of the
     incident faces."""
@@ -204,6 +344,12 @@ def mesh_for_config(name: str):
     with randomly relabelled vertices (locality stress cases)."""
     if name == "R3":
         p, t = random_sphere(163842, 10.0, seed=0)
+        return p, t, vertex_normals(p, t), triangle_areas(p, t)
+    if name in ("S1", "S1s"):
+        # S1-like surfaces (electrode_surface): S1 = a 51 x 51 grid (160,801
+        # vertices, the 160k class), S1s = an 8 x 8 grid (3,249 vertices, the
+        # size of the reference's real surfaces, find_singularity_point.py:19-20)
+        p, t = electrode_surface(51 if name == "S1" else 8)
         return p, t, vertex_normals(p, t), triangle_areas(p, t)
     if name == "P3":
         p, t, _, _ = mesh_for_config("C3")
