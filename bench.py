@@ -79,6 +79,9 @@ def parse():
                     help="fraction of the triangle loop the CPU baseline times")
     ap.add_argument("--cpu-timesteps-per-core", type=int, default=2,
                     help="CPU baseline: timesteps per pool process (SURVEY.md 8(d): 2 per core)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="CPU baseline pool size (0: the box's CPU share per GPU, 16; BASELINE.md names "
+                         "os.cpu_count(), which a larger pool approaches)")
     ap.add_argument("--lambda_", type=float, default=0.01)
     ap.add_argument("--fixed-timesteps", type=int, default=0,
                     help="strong scaling: one step = this many timesteps split over the ranks")
@@ -88,6 +91,9 @@ def parse():
                     help="timesteps of the last timed batch checked against the oracle + spsolve (0: none)")
     ap.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
                     help="fp64: the one-launch fused solve per batch (auto: the library's choice, small meshes)")
+    ap.add_argument("--lanes", type=int, default=1, choices=[1, 2],
+                    help="2: two batches in flight per GPU (MOF_TWO_LANES); the timed region is then one library "
+                         "call over all timed batches")
     ap.add_argument("--host-batches", type=int, default=4,
                     help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
                          "the device-resident region (0: none)")
@@ -178,7 +184,7 @@ def parity_check(geom, t, a, lam, samples):
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
-def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0):
+def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0, cores=0):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
     host on a bounded sample: Pool(C) runs per_core * C timesteps (SURVEY.md
     §8(d): 2 C); each assembles the first `frac` of the triangles with the
@@ -188,7 +194,7 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0)
     is extrapolated linearly in the triangle count."""
     import oracle
     import reference_clone as clone
-    C = clone.default_cores()
+    C = int(cores) if cores and cores > 0 else clone.default_cores()
     K = per_core * C
     if full_timesteps:  # SURVEY.md 8(d): C1 is timed in full (every timestep, the whole triangle loop)
         K, frac = full_timesteps, 1.0
@@ -210,7 +216,9 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0)
     return {
         "value": value, "unit": "timesteps/s", "cores": C, "kind": "port",
         "host_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
-        "cores_reason": "the GPU box's CPU share is 16 cores per GPU (OMP_NUM_THREADS=16 there); "
+        "cores_reason": ("--cpu-cores %d: a pool larger than the box's 16-core share per GPU, to measure "
+                         "the baseline's scaling towards os.cpu_count()" % C) if cores and cores > 0 else
+                        "the GPU box's CPU share is 16 cores per GPU (OMP_NUM_THREADS=16 there); "
                         "os.cpu_count() reports the whole machine",
         "sample": ("Pool(%d) x %d timesteps of the reference algorithm (lil scalar assembly, csr, "
                    "spsolve; oracle/reference_clone.py, calibrated vs the reference) on the %d-vertex "
@@ -296,12 +304,16 @@ def main():
         del I_dev
         I_dev = None
     else:
-        V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
+        # two lanes: one call over all timed batches writes all of their V
+        v_rows = B
+        if args.lanes > 1:
+            v_rows = K_rank if strong else B * max(args.steps, args.warmup)
+        V_dev = torch.empty((v_rows, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(K_rank + 1, dtype=np.float64)
     sync()
     precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
     opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol,
-                fused={"auto": None, "on": True, "off": False}[args.fused])
+                fused={"auto": None, "on": True, "off": False}[args.fused], lanes=args.lanes)
 
     kept = []  # host V of the timed calls, freed after the clock stops (the caller keeps its result)
 
@@ -329,7 +341,7 @@ def main():
         opts["batch"] = B_eff
         batches = [(a, min(a + B_eff, K_rank)) for a in range(0, K_rank, B_eff)]
         warm = batches[:max(1, args.warmup)] if batches else []
-        if host_io:
+        if host_io or args.lanes > 1:
             step_calls = [(0, K_rank)]
         else:
             step_calls = batches
@@ -337,8 +349,9 @@ def main():
     else:
         warm = [(s * B, (s + 1) * B) for s in range(args.warmup)]
         timed = [(s * B, (s + 1) * B) for s in range(args.warmup, args.warmup + args.steps)]
-        timed_calls = [(timed[0][0], timed[-1][1])] if host_io else timed
-        if host_io and warm:
+        one_call = host_io or args.lanes > 1
+        timed_calls = [(timed[0][0], timed[-1][1])] if one_call else timed
+        if one_call and warm:
             warm = [(warm[0][0], warm[-1][1])]
     for a_, b_ in warm:
         solve(a_, b_, False)
@@ -465,7 +478,8 @@ def main():
     parity = parity_check(geom, t, a, args.lambda_, samples) if samples else None
     if rank == 0 and not args.no_cpu_baseline and not dry:
         cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom,
-                           full_timesteps=args.fixed_timesteps if args.config in SMALL_JOBS else 0)
+                           full_timesteps=args.fixed_timesteps if args.config in SMALL_JOBS else 0,
+                           cores=args.cpu_cores)
 
     if rank == 0:
         line = {

@@ -96,6 +96,12 @@ extern "C" {
                                   (MOF_FUSED_MAX_BLK), where the eager
                                   launches are latency-bound */
 #define MOF_SOLVE_EAGER 256u   /* never the fused solve */
+#define MOF_TWO_LANES 512u     /* two batches in flight: batches alternate
+                                  between the handle and a twin handle on the
+                                  same device (own stream and workspace,
+                                  created on first use), each driven by its
+                                  own host thread; V is bit-identical to one
+                                  lane. Ignored with a caller stream */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */

@@ -126,6 +126,145 @@ void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
     }
 }
 
+// One lane of mof_solve_range: batches j = lane, lane + lanes, ... of the
+// call's range [k0, k1) (batch j = timesteps k0 + j B ...), each assembled,
+// solved, recovered and written as planar V on the lane's handle and stream.
+// Host pointers: the lane's own double-buffered copy pipeline (mof_hostio.h).
+void solve_lane(mof_mesh *m, const double *I, const double *I2, const double *t_k, int32_t k0, int32_t k1,
+                int32_t B, int lane, int lanes, double lambda, const mof::SolveParams &sp, const mof_opts &o,
+                bool recovery, bool dev_io, hipStream_t s, double *V_out, mof_stats &st, mof::SpmvTiming &timing) {
+    const int32_t K = k1 - k0;
+    const int32_t nbat_all = (K + B - 1) / B;
+    std::vector<int32_t> js;  // this lane's batches
+    for (int32_t j = lane; j < nbat_all; j += lanes) js.push_back(j);
+    const int32_t nbat = (int32_t)js.size();
+    if (!nbat) return;
+    mof::ensure_workspace(m, B, sp.precision);
+    mof::Workspace &w = m->ws;
+    const int64_t N = m->N;
+    Events ev;
+    mof::prepare_operator(m, lambda, s);
+    // multigrid hierarchy before the first assembly (which writes the
+    // level-0 smoother's bf16 copies)
+    const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && mof::amg_build(m);
+    if (amg) mof::amg_ensure(m, B);
+    // host pointers: one upload of the nb+1 rows when I2 is I (S3
+    // passes I_k twice), else nb rows of each
+    const bool shared_I = (I2 == I);
+    const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
+    if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B);
+    auto bk = [&](int32_t q) { return k0 + js[q] * B; };
+    auto bn = [&](int32_t q) { return std::min(B, k1 - bk(q)); };
+    // helper-thread steps of the host pipeline (copy stream): the lane's q-th
+    // batch's I rows into slot q&1 once batch q-2's assembly has read it, and
+    // batch q's V out of slot q&1 into V_out
+    // MOF_HOSTIO_VERBOSE: helper-thread and wait times on stderr
+    const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
+    double t_in = 0.0, t_out = 0.0, t_wait = 0.0;
+    const double t_call = now_ms();
+    mof::g_fetch_ms = 0.0;
+    mof::g_fetch_n = 0;
+    auto stage_in = [&](int32_t q) {
+        const double t0 = now_ms();
+        struct Acc {
+            double &t, t0;
+            ~Acc() { t += now_ms() - t0; }
+        } acc{t_in, t0};
+        MOF_HIP(hipSetDevice(m->device));
+        const int32_t sl = q & 1, kj = bk(q), nb = bn(q);
+        hipStream_t cs = m->stage->stream();
+        MOF_HIP(hipStreamWaitEvent(cs, m->hev[2 + sl], 0));
+        if (shared_I) {
+            m->stage->h2d(m->hin[sl].p, I + (int64_t)kj * N, sizeof(double) * N * (nb + 1));
+        } else {
+            m->stage->h2d(m->hin[sl].p, I + (int64_t)kj * N, sizeof(double) * N * nb);
+            m->stage->h2d(m->hin[sl].p + N * B, I2 + (int64_t)(kj + 1) * N, sizeof(double) * N * nb);
+        }
+        MOF_HIP(hipEventRecord(m->hev[sl], cs));
+    };
+    auto drain_out = [&](int32_t q) {
+        struct Acc {
+            double &t, t0;
+            ~Acc() { t += now_ms() - t0; }
+        } acc{t_out, now_ms()};
+        MOF_HIP(hipSetDevice(m->device));
+        const int32_t sl = q & 1;
+        m->stage->d2h(V_out + (int64_t)(bk(q) - k0) * 2 * N, m->hout[sl].p, sizeof(double) * 2 * N * bn(q),
+                      m->hev[4 + sl]);
+    };
+    std::vector<double> dts(B);
+    std::vector<uint8_t> only(B);
+    // declared after everything its tasks reference: its destructor
+    // waits for a task still running when an error unwinds
+    std::future<void> io;
+    if (!dev_io) io = std::async(std::launch::async, [&] { stage_in(0); });
+    for (int32_t q = 0; q < nbat; ++q) {
+        const int32_t k = bk(q), nb = bn(q), sl = q & 1;
+        for (int32_t b = 0; b < nb; ++b) dts[b] = t_k[k + b + 1] - t_k[k + b];
+        MOF_HIP(hipMemcpyAsync(w.dt.p, dts.data(), sizeof(double) * nb, hipMemcpyHostToDevice, s));
+        const double *I0p, *I1p;
+        if (dev_io) {
+            I0p = I + (int64_t)k * N;
+            I1p = I2 + (int64_t)(k + 1) * N;
+        } else {
+            const double tw = now_ms();
+            io.get();  // batch q staged, batch q-1 drained
+            t_wait += now_ms() - tw;
+            if (q + 1 < nbat || q > 0)
+                io = std::async(std::launch::async, [&, q] {
+                    if (q + 1 < nbat) stage_in(q + 1);
+                    if (q > 0) drain_out(q - 1);
+                });
+            MOF_HIP(hipStreamWaitEvent(s, m->hev[sl], 0));
+            I0p = m->hin[sl].p;
+            I1p = shared_I ? I0p + N : I0p + N * B;
+        }
+        MOF_HIP(hipEventRecord(ev.e[0], s));
+        mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s, amg);
+        if (!dev_io) MOF_HIP(hipEventRecord(m->hev[2 + sl], s));
+        MOF_HIP(hipEventRecord(ev.e[1], s));
+        int32_t outer = 0;
+        st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
+        st.outer_steps = outer;
+        if (recovery)
+            mof::recover_systems(
+                nb, sp, o.max_iter, m->h_sysi, only, st,
+                [&](uint32_t prec) {
+                    mof::ensure_workspace(m, nb, prec);
+                    mof::launch_recovery_operator(m, nb, prec, s);
+                },
+                [&](const mof::SolveParams &rp, const uint8_t *on) {
+                    int32_t outer_r = 0;
+                    return mof::solve_batch(m, nb, rp, s, &outer_r, &st.max_iterations, nullptr, on);
+                },
+                [&] { mof::release_f64_terms(m); });
+        double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[sl].p;
+        mof::launch_to_planar(m, nb, Vdst, s);
+        if (!dev_io) MOF_HIP(hipEventRecord(m->hev[4 + sl], s));
+        MOF_HIP(hipEventRecord(ev.e[2], s));
+        MOF_HIP(hipEventSynchronize(ev.e[2]));
+        st.ms_assembly += ev.ms(0, 1);
+        st.ms_solve += ev.ms(1, 2);
+        for (int32_t b = 0; b < nb; ++b) {
+            if (m->h_sysi[b * mof::kSysStride + mof::SI_FAILED]) st.failed++;
+            st.max_rel_residual = std::max(st.max_rel_residual, m->h_sysd[b * mof::kSysStride + mof::SD_REL]);
+        }
+        st.batches++;
+    }
+    if (dev_io && hostio_verbose)
+        fprintf(stderr, "[mof hostio] lane %d device K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n", lane, K,
+                B, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
+    if (!dev_io) {
+        if (io.valid()) io.get();
+        drain_out(nbat - 1);
+        if (hostio_verbose)
+            fprintf(stderr,
+                    "[mof hostio] lane %d K=%d B=%d: stage_in %.1f ms, drain %.1f ms, main waited %.1f ms, "
+                    "call %.1f ms, %lld flag fetches %.1f ms\n",
+                    lane, K, B, t_in, t_out, t_wait, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
+    }
+}
+
 }  // namespace
 
 namespace mof {
@@ -471,6 +610,10 @@ int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out) {
 int mof_mesh_destroy(mof_mesh *m) {
     if (!m) return MOF_OK;
     return guarded([&] {
+        if (m->twin) {
+            mof_mesh_destroy(m->twin);
+            m->twin = nullptr;
+        }
         {
             DeviceGuard dg(m->device);
             if (m->stream) (void)hipStreamSynchronize(m->stream);
@@ -604,7 +747,6 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         // the multigrid smoother is the 2x2 block Jacobi
         sp.block_jacobi = sp.amg || !(o.flags & MOF_NO_BLOCK_JACOBI);
         sp.time_spmv = (o.flags & MOF_TIME_SPMV) != 0;
-        mof::SpmvTiming timing;
         sp.max_iter = o.max_iter > 0 ? o.max_iter : (sp.amg ? 1000 : 10000);
         sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
         sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
@@ -619,9 +761,9 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;
         if (!I2) I2 = I;
         DeviceGuard dg(m->device);
-        hipStream_t s = o.stream ? (hipStream_t)o.stream : m->stream;
         const int32_t K = k1 - k0;
         mof_stats st{};
+        mof::SpmvTiming timing;
         if (K > 0) {
             int32_t Bmax = o.batch;
             if (Bmax <= 0) {
@@ -635,131 +777,66 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 Bmax = (int32_t)std::max(1.0, std::min(512.0, 0.25 * (double)free_b / per_sys));
             }
             const int32_t B = std::min(K, Bmax);
-            mof::ensure_workspace(m, B, sp.precision);
-            mof::Workspace &w = m->ws;
-            const int64_t N = m->N;
-            Events ev;
-            mof::prepare_operator(m, lambda, s);
-            // multigrid hierarchy before the first assembly (which writes the
-            // level-0 smoother's bf16 copies)
-            const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && mof::amg_build(m);
-            if (amg) mof::amg_ensure(m, B);
-            // host pointers: one upload of the nb+1 rows when I2 is I (S3
-            // passes I_k twice), else nb rows of each
-            const bool shared_I = (I2 == I);
-            const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
-            if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B);
             const int32_t nbat = (K + B - 1) / B;
-            auto bk = [&](int32_t j) { return k0 + j * B; };
-            auto bn = [&](int32_t j) { return std::min(B, k1 - bk(j)); };
-            // helper-thread steps of the host pipeline (copy stream): batch j's
-            // I rows into slot j&1 once batch j-2's assembly has read it, and
-            // batch j's V out of slot j&1 into V_out
-            // MOF_HOSTIO_VERBOSE: helper-thread and wait times on stderr
-            const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
-            double t_in = 0.0, t_out = 0.0, t_wait = 0.0;
-            const double t_call = now_ms();
-            mof::g_fetch_ms = 0.0;
-            mof::g_fetch_n = 0;
-            auto stage_in = [&](int32_t j) {
-                const double t0 = now_ms();
-                struct Acc {
-                    double &t, t0;
-                    ~Acc() { t += now_ms() - t0; }
-                } acc{t_in, t0};
-                MOF_HIP(hipSetDevice(m->device));
-                const int32_t sl = j & 1, kj = bk(j), nb = bn(j);
-                hipStream_t cs = m->stage->stream();
-                MOF_HIP(hipStreamWaitEvent(cs, m->hev[2 + sl], 0));
-                if (shared_I) {
-                    m->stage->h2d(m->hin[sl].p, I + (int64_t)kj * N, sizeof(double) * N * (nb + 1));
-                } else {
-                    m->stage->h2d(m->hin[sl].p, I + (int64_t)kj * N, sizeof(double) * N * nb);
-                    m->stage->h2d(m->hin[sl].p + N * B, I2 + (int64_t)(kj + 1) * N, sizeof(double) * N * nb);
-                }
-                MOF_HIP(hipEventRecord(m->hev[sl], cs));
-            };
-            auto drain_out = [&](int32_t j) {
-                struct Acc {
-                    double &t, t0;
-                    ~Acc() { t += now_ms() - t0; }
-                } acc{t_out, now_ms()};
-                MOF_HIP(hipSetDevice(m->device));
-                const int32_t sl = j & 1;
-                m->stage->d2h(V_out + (int64_t)(bk(j) - k0) * 2 * N, m->hout[sl].p, sizeof(double) * 2 * N * bn(j),
-                              m->hev[4 + sl]);
-            };
-            std::vector<double> dts(B);
-            std::vector<uint8_t> only(B);
-            // declared after everything its tasks reference: its destructor
-            // waits for a task still running when an error unwinds
-            std::future<void> io;
-            if (!dev_io) io = std::async(std::launch::async, [&] { stage_in(0); });
-            for (int32_t j = 0; j < nbat; ++j) {
-                const int32_t k = bk(j), nb = bn(j), sl = j & 1;
-                for (int32_t b = 0; b < nb; ++b) dts[b] = t_k[k + b + 1] - t_k[k + b];
-                MOF_HIP(hipMemcpyAsync(w.dt.p, dts.data(), sizeof(double) * nb, hipMemcpyHostToDevice, s));
-                const double *I0p, *I1p;
-                if (dev_io) {
-                    I0p = I + (int64_t)k * N;
-                    I1p = I2 + (int64_t)(k + 1) * N;
-                } else {
-                    const double tw = now_ms();
-                    io.get();  // batch j staged, batch j-1 drained
-                    t_wait += now_ms() - tw;
-                    if (j + 1 < nbat || j > 0)
-                        io = std::async(std::launch::async, [&, j] {
-                            if (j + 1 < nbat) stage_in(j + 1);
-                            if (j > 0) drain_out(j - 1);
-                        });
-                    MOF_HIP(hipStreamWaitEvent(s, m->hev[sl], 0));
-                    I0p = m->hin[sl].p;
-                    I1p = shared_I ? I0p + N : I0p + N * B;
-                }
-                MOF_HIP(hipEventRecord(ev.e[0], s));
-                mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s, amg);
-                if (!dev_io) MOF_HIP(hipEventRecord(m->hev[2 + sl], s));
-                MOF_HIP(hipEventRecord(ev.e[1], s));
-                int32_t outer = 0;
-                st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
-                st.outer_steps = outer;
-                if (recovery)
-                    mof::recover_systems(
-                        nb, sp, o.max_iter, m->h_sysi, only, st,
-                        [&](uint32_t prec) {
-                            mof::ensure_workspace(m, nb, prec);
-                            mof::launch_recovery_operator(m, nb, prec, s);
-                        },
-                        [&](const mof::SolveParams &rp, const uint8_t *on) {
-                            int32_t outer_r = 0;
-                            return mof::solve_batch(m, nb, rp, s, &outer_r, &st.max_iterations, nullptr, on);
-                        },
-                        [&] { mof::release_f64_terms(m); });
-                double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[sl].p;
-                mof::launch_to_planar(m, nb, Vdst, s);
-                if (!dev_io) MOF_HIP(hipEventRecord(m->hev[4 + sl], s));
-                MOF_HIP(hipEventRecord(ev.e[2], s));
-                MOF_HIP(hipEventSynchronize(ev.e[2]));
-                st.ms_assembly += ev.ms(0, 1);
-                st.ms_solve += ev.ms(1, 2);
-                for (int32_t b = 0; b < nb; ++b) {
-                    if (m->h_sysi[b * mof::kSysStride + mof::SI_FAILED]) st.failed++;
-                    st.max_rel_residual =
-                        std::max(st.max_rel_residual, m->h_sysd[b * mof::kSysStride + mof::SD_REL]);
-                }
-                st.batches++;
+            // two lanes: batches alternate between this handle and its twin
+            // (a clone on the same device: own stream, own workspace), each
+            // driven by its own host thread, so one batch's latency-bound
+            // setup kernels (assembly, fp64 residuals, Galerkin products) run
+            // beside the other's bandwidth-bound iterations. Batch
+            // composition is unchanged, so V is bit-identical to one lane.
+            // Not with a caller stream (the lanes' streams are the handles').
+            const int lanes = ((o.flags & MOF_TWO_LANES) && !o.stream && nbat >= 2) ? 2 : 1;
+            if (lanes == 2 && !m->twin) {
+                mof_mesh *t = nullptr;
+                const int rc2 = mof_mesh_clone(m, m->device, &t);
+                if (rc2 != MOF_OK) throw mof::Error{rc2, "second lane: " + g_err};
+                m->twin = t;
             }
-            if (dev_io && hostio_verbose)
-                fprintf(stderr, "[mof hostio] device K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n", K, B,
-                        now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
-            if (!dev_io) {
-                if (io.valid()) io.get();
-                drain_out(nbat - 1);
-                if (hostio_verbose)
-                    fprintf(stderr,
-                            "[mof hostio] K=%d B=%d: stage_in %.1f ms, drain %.1f ms, main waited %.1f ms, "
-                            "call %.1f ms, %lld flag fetches %.1f ms\n",
-                            K, B, t_in, t_out, t_wait, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
+            mof::SolveParams sp_l = sp;
+            std::vector<mof_stats> lst(lanes);
+            std::vector<mof::SpmvTiming> ltm(lanes);
+            std::vector<std::string> lerr(lanes);
+            std::vector<int> lrc(lanes, MOF_OK);
+            auto lane = [&](int l) {
+                lrc[l] = guarded([&] {
+                    mof_mesh *L = l == 0 ? m : m->twin;
+                    MOF_HIP(hipSetDevice(L->device));
+                    hipStream_t ls = (l == 0 && o.stream) ? (hipStream_t)o.stream : L->stream;
+                    solve_lane(L, I, I2, t_k, k0, k1, B, l, lanes, lambda, sp_l, o, recovery, dev_io, ls, V_out,
+                               lst[l], ltm[l]);
+                });
+                if (lrc[l] != MOF_OK) lerr[l] = g_err;
+            };
+            if (lanes == 1) {
+                lane(0);
+            } else {
+                auto f1 = std::async(std::launch::async, [&] { lane(1); });
+                lane(0);
+                f1.get();
+            }
+            for (int l = 0; l < lanes; ++l)
+                if (lrc[l] != MOF_OK) throw mof::Error{lrc[l], lerr[l]};
+            for (int l = 0; l < lanes; ++l) {
+                const mof_stats &a = lst[l];
+                st.iterations += a.iterations;
+                st.max_iterations = std::max(st.max_iterations, a.max_iterations);
+                st.failed += a.failed;
+                st.outer_steps = std::max(st.outer_steps, a.outer_steps);
+                st.batches += a.batches;
+                st.max_rel_residual = std::max(st.max_rel_residual, a.max_rel_residual);
+                st.ms_assembly += a.ms_assembly;
+                st.ms_solve += a.ms_solve;
+                st.recovered += a.recovered;
+                st.recovered_f64 += a.recovered_f64;
+                const mof::SpmvTiming &t = ltm[l];
+                timing.launches += t.launches;
+                timing.systems += t.systems;
+                timing.full_launches += t.full_launches;
+                timing.ms += t.ms;
+                timing.bytes += t.bytes;
+                timing.ms_full += t.ms_full;
+                timing.fused_launches += t.fused_launches;
+                timing.ms_fused += t.ms_fused;
             }
         }
         st.systems = K;

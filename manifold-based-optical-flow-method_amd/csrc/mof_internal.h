@@ -260,6 +260,10 @@ struct mof_mesh {
     // host state shared with the clones of this mesh on other devices
     std::shared_ptr<mof::MeshShared> shared;
     hipEvent_t hev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // the second lane of a two-lane solve (mof_solve_range, MOF_TWO_LANES): a
+    // clone of this mesh on the same device with its own stream and
+    // workspace, created on first use, destroyed with this handle
+    mof_mesh *twin = nullptr;
 };
 
 namespace mof {
