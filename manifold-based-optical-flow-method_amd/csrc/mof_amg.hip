@@ -477,6 +477,102 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ns(
     }
 }
 
+// Levels >= 1 by gather entry (k_galerkin0_ent's scheme for the fp32 3x3
+// blocks): one entry of kGalENS systems per thread, its terms staged in LDS,
+// one thread per (coarse position, system) summing them in list order -- the
+// same bits as k_galerkin3_ns.
+__global__ __launch_bounds__(kWG) void k_galerkin3_ent(
+    int32_t ngrp, const int32_t *__restrict__ ggrp, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ gent, const float *__restrict__ Q, const float *__restrict__ Af, int64_t f_sell_nb,
+    int64_t c_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh, uint16_t *__restrict__ Dh22,
+    uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
+#pragma clang fp contract(off)
+    __shared__ float con[kGalENS][9][kWG];
+    int32_t g, bq;
+    const int32_t nq = (B + kGalENS - 1) / kGalENS;
+    if (!xcd_map(ngrp, nq, g, bq, kGrpGal)) return;
+    const int32_t b0 = bq * kGalENS;
+    const int32_t p0 = ggrp[g], p1 = ggrp[g + 1];
+    const int32_t e0 = gptr[p0], e1 = gptr[p1];
+    const int32_t e = e0 + (int32_t)threadIdx.x;
+    const int32_t np = p1 - p0;
+    int32_t tI = nC, tq0 = 0, tq1 = 0, tdg = -1;
+    if ((int32_t)threadIdx.x < np * kGalENS) {
+        const int32_t pos = p0 + (int32_t)threadIdx.x / kGalENS;
+        tI = c_sell_row[pos];
+        tq0 = gptr[pos];
+        tq1 = gptr[pos + 1];
+        if (tI < nC) tdg = c_diag[tI];
+    }
+    if (e < e1) {
+        const int32_t fp = gent[3 * (int64_t)e], ii = gent[3 * (int64_t)e + 1], jj = gent[3 * (int64_t)e + 2];
+        float qi[3][3], qj[3][3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                qi[k][c] = Q[((int64_t)ii * 3 + k) * 3 + c];
+                qj[k][c] = Q[((int64_t)jj * 3 + k) * 3 + c];
+            }
+        float a[kGalENS][3][3];
+#pragma unroll
+        for (int t = 0; t < kGalENS; ++t) {
+            ldm<3>(Af + (int64_t)min(b0 + t, B - 1) * f_sell_nb * kB3, max(fp, 0), a[t]);
+            if (fp < 0) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) a[t][r][k] = (fp == -1 && r == k) ? 1.f : 0.f;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kGalENS; ++t) {
+            float T[3][3];  // A Q_j
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) sum += a[t][r][k] * qj[k][c];
+                    T[r][c] = sum;
+                }
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) sum += qi[k][r] * T[k][c];
+                    con[t][3 * r + c][threadIdx.x] = sum;
+                }
+        }
+    }
+    __syncthreads();
+    for (int32_t task = threadIdx.x; task < np * kGalENS; task += kWG) {
+        const int32_t pos = p0 + task / kGalENS, t = task % kGalENS, b = b0 + t;
+        const bool first = task == (int32_t)threadIdx.x;
+        const int32_t I = first ? tI : c_sell_row[pos];
+        if (I >= nC || b >= B) continue;
+        float Cm[3][3] = {};
+        const int32_t q0 = first ? tq0 : gptr[pos], q1 = first ? tq1 : gptr[pos + 1];
+        for (int32_t q = q0; q < q1; ++q)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Cm[k / 3][k % 3] += con[t][k][q - e0];
+        if (pos == (first ? tdg : c_diag[I])) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
+            float D[3][3];
+            inv3(Cm, D);
+            st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
+        }
+        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
+        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+    }
+}
+
 constexpr int kMaxCoarse = 128;
 constexpr int kInvWG = 1024;
 constexpr int kSweepRows = kMaxCoarse * kMaxCoarse / kInvWG;  // 16 matrix rows per thread
@@ -1371,11 +1467,15 @@ bool amg_build(mof_mesh *m) {
             grp.push_back(na);
             D.ngrp = (int32_t)grp.size() - 1;
             put_i(D.rgrp, grp);
-            // level 0, tentative P: coarse position ranges of <= kWG gather
-            // entries for k_galerkin0_ent (unless a single position has more,
-            // or MOF_GAL_ENT=0)
+            // tentative P (every level but a smoothed level 0): coarse position
+            // ranges of <= kWG gather entries and positions for the products by
+            // entry, k_galerkin0_ent / k_galerkin3_ent (unless a single
+            // position has more, or MOF_GAL_ENT=0)
+            // MOF_GAL_ENT=0: no product by entry; MOF_GAL3_ENT=0: level 0 only
             const char *ge = std::getenv("MOF_GAL_ENT");
-            if (l == 0 && !L.smoothed && !(ge && *ge && std::atoi(ge) == 0)) {
+            const char *ge3 = std::getenv("MOF_GAL3_ENT");
+            const bool ent_here = l == 0 || !(ge3 && *ge3 && std::atoi(ge3) == 0);
+            if (!L.smoothed && ent_here && !(ge && *ge && std::atoi(ge) == 0)) {
                 const std::vector<int32_t> &gq = L.gptr;
                 const int32_t npos = (int32_t)gq.size() - 1;
                 bool ok = true;
@@ -1487,6 +1587,10 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                           F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
                                               ? nullptr
                                               : reinterpret_cast<const uint2 *>(G.A0h.p));
+        else if (F.nggrp > 0)
+            k_galerkin3_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
+                F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
+                F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
         else
             k_galerkin3_ns<kGal3NS>
                 <<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGal3NS - 1) / kGal3NS, kGrpGal)), kWG,

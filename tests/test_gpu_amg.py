@@ -234,3 +234,24 @@ def test_galerkin_by_entry_bit_identical(case, monkeypatch):
         m.close()
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][0], out[1][0])
+
+
+def test_coarse_galerkin_by_entry_bit_identical(monkeypatch):
+    """Levels >= 1 by gather entry (k_galerkin3_ent, round 4) against the
+    per-position product (MOF_GAL3_ENT=0, k_galerkin3_ns): the same terms in
+    the same order, the same bits, on a mesh with two coarse products
+    (10,242 -> ~1.3k -> ~170 nodes), ragged system groups."""
+    p, t = synth.icosphere(32, jitter=0.005)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    I = synth.travelling_wave(p, 12)
+    tk = np.arange(12, dtype=np.float64)
+    out = []
+    for ent in ("1", "0"):
+        monkeypatch.setenv("MOF_GAL3_ENT", ent)
+        m = DeviceMesh(p, n, t, a)
+        V, st = m.solve_range(I, tk, 0, 11, 0.01, precision="mixed", precond="amg", batch=7)
+        assert st["failed"] == 0 and st["recovered"] == 0
+        out.append((V, st["iterations"]))
+        m.close()
+    assert out[0][1] == out[1][1]
+    assert np.array_equal(out[0][0], out[1][0])
