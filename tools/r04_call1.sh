@@ -1,7 +1,8 @@
 #!/bin/bash
 # round-4 call 1: the full GPU suite (fused small-mesh solve, two lanes, 3-D
 # residual), C1 / S1s lines eager vs fused, and the C3 A/B of the 3-D residual
-# (MOF_RESIDUAL=rcn: the round-3 one) and of two batches in flight
+# (MOF_RESIDUAL=rcn: the round-3 one), of the coarse Galerkin product by
+# entry (MOF_GAL3_ENT=0: per position) and of two batches in flight
 o=gpurun_out/r04c1
 mkdir -p $o
 S=tools/gpu_step.sh
@@ -14,5 +15,6 @@ done
 for rep in 1 2; do
   $S 300 $o/c3_x3_$rep.json python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 1 --host-batches 0 || exit 99
   MOF_RESIDUAL=rcn $S 300 $o/c3_rcn_$rep.json python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 0 --host-batches 0 || exit 99
+  MOF_GAL3_ENT=0 $S 300 $o/c3_gal3ns_$rep.json python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 0 --host-batches 0 || exit 99
   $S 300 $o/c3_l2_$rep.json python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 0 --host-batches 0 --lanes 2 || exit 99
 done
