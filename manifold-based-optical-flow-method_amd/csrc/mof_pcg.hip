@@ -364,16 +364,17 @@ constexpr int kForce = 1;  // bench: ignore convergence / activity flags
 // __global__ wrappers map blockIdx to them, and the fused small-mesh solve
 // (k_solve_fused) runs the same bodies over every row block of its system in
 // one workgroup -- the same arithmetic in the same order, so the same bits.
-template <typename V>
+template <typename V, int NQ = 1>
 __device__ __forceinline__ void pcg_init_rows(const PcgArgs<V> &a, const double *__restrict__ rhs, int32_t rb,
                                               int32_t b) {
-    __shared__ double lds[8];
+    __shared__ double lds[8 * NQ];
+    const int32_t tid = row_tid();
     if (!a.sysi[b * kSysStride + SI_ACTIVE]) return;
     using V2 = typename VT<V>::V2;
     double rz = 0.0, rr = 0.0;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        const int32_t i = rb * kRowsPerWG + r * kWG + tid;
         if (i >= a.N) break;
         const int64_t vi = (int64_t)b * a.N + i;
         const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
@@ -396,8 +397,8 @@ __device__ __forceinline__ void pcg_init_rows(const PcgArgs<V> &a, const double 
         if (i < a.red.nown) rr += (double)r0 * r0 + (double)r1 * r1;
     }
     double v[2] = {rz, rr};
-    block_sum<2>(v, lds);
-    if (threadIdx.x == 0) {
+    block_sum_q<2, NQ>(v, lds);
+    if (tid == 0 && rb < a.nblk) {
         double *o = a.part_rzrr + 2 * red_rec(a.red, a.B, b, rb);  // slot 0
         o[0] = v[0];
         o[1] = v[1];
@@ -413,12 +414,12 @@ __global__ __launch_bounds__(kWG) void k_pcg_init(PcgArgs<V> a, const double *__
 // row kernels read two doubles instead of re-reducing every workgroup's
 // partial record -- which is what lets the row kernels use small (256-row)
 // workgroups.
-template <typename V>
+template <typename V, int NT = kWG>
 __device__ __forceinline__ void red_rzrr_sys(const PcgArgs<V> &a, int32_t slot, int32_t b) {
-    __shared__ double lds[8];
+    __shared__ double lds[2 * (NT / 64)];
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
     double v[2];
-    reduce_sys<2>(a.part_rzrr + slot * ps, a.red, a.B, b, v, lds);
+    reduce_sys<2, NT>(a.part_rzrr + slot * ps, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) {
         double *o = sc_rzrr(a.sc, a.B, slot, b);
         o[0] = v[0];
@@ -429,12 +430,12 @@ template <typename V>
 __global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
     red_rzrr_sys<V>(a, slot, blockIdx.x);
 }
-template <typename V>
+template <typename V, int NT = kWG>
 __device__ __forceinline__ void red_pq_sys(const PcgArgs<V> &a, int32_t slot, int32_t b) {
-    __shared__ double lds[8];
+    __shared__ double lds[NT / 64];
     const int64_t pqs = (int64_t)a.red.P * a.B * a.red.nmax;
     double v[1];
-    reduce_sys<1>(a.part_pq + slot * pqs, a.red, a.B, b, v, lds);
+    reduce_sys<1, NT>(a.part_pq + slot * pqs, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) *sc_pq(a.sc, a.B, slot, b) = v[0];
 }
 template <typename V>
@@ -448,16 +449,16 @@ __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
 // kept within [rtol, 0.5] -- a system 3x above the outer target (R3 after two
 // steps: the fp32 operator's rounding limits a step to ~3e-4 there) takes a
 // short inner solve, not a full 1e-4 one.
-template <typename V>
+template <typename V, int NT = kWG>
 __device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, double outer_rtol, int32_t b) {
-    __shared__ double lds[8];
+    __shared__ double lds[2 * (NT / 64)];
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) {
         if (threadIdx.x == 0) si[SI_CONV] = 0;
         return;
     }
     double v[2];
-    reduce_sys<2>(a.part_rzrr, a.red, a.B, b, v, lds);
+    reduce_sys<2, NT>(a.part_rzrr, a.red, a.B, b, v, lds);
     if (threadIdx.x == 0) {
         double t = rtol;
         if (outer_rtol > 0.0) {
@@ -476,10 +477,11 @@ __global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, doub
     pcg_tol_sys<V>(a, rtol, outer_rtol, blockIdx.x);
 }
 
-template <typename V, bool FIRST, bool ZH = false>
+template <typename V, bool FIRST, bool ZH = false, int NQ = 1>
 __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, int32_t flags, int32_t rb, int32_t b) {
     constexpr int NT = kWG, RPT = kRows;  // rows per thread
-    __shared__ double lds[2 * (NT / 64)];
+    __shared__ double lds[NQ * (NT / 64)];
+    const int32_t tid = row_tid();
     const bool force = flags & kForce;
     // retired systems: inactive, or converged in an earlier iteration (the
     // word is sticky, so no later launch re-reads a stale partial slot)
@@ -511,7 +513,7 @@ __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, i
         if (!FIRST) {
 #pragma unroll
             for (int r = 0; r < RPT; ++r) {
-                const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
+                const int32_t i = rb * kRowsPerWG + r * NT + tid;
                 if (i >= a.N) break;
                 const int64_t vi = vb + i;
                 const V2 p0 = *reinterpret_cast<const V2 *>(a.p + 2 * vi);
@@ -521,13 +523,13 @@ __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, i
                 *reinterpret_cast<V2 *>(a.x + 2 * vi) = xi;
             }
         }
-        if (rb == 0 && threadIdx.x == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
+        if (rb == 0 && tid == 0 && a.sysi[b * kSysStride + SI_CONV] < 0)
             a.sysi[b * kSysStride + SI_CONV] = it;
         return;
     }
     // stagnation bookkeeping: one thread of the system's first row block (no
     // other workgroup reads these slots; k_pcg_update reads them next launch)
-    if (!force && rb == 0 && threadIdx.x == 0 && cur[1] < a.sysd[b * kSysStride + SD_BEST]) {
+    if (!force && rb == 0 && tid == 0 && cur[1] < a.sysd[b * kSysStride + SD_BEST]) {
         a.sysd[b * kSysStride + SD_BEST] = cur[1];
         a.sysi[b * kSysStride + SI_BEST_IT] = it;
     }
@@ -536,7 +538,7 @@ __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, i
     double pq = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * NT + threadIdx.x;
+        const int32_t i = rb * kRowsPerWG + r * NT + tid;
         if (i >= a.N) break;
         V y0, y1;
         const int64_t vi = vb + i;
@@ -571,8 +573,8 @@ __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, i
         if (i < a.red.nown) pq += (double)pi.x * qi.x + (double)pi.y * qi.y;
     }
     double v[1] = {pq};
-    block_sum<1, NT>(v, lds);
-    if (threadIdx.x == 0) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, b, rb)] = v[0];
+    block_sum_q<1, NQ>(v, lds);
+    if (tid == 0 && rb < a.nblk) a.part_pq[(it & 1) * pqs + red_rec(a.red, a.B, b, rb)] = v[0];
 }
 template <typename V, bool FIRST, bool ZH = false>
 __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
@@ -636,9 +638,10 @@ constexpr int kUpdRB = 4;  // row blocks per update workgroup
 inline unsigned upd_blocks(int32_t nblk) { return (unsigned)((nblk + kUpdRB - 1) / kUpdRB); }
 
 // g: the group of kUpdRB row blocks
-template <typename V>
+template <typename V, int NQ = 1>
 __device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it, int32_t g, int32_t b) {
-    __shared__ double lds[(kWG / 64) * 2 * kUpdRB];
+    __shared__ double lds[NQ * (kWG / 64) * 2 * kUpdRB];
+    const int32_t tid = row_tid();
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
@@ -663,7 +666,7 @@ __device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it,
     else if (a.stall > 0 && it - si[SI_BEST_IT] > a.stall)
         why = FW_STALLED;
     if (why) {
-        if (g == 0 && threadIdx.x == 0) {
+        if (g == 0 && tid == 0) {
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
             si[SI_FAIL_IT] = it;
@@ -685,7 +688,7 @@ __device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it,
     V2 qv[R], rv[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-        iv[q] = (g * R + q) * kRowsPerWG + threadIdx.x;
+        iv[q] = (g * R + q) * kRowsPerWG + tid;
         const int64_t vi = (int64_t)b * a.N + min(iv[q], a.N - 1);
         qv[q] = *reinterpret_cast<const V2 *>(a.q + 2 * vi);
         rv[q] = *reinterpret_cast<const V2 *>(a.r + 2 * vi);
@@ -726,8 +729,8 @@ __device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it,
         v[2 * q] = rz;
         v[2 * q + 1] = rr;
     }
-    block_sum<2 * R>(v, lds);
-    if (threadIdx.x == 0) {
+    block_sum_q<2 * R, NQ>(v, lds);
+    if (tid == 0) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int32_t rbk = g * R + q;
@@ -759,7 +762,7 @@ __device__ __forceinline__ void outer_update_rows(int32_t N, int32_t first, cons
                                                   int32_t blk, int32_t b, const double *__restrict__ e = nullptr,
                                                   double *__restrict__ X3 = nullptr) {
     if (!sysi[b * kSysStride + SI_ACTIVE]) return;
-    const int32_t i = blk * kWG + threadIdx.x;
+    const int32_t i = blk * kWG + row_tid();
     if (i >= N) return;
     const int64_t vi = (int64_t)b * N + i;
     using V2 = typename VT<V>::V2;
@@ -797,18 +800,20 @@ __global__ __launch_bounds__(kWG) void k_make_x3(int32_t N, const double *__rest
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
 // partial |r|^2 and |f|^2.
+template <int NQ = 1>
 __device__ __forceinline__ void residual_rows(const OpArgs<double> &op, int32_t B, const RedArgs &rd,
                                               const double *__restrict__ rhs, const double *__restrict__ x64,
                                               const int32_t *__restrict__ sysi, double *__restrict__ r64,
                                               double *__restrict__ part, int32_t rb, int32_t b) {
-    __shared__ double lds[8];
+    __shared__ double lds[8 * NQ];
+    const int32_t tid = row_tid();
     if (!sysi[b * kSysStride + SI_ACTIVE]) return;
     const int32_t N = op.N;
     const int64_t vb = (int64_t)b * N;
     double rr = 0.0, ff = 0.0;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
+        const int32_t i = rb * kRowsPerWG + r * kWG + tid;
         if (i >= N) break;
         double y0, y1;
         apply_row_mf<double>(op, b, i, x64 + 2 * vb, y0, y1);
@@ -821,8 +826,8 @@ __device__ __forceinline__ void residual_rows(const OpArgs<double> &op, int32_t 
         }
     }
     double v[2] = {rr, ff};
-    block_sum<2>(v, lds);
-    if (threadIdx.x == 0) {
+    block_sum_q<2, NQ>(v, lds);
+    if (tid == 0 && rb < rd.nmax) {
         double *o = part + 2 * red_rec(rd, B, b, rb);
         o[0] = v[0];
         o[1] = v[1];
@@ -836,7 +841,7 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
                                                   double *__restrict__ part) {
     int32_t rb, b;  // XCD-aware: the systems of a row block share its a2 blocks in L2
     if (!xcd_map(nblk, B, rb, b, kGrpRes)) return;
-    residual_rows(op, B, rd, rhs, x64, sysi, r64, part, rb, b);
+    residual_rows<1>(op, B, rd, rhs, x64, sysi, r64, part, rb, b);
 }
 
 // The re-forming residual, NS systems per thread (apply_row_rcn): grid
@@ -1056,14 +1061,15 @@ __global__ __launch_bounds__(kWG) void k_residual_x3(OpArgs<double> op, const do
 }
 
 // One workgroup per system: relative true residual; retire converged systems.
+template <int NT = kWG>
 __device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, const double *__restrict__ part,
                                                 double rtol, double *__restrict__ sysd, int32_t *__restrict__ sysi,
                                                 int32_t b) {
-    __shared__ double lds[8];
+    __shared__ double lds[2 * (NT / 64)];
     int32_t *si = sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) return;
     double v[2];
-    reduce_sys<2>(part, rd, B, b, v, lds);
+    reduce_sys<2, NT>(part, rd, B, b, v, lds);
     if (threadIdx.x == 0) {
         const double rel = v[1] > 0.0 ? sqrt(v[0] / v[1]) : (v[0] > 0.0 ? INFINITY : 0.0);
         sysd[b * kSysStride + SD_REL] = rel;
@@ -1081,7 +1087,7 @@ __device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, co
 __global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, const double *__restrict__ part,
                                                      double rtol, double *__restrict__ sysd,
                                                      int32_t *__restrict__ sysi) {
-    outer_check_sys(rd, B, part, rtol, sysd, sysi, blockIdx.x);
+    outer_check_sys<kWG>(rd, B, part, rtol, sysd, sysi, blockIdx.x);
 }
 
 __global__ void k_sys_reset(int32_t B, int32_t *__restrict__ sysi, double *__restrict__ sysd) {
@@ -1417,7 +1423,8 @@ __device__ __forceinline__ int32_t ld_flag(const int32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ __launch_bounds__(kWG) void k_solve_fused(PcgArgs<double> a, OpArgs<double> op, FusedArgs f) {
+template <int NQ>
+__global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpArgs<double> op, FusedArgs f) {
     const int32_t b = blockIdx.x;
     int32_t *si = a.sysi + b * kSysStride;
     double *sd = a.sysd + b * kSysStride;
@@ -1432,43 +1439,45 @@ __global__ __launch_bounds__(kWG) void k_solve_fused(PcgArgs<double> a, OpArgs<d
     __syncthreads();
     const int32_t nvb = (a.N + kWG - 1) / kWG;              // k_outer_update's blocks
     const int32_t nug = (a.nblk + kUpdRB - 1) / kUpdRB;     // k_pcg_update's row-block groups
+    constexpr int NT = NQ * kWG;
+    const int32_t q = threadIdx.x / kWG;  // this thread's row block of each group of NQ
     int32_t itsum = 0, itmax = 0, o = 0;
     for (; o < f.max_outer; ++o) {
         // pcg<double>: the first step to 0.5 rtol, later ones to inner_rtol
         const double *rhs = o == 0 ? f.rhs : f.r64;
-        for (int32_t rb = 0; rb < a.nblk; ++rb) pcg_init_rows<double>(a, rhs, rb, b);
+        for (int32_t rb = 0; rb < a.nblk; rb += NQ) pcg_init_rows<double, NQ>(a, rhs, rb + q, b);
         __syncthreads();
-        pcg_tol_sys<double>(a, o == 0 ? 0.5 * f.rtol : f.inner_rtol, o > 0 && f.adaptive ? f.rtol : 0.0, b);
+        pcg_tol_sys<double, NT>(a, o == 0 ? 0.5 * f.rtol : f.inner_rtol, o > 0 && f.adaptive ? f.rtol : 0.0, b);
         __syncthreads();
-        red_rzrr_sys<double>(a, 0, b);
+        red_rzrr_sys<double, NT>(a, 0, b);
         __syncthreads();
         int32_t it = 0;
         bool fin = false;
         for (; it < f.max_iter; ++it) {
-            for (int32_t rb = 0; rb < a.nblk; ++rb) {
+            for (int32_t rb = 0; rb < a.nblk; rb += NQ) {
                 if (it == 0)
-                    pcg_spmv_rows<double, true>(a, it, 0, rb, b);
+                    pcg_spmv_rows<double, true, false, NQ>(a, it, 0, rb + q, b);
                 else
-                    pcg_spmv_rows<double, false>(a, it, 0, rb, b);
+                    pcg_spmv_rows<double, false, false, NQ>(a, it, 0, rb + q, b);
             }
             __syncthreads();
             if (ld_flag(si + SI_CONV) >= 0 || !ld_flag(si + SI_ACTIVE)) {
                 fin = true;
                 break;
             }
-            red_pq_sys<double>(a, it & 1, b);
+            red_pq_sys<double, NT>(a, it & 1, b);
             __syncthreads();
-            for (int32_t g = 0; g < nug; ++g) pcg_update_rows<double>(a, it, g, b);
+            for (int32_t g = 0; g < nug; g += NQ) pcg_update_rows<double, NQ>(a, it, g + q, b);
             __syncthreads();
             if (!ld_flag(si + SI_ACTIVE)) {  // breakdown / divergence / stagnation
                 fin = true;
                 break;
             }
-            red_rzrr_sys<double>(a, (it + 1) & 1, b);
+            red_rzrr_sys<double, NT>(a, (it + 1) & 1, b);
             __syncthreads();
         }
         if (!fin) {  // the check launch after max_iter (SI_CONV of a system converged there)
-            for (int32_t rb = 0; rb < a.nblk; ++rb) pcg_spmv_rows<double, false>(a, it, 0, rb, b);
+            for (int32_t rb = 0; rb < a.nblk; rb += NQ) pcg_spmv_rows<double, false, false, NQ>(a, it, 0, rb + q, b);
             __syncthreads();
         }
         // this inner solve's iterations, counted as pcg() counts them
@@ -1479,12 +1488,12 @@ __global__ __launch_bounds__(kWG) void k_solve_fused(PcgArgs<double> a, OpArgs<d
                                           : it);
         itsum += its;
         itmax = max(itmax, its);
-        for (int32_t blk = 0; blk < nvb; ++blk) outer_update_rows<double>(a.N, o == 0, a.x, a.sysi, f.x64, blk, b);
+        for (int32_t blk = 0; blk < nvb; blk += NQ) outer_update_rows<double>(a.N, o == 0, a.x, a.sysi, f.x64, blk + q, b);
         __syncthreads();
-        for (int32_t rb = 0; rb < a.nblk; ++rb)
-            residual_rows(op, a.B, a.red, f.rhs, f.x64, a.sysi, f.r64, f.part_rr0, rb, b);
+        for (int32_t rb = 0; rb < a.nblk; rb += NQ)
+            residual_rows<NQ>(op, a.B, a.red, f.rhs, f.x64, a.sysi, f.r64, f.part_rr0, rb + q, b);
         __syncthreads();
-        outer_check_sys(a.red, a.B, f.part_rr0, f.rtol, a.sysd, a.sysi, b);
+        outer_check_sys<NT>(a.red, a.B, f.part_rr0, f.rtol, a.sysd, a.sysi, b);
         __syncthreads();
         if (!ld_flag(si + SI_ACTIVE)) {
             ++o;
@@ -1591,6 +1600,17 @@ bool fused_eligible(const mof_mesh *m, const SolveParams &sp, const uint8_t *onl
     return m->ws.nblk <= max_blk;
 }
 
+// Row blocks the fused solve's workgroup runs side by side (groups of 256
+// threads; MOF_FUSED_NQ = 1 / 2 / 4 forces a width)
+int fused_quarters(int32_t nblk) {
+    static const int forced = [] {
+        const char *v = std::getenv("MOF_FUSED_NQ");
+        return v && *v ? std::atoi(v) : 0;
+    }();
+    if (forced == 1 || forced == 2 || forced == 4) return forced;
+    return nblk >= 4 ? 4 : (nblk >= 2 ? 2 : 1);
+}
+
 int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s, int32_t *outer,
                     int32_t *max_iters, SpmvTiming *timing, const uint8_t *only) {
     SpmvTiming *tm = sp.time_spmv ? timing : nullptr;
@@ -1611,10 +1631,14 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             }
             e0 = m->spmv_events[0];
             e1 = m->spmv_events[1];
-            hipExtLaunchKernelGGL(k_solve_fused, dim3((unsigned)B), dim3(kWG), 0, s, e0, e1, 0, a, op64(m), fa);
-        } else {
-            k_solve_fused<<<dim3((unsigned)B), kWG, 0, s>>>(a, op64(m), fa);
         }
+        // row blocks side by side: NQ groups of 256 threads per workgroup
+        const int nq = fused_quarters(m->ws.nblk);
+        auto kf = nq >= 4 ? k_solve_fused<4> : (nq == 2 ? k_solve_fused<2> : k_solve_fused<1>);
+        if (tm)
+            hipExtLaunchKernelGGL(kf, dim3((unsigned)B), dim3(nq * kWG), 0, s, e0, e1, 0, a, op64(m), fa);
+        else
+            hipLaunchKernelGGL(kf, dim3((unsigned)B), dim3(nq * kWG), 0, s, a, op64(m), fa);
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
         int64_t iters = 0;

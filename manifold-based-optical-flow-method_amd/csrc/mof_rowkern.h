@@ -104,6 +104,31 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
     __syncthreads();
 }
 
+// block_sum over each group of kWG threads of an NQ * kWG workgroup (the
+// fused solve runs NQ row blocks side by side): lds holds NQ * 4 * NV
+// doubles; the same order as block_sum<NV, kWG>, so the same bits.
+template <int NV, int NQ>
+__device__ __forceinline__ void block_sum_q(double (&v)[NV], double *lds) {
+    if constexpr (NQ == 1) {
+        block_sum<NV, kWG>(v, lds);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+        }
+        __syncthreads();
+        const double *L = lds + (w & ~3) * NV;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = ((L[k] + L[NV + k]) + L[2 * NV + k]) + L[3 * NV + k];
+        __syncthreads();
+    }
+}
+// the thread's index within its group of kWG (row kernels: its row)
+__device__ __forceinline__ int32_t row_tid() { return (int32_t)(threadIdx.x & (kWG - 1)); }
+
 // Sum n partials of NV values each (record stride NV) in a fixed order: the
 // first kWG threads load, so any workgroup size NT gets the same bits.
 template <int NV, int NT = kWG>

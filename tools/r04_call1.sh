@@ -12,6 +12,9 @@ for cfg in C1 S1s; do
   $S 300 $o/bench_${cfg}_f64_eager.json python3 bench.py --config $cfg --precision f64 --fused off --steps 20 --warmup 2 --no-cpu-baseline --host-batches 0 || exit 99
   $S 300 $o/bench_${cfg}_f64_fused.json python3 bench.py --config $cfg --precision f64 --fused on --steps 20 --warmup 2 --no-cpu-baseline --host-batches 0 || exit 99
 done
+for nq in 1 2 4; do
+  MOF_FUSED_NQ=$nq $S 300 $o/bench_S1s_f64_fused_nq$nq.json python3 bench.py --config S1s --precision f64 --fused on --steps 20 --warmup 2 --no-cpu-baseline --host-batches 0 --parity-samples 0 || exit 99
+done
 for rep in 1 2; do
   $S 300 $o/c3_x3_$rep.json python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 1 --host-batches 0 || exit 99
   MOF_RESIDUAL=rcn $S 300 $o/c3_rcn_$rep.json python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --parity-samples 0 --host-batches 0 || exit 99
