@@ -531,7 +531,49 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
 struct TriGeo {
     const double *gw, *e, *area, *J0, *J1, *dt;  // J0 / J1: the batch's I rows (internal order, stride N)
 };
+// Round 4: the a1 fold in ambient 3-D. a1's block (i, j) is
+// sum_T w_ij (E_i gI_T)(E_j gI_T)^T = E_i G_ij E_j^T with the symmetric 3x3
+// G_ij = sum_T w_ij gI_T gI_T^T (compute_a1 :273-285), so a row folds one
+// outer product per incident triangle into its slots' G (6 floats each) and
+// projects each stored slot once at the end -- no tangent frames of the two
+// other corners gathered per incidence and no u_j, u_k dots (A32 is an fp32
+// fold of the same operator, rounded differently; f keeps its bits).
+// g3_store: the slots' blocks E_i G E_j^T + lambda a2, then rows_store's stores.
 template <int WMAX>
+__device__ __forceinline__ void g3_project(const float (&G)[WMAX][6], const double (&ei)[6], int32_t deg, int64_t o,
+                                           const int32_t *__restrict__ sell_col, const double *__restrict__ e,
+                                           const int32_t *__restrict__ mir, float (&acc)[WMAX][4]) {
+    float eif[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) eif[k] = (float)ei[k];
+#pragma unroll
+    for (int z = 0; z < WMAX; ++z) {
+        acc[z][0] = acc[z][1] = acc[z][2] = acc[z][3] = 0.f;
+        if (z >= deg) continue;
+        const int64_t pos = o + (int64_t)z * kSlice;
+        if (mir && (mir[pos] & kMirT)) continue;  // lower blocks are never stored
+        const int32_t j = sell_col[pos];
+        float ej[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ej[k] = (float)e[6 * (int64_t)j + k];
+        // G = [xx xy xz; xy yy yz; xz yz zz]; H = G E_j^T (3 x 2)
+        const float *g = G[z];
+        float H[3][2];
+#pragma unroll
+        for (int be = 0; be < 2; ++be) {
+            const float *v = ej + 3 * be;
+            H[0][be] = g[0] * v[0] + g[1] * v[1] + g[2] * v[2];
+            H[1][be] = g[1] * v[0] + g[3] * v[1] + g[4] * v[2];
+            H[2][be] = g[2] * v[0] + g[4] * v[1] + g[5] * v[2];
+        }
+#pragma unroll
+        for (int al = 0; al < 2; ++al)
+#pragma unroll
+            for (int be = 0; be < 2; ++be)
+                acc[z][2 * al + be] = eif[3 * al] * H[0][be] + eif[3 * al + 1] * H[1][be] + eif[3 * al + 2] * H[2][be];
+    }
+}
+template <int WMAX, bool G3 = false>
 __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
@@ -548,11 +590,16 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
         if (i >= N) break;
         const int32_t s = i >> 6, l = i & 63;
         float acc[WMAX][4];
+        float G[G3 ? WMAX : 1][6];
         double ei[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) ei[k] = geo.e[6 * (int64_t)i + k];
 #pragma unroll
         for (int z = 0; z < WMAX; ++z) acc[z][0] = acc[z][1] = acc[z][2] = acc[z][3] = 0.f;
+#pragma unroll
+        for (int z = 0; z < (G3 ? WMAX : 1); ++z)
+#pragma unroll
+            for (int x = 0; x < 6; ++x) G[z][x] = 0.f;
         double f0 = 0.0, f1 = 0.0;
         const double Ii0 = I0b[i], pdi = (I1b[i] - Ii0) / hb;
         const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
@@ -566,10 +613,12 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             double g[9], ej[6], ek[6];
 #pragma unroll
             for (int k = 0; k < 9; ++k) g[k] = geo.gw[9 * T + k];
+            if constexpr (!G3) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                ej[k] = geo.e[6 * (int64_t)vj + k];
-                ek[k] = geo.e[6 * (int64_t)vk + k];
+                for (int k = 0; k < 6; ++k) {
+                    ej[k] = geo.e[6 * (int64_t)vj + k];
+                    ek[k] = geo.e[6 * (int64_t)vk + k];
+                }
             }
             const double At = geo.area[T];
             const float wv = w12[q.x];
@@ -595,6 +644,17 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             // a term on the diagonal block takes A/6 = 2 A/12 (a degenerate
             // triangle's second corner at i included)
             const float wd = wv + wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
+            if constexpr (G3) {
+                const float gx = (float)gI[0], gy = (float)gI[1], gz = (float)gI[2];
+                const float op[6] = {gx * gx, gx * gy, gx * gz, gy * gy, gy * gz, gz * gz};
+#pragma unroll
+                for (int z = 0; z < WMAX; ++z) {
+                    const float cz = (z == 0 ? wd : 0.f) + (z == sj ? wj : 0.f) + (z == sk ? wk : 0.f);
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) G[z][x] = __builtin_fmaf(cz, op[x], G[z][x]);
+                }
+                continue;
+            }
             const float ui[2] = {(float)ui0, (float)ui1};
             const float uj[2] = {(float)dot64(gI, ej), (float)dot64(gI, ej + 3)};
             const float uk[2] = {(float)dot64(gI, ek), (float)dot64(gI, ek + 3)};
@@ -612,6 +672,8 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
                 }
             }
         }
+        if constexpr (G3)
+            g3_project<WMAX>(G, ei, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_col, geo.e, mir, acc);
         rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
                          block_jacobi, A, dinv32, rhs, Ah, nown, mir);
     }
@@ -914,8 +976,11 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
     const int32_t *mirw = m->sym_reads ? m->sell_mir.p : nullptr;
+    // MOF_ASM_G3=1: the a1 fold in ambient 3-D (A/B switch, read per batch)
+    const char *g3e = std::getenv("MOF_ASM_G3");
+    const bool g3 = g3e && *g3e && std::atoi(g3e) != 0;
 #define MOF_ASM_RC_LAUNCH(WM)                                                                                     \
-    k_assemble_rows_rc<WM><<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>(                                        \
+    (g3 ? k_assemble_rows_rc<WM, true> : k_assemble_rows_rc<WM, false>)<<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>( \
         m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
         reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p, m->w12_32.p, m->a2s32.p, bj, w.A32.p, w.dinv32.p,   \
         w.rhs.p, bf.A0h, m->n_own, mirw, geo)

@@ -282,3 +282,30 @@ def test_f64_without_block_jacobi_recovers():
                           max_iter=5, max_outer=1)
     assert st["failed"] == 0 and st["recovered"] == 4 and st["recovered_f64"] == 4, st
     assert np.abs(V - g["V_k"][:4]).max() < VTOL
+
+
+def test_assembly_g3_fold_matches_spsolve(monkeypatch):
+    """The row assembly's a1 fold in ambient 3-D (MOF_ASM_G3=1: E_i G E_j^T
+    per slot, round 4) assembles the same operator up to fp32 rounding: V
+    within the north-star bar of spsolve, f (fp64) untouched."""
+    from mofhip import DeviceMesh, synth
+    import oracle
+    from scipy.sparse.linalg import spsolve
+    p, t = synth.icosphere(20, jitter=0.005)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    I = synth.travelling_wave(p, 5)
+    tk = np.arange(5, dtype=np.float64)
+    out = {}
+    for g3 in ("0", "1"):
+        monkeypatch.setenv("MOF_ASM_G3", g3)
+        m = DeviceMesh(p, n, t, a)
+        V, st = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", precond="amg")
+        assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
+        out[g3] = (V, st["iterations"])
+        m.close()
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    for k in (0, 3):
+        A, f = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
+        Vo = spsolve(A.tocsc(), f)
+        assert np.abs(out["1"][0][k] - Vo).max() < 1e-6
+    assert abs(out["1"][1] - out["0"][1]) <= 0.1 * out["0"][1]
