@@ -976,9 +976,11 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
     const int32_t *mirw = m->sym_reads ? m->sell_mir.p : nullptr;
-    // MOF_ASM_G3=1: the a1 fold in ambient 3-D (A/B switch, read per batch)
+    // the a1 fold in ambient 3-D (k_assemble_rows_rc<., true>); MOF_ASM_G3=0/1
+    // forces either (A/B switch, read per batch)
+    constexpr bool kAsmG3 = false;
     const char *g3e = std::getenv("MOF_ASM_G3");
-    const bool g3 = g3e && *g3e && std::atoi(g3e) != 0;
+    const bool g3 = g3e && *g3e ? std::atoi(g3e) != 0 : kAsmG3;
 #define MOF_ASM_RC_LAUNCH(WM)                                                                                     \
     (g3 ? k_assemble_rows_rc<WM, true> : k_assemble_rows_rc<WM, false>)<<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>( \
         m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
