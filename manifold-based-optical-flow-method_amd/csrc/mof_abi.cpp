@@ -293,6 +293,21 @@ void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, c
     int32_t nfirst = 0;
     for (int32_t b = 0; b < nb; ++b) nfirst += (first[b] = failed(b));
     if (!nfirst) return;
+    // MOF_SOLVE_VERBOSE: why and when the first solve's failed systems failed
+    if (std::getenv("MOF_SOLVE_VERBOSE")) {
+        int32_t why[8] = {0}, itmin = 1 << 30, itmax = 0;
+        for (int32_t b = 0; b < nb; ++b)
+            if (first[b]) {
+                why[std::min(7, std::max(0, sysi[b * kSysStride + SI_FAIL_WHY]))]++;
+                itmin = std::min(itmin, sysi[b * kSysStride + SI_FAIL_IT]);
+                itmax = std::max(itmax, sysi[b * kSysStride + SI_FAIL_IT]);
+            }
+        std::fprintf(stderr,
+                     "[mof recover] %d of %d failed: breakdown %d diverged %d stalled %d max_iter %d residual %d; "
+                     "at inner iteration %d..%d\n",
+                     nfirst, nb, why[FW_BREAKDOWN], why[FW_DIVERGED], why[FW_STALLED], why[FW_MAXITER],
+                     why[FW_RESIDUAL], itmin, itmax);
+    }
     bool used_f64 = false;
     for (uint32_t prec : passes) {
         int32_t n = 0;

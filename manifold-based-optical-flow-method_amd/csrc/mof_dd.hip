@@ -830,7 +830,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                                     ok = false;
                                     err = e;
                                 }
-                                if (env_int_dd("MOF_DD_TEST_OOM_RANK", -1) == d->rank && prec == MOF_PREC_F64) {
+                                if (d->rank >= 0 && env_int_dd("MOF_DD_TEST_OOM_RANK", -1) == d->rank && prec == MOF_PREC_F64) {
                                     ok = false;  // test hook: this rank's fp64 workspace "fails"
                                     err = Error{MOF_E_HIP, "injected allocation failure"};
                                 }
