@@ -184,7 +184,7 @@ def parity_check(geom, t, a, lam, samples):
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
-def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0, cores=0):
+def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0, cores=0, config="C3"):
     """The reference CPU path (lil assembly + spsolve on a Pool), timed on this
     host on a bounded sample: Pool(C) runs per_core * C timesteps (SURVEY.md
     §8(d): 2 C); each assembles the first `frac` of the triangles with the
@@ -203,7 +203,7 @@ def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0,
     a2l = clone.as_lil(a2)
     T = K + 1
     from mofhip import synth
-    I = synth.travelling_wave(p, T)
+    I = synth.config_wave(config, p, T)
     tk = list(range(T))
     M = len(t)
     S = max(1, int(M * frac))
@@ -289,14 +289,15 @@ def main():
     # (K_rank + 1) x N f64 is 7.4 GB per rank at the default C3 sizes, which
     # 8 ranks would otherwise hold in host memory
     dev = torch.device("cpu") if dry else torch.device("cuda", local)
-    pts = torch.from_numpy(np.ascontiguousarray(p[:, :2])).to(dev)
-    phi = torch.atan2(pts[:, 1], pts[:, 0])
+    # the config's travelling wave (synth.wave_phase): sin(kappa phase - 0.3 k)
+    phase, kappa = synth.wave_phase(args.config, p)
+    phi = torch.from_numpy(np.ascontiguousarray(phase)).to(dev)
     kk = k_off + torch.arange(K_rank + 1, dtype=torch.float64, device=dev)
     I_dev = torch.empty((K_rank + 1, N), dtype=torch.float64, device=dev)
     for r0 in range(0, (K_rank + 1) if not dry else 0, 256):
         r1 = min(K_rank + 1, r0 + 256)
-        I_dev[r0:r1] = torch.sin(3.0 * phi[None, :] - 0.3 * kk[r0:r1, None])
-    del pts, phi, kk
+        I_dev[r0:r1] = torch.sin(kappa * phi[None, :] - 0.3 * kk[r0:r1, None])
+    del phi, kk
     host_io = args.io == "host"
     I_host = V_host = None
     if host_io:
@@ -479,7 +480,7 @@ def main():
     if rank == 0 and not args.no_cpu_baseline and not dry:
         cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom,
                            full_timesteps=args.fixed_timesteps if args.config in SMALL_JOBS else 0,
-                           cores=args.cpu_cores)
+                           cores=args.cpu_cores, config=args.config)
 
     if rank == 0:
         line = {
@@ -490,7 +491,8 @@ def main():
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "f32" if precision == "mixed" else "f64",
-            "data": "synthetic travelling wave sin(3 phi - 0.3 k), dt = 1, lambda = 0.01",
+            "data": "synthetic travelling wave sin(%g phi - 0.3 k) (synth.wave_phase), dt = 1, lambda = 0.01"
+                    % synth.wave_phase(args.config, p[:1])[1],
             "config": {"workload": CONFIG_NAMES[args.config], "vertices": N, "triangles": len(t),
                        "timesteps_per_step": args.fixed_timesteps if strong else world * B,
                        "timesteps_timed": n_ts, "batch": B, "precision": precision,

@@ -28,6 +28,8 @@ __all__ = [
     "travelling_wave",
     "electrode_surface",
     "mesh_for_config",
+    "wave_phase",
+    "config_wave",
     "CONFIG_FREQ",
 ]
 
@@ -332,6 +334,27 @@ def travelling_wave(points: np.ndarray, T: int, kappa: float = 3.0,
                     omega: float = 0.3) -> np.ndarray:
     """``I[k, x] = sin(kappa * atan2(y, x) - omega * k)``, shape (T, N) f64."""
     phi = np.arctan2(points[:, 1], points[:, 0])
+    k = np.arange(T, dtype=np.float64)[:, None]
+    return np.sin(kappa * phi[None, :] - omega * k)
+
+
+def wave_phase(name: str, points: np.ndarray):
+    """(phase (N,), kappa) of the bench signal I_k = sin(kappa phase - 0.3 k)
+    on config ``name``'s mesh: on the spheres the azimuth about the z axis
+    (kappa 3: a pattern rotating around the sphere); on the S1-like patches
+    (centred on the z axis, curvature centre (0, 0, -70 mm)) the angle about
+    the x axis through the curvature centre, kappa 30 -- a wave travelling
+    across the electrode grid (about 3 wavelengths over it) instead of a
+    pinwheel whose unbounded gradient would sit at the patch centre."""
+    p = np.asarray(points, dtype=np.float64)
+    if name in ("S1", "S1s"):
+        return np.arctan2(p[:, 2] + 70.0, p[:, 1]), 30.0
+    return np.arctan2(p[:, 1], p[:, 0]), 3.0
+
+
+def config_wave(name: str, points: np.ndarray, T: int, omega: float = 0.3) -> np.ndarray:
+    """The bench signal of config ``name`` (wave_phase), shape (T, N) f64."""
+    phi, kappa = wave_phase(name, points)
     k = np.arange(T, dtype=np.float64)[:, None]
     return np.sin(kappa * phi[None, :] - omega * k)
 
