@@ -91,9 +91,6 @@ def parse():
                     help="timesteps of the last timed batch checked against the oracle + spsolve (0: none)")
     ap.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
                     help="fp64: the one-launch fused solve per batch (auto: the library's choice, small meshes)")
-    ap.add_argument("--lanes", type=int, default=1, choices=[1, 2],
-                    help="2: two batches in flight per GPU (MOF_TWO_LANES); the timed region is then one library "
-                         "call over all timed batches")
     ap.add_argument("--host-batches", type=int, default=4,
                     help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
                          "the device-resident region (0: none)")
@@ -305,16 +302,12 @@ def main():
         del I_dev
         I_dev = None
     else:
-        # two lanes: one call over all timed batches writes all of their V
-        v_rows = B
-        if args.lanes > 1:
-            v_rows = K_rank if strong else B * max(args.steps, args.warmup)
-        V_dev = torch.empty((v_rows, 2 * N), dtype=torch.float64, device=dev)
+        V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
     tk = np.arange(K_rank + 1, dtype=np.float64)
     sync()
     precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
     opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol,
-                fused={"auto": None, "on": True, "off": False}[args.fused], lanes=args.lanes)
+                fused={"auto": None, "on": True, "off": False}[args.fused])
 
     kept = []  # host V of the timed calls, freed after the clock stops (the caller keeps its result)
 
@@ -342,7 +335,7 @@ def main():
         opts["batch"] = B_eff
         batches = [(a, min(a + B_eff, K_rank)) for a in range(0, K_rank, B_eff)]
         warm = batches[:max(1, args.warmup)] if batches else []
-        if host_io or args.lanes > 1:
+        if host_io:
             step_calls = [(0, K_rank)]
         else:
             step_calls = batches
@@ -350,9 +343,8 @@ def main():
     else:
         warm = [(s * B, (s + 1) * B) for s in range(args.warmup)]
         timed = [(s * B, (s + 1) * B) for s in range(args.warmup, args.warmup + args.steps)]
-        one_call = host_io or args.lanes > 1
-        timed_calls = [(timed[0][0], timed[-1][1])] if one_call else timed
-        if one_call and warm:
+        timed_calls = [(timed[0][0], timed[-1][1])] if host_io else timed
+        if host_io and warm:
             warm = [(warm[0][0], warm[-1][1])]
     for a_, b_ in warm:
         solve(a_, b_, False)

@@ -72,9 +72,10 @@ extern "C" {
 #define MOF_NO_RECOVERY 16u    /* systems whose solve fails (breakdown,
                                   divergence, stagnation, max_iter) are
                                   NaN-filled at once. Default: they are
-                                  re-solved, alone, with block-Jacobi PCG in
-                                  the same precision (after a multigrid
-                                  solve) and then in fp64 (an fp64 solve:
+                                  re-solved, alone, with the multigrid at a
+                                  fine-level damping of 0.6 and with
+                                  block-Jacobi PCG in the same precision
+                                  (after a multigrid solve) and then in fp64 (an fp64 solve:
                                   once more in fp64 with block Jacobi when
                                   it ran without it or with max_iter below
                                   10^4), each with max(max_iter, 10^4)
@@ -96,12 +97,6 @@ extern "C" {
                                   (MOF_FUSED_MAX_BLK), where the eager
                                   launches are latency-bound */
 #define MOF_SOLVE_EAGER 256u   /* never the fused solve */
-#define MOF_TWO_LANES 512u     /* two batches in flight: batches alternate
-                                  between the handle and a twin handle on the
-                                  same device (own stream and workspace,
-                                  created on first use), each driven by its
-                                  own host thread; V is bit-identical to one
-                                  lane. Ignored with a caller stream */
 
 /* mof_csr_export which */
 #define MOF_CSR_A2 0           /* smoothness matrix a2 (2N x 2N) */

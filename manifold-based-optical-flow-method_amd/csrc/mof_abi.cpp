@@ -126,19 +126,20 @@ void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
     }
 }
 
-// One lane of mof_solve_range: batches j = lane, lane + lanes, ... of the
-// call's range [k0, k1) (batch j = timesteps k0 + j B ...), each assembled,
-// solved, recovered and written as planar V on the lane's handle and stream.
-// Host pointers: the lane's own double-buffered copy pipeline (mof_hostio.h).
-void solve_lane(mof_mesh *m, const double *I, const double *I2, const double *t_k, int32_t k0, int32_t k1,
-                int32_t B, int lane, int lanes, double lambda, const mof::SolveParams &sp, const mof_opts &o,
-                bool recovery, bool dev_io, hipStream_t s, double *V_out, mof_stats &st, mof::SpmvTiming &timing) {
+// The batches of mof_solve_range's range [k0, k1) (batch j = timesteps
+// k0 + j B ...), each assembled, solved, recovered and written as planar V
+// on stream s. Host pointers: the handle's double-buffered copy pipeline
+// (mof_hostio.h). Measured and not kept (round 4,
+// profiles/r04_ab/call1*/c3_l2_*, c3_b256_l2): two batches in flight on one
+// GPU (the batches alternating between the handle and a same-device twin on
+// their own streams and host threads) -- 3533 vs 3602 timesteps/s at B = 512
+// and 3419 vs 3463 at B = 256: the latency-bound setup kernels beside the
+// other batch's bandwidth-bound sweeps slow both.
+void solve_batches(mof_mesh *m, const double *I, const double *I2, const double *t_k, int32_t k0, int32_t k1,
+                   int32_t B, double lambda, const mof::SolveParams &sp, const mof_opts &o, bool recovery,
+                   bool dev_io, hipStream_t s, double *V_out, mof_stats &st, mof::SpmvTiming &timing) {
     const int32_t K = k1 - k0;
-    const int32_t nbat_all = (K + B - 1) / B;
-    std::vector<int32_t> js;  // this lane's batches
-    for (int32_t j = lane; j < nbat_all; j += lanes) js.push_back(j);
-    const int32_t nbat = (int32_t)js.size();
-    if (!nbat) return;
+    const int32_t nbat = (K + B - 1) / B;
     mof::ensure_workspace(m, B, sp.precision);
     mof::Workspace &w = m->ws;
     const int64_t N = m->N;
@@ -153,11 +154,11 @@ void solve_lane(mof_mesh *m, const double *I, const double *I2, const double *t_
     const bool shared_I = (I2 == I);
     const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
     if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B);
-    auto bk = [&](int32_t q) { return k0 + js[q] * B; };
+    auto bk = [&](int32_t q) { return k0 + q * B; };
     auto bn = [&](int32_t q) { return std::min(B, k1 - bk(q)); };
-    // helper-thread steps of the host pipeline (copy stream): the lane's q-th
-    // batch's I rows into slot q&1 once batch q-2's assembly has read it, and
-    // batch q's V out of slot q&1 into V_out
+    // helper-thread steps of the host pipeline (copy stream): batch q's I rows
+    // into slot q&1 once batch q-2's assembly has read it, and batch q's V
+    // out of slot q&1 into V_out
     // MOF_HOSTIO_VERBOSE: helper-thread and wait times on stderr
     const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
     double t_in = 0.0, t_out = 0.0, t_wait = 0.0;
@@ -252,16 +253,16 @@ void solve_lane(mof_mesh *m, const double *I, const double *I2, const double *t_
         st.batches++;
     }
     if (dev_io && hostio_verbose)
-        fprintf(stderr, "[mof hostio] lane %d device K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n", lane, K,
-                B, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
+        fprintf(stderr, "[mof hostio] device K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n", K, B,
+                now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
     if (!dev_io) {
         if (io.valid()) io.get();
         drain_out(nbat - 1);
         if (hostio_verbose)
             fprintf(stderr,
-                    "[mof hostio] lane %d K=%d B=%d: stage_in %.1f ms, drain %.1f ms, main waited %.1f ms, "
+                    "[mof hostio] K=%d B=%d: stage_in %.1f ms, drain %.1f ms, main waited %.1f ms, "
                     "call %.1f ms, %lld flag fetches %.1f ms\n",
-                    lane, K, B, t_in, t_out, t_wait, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
+                    K, B, t_in, t_out, t_wait, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
     }
 }
 
@@ -269,7 +270,11 @@ void solve_lane(mof_mesh *m, const double *I, const double *I2, const double *t_
 
 namespace mof {
 
-// Systems of the batch whose solve failed are re-solved alone: with 2x2
+// the fine-level smoother damping of the recovery's multigrid pass
+constexpr float kRecoverOmega = 0.6f;
+
+// Systems of the batch whose solve failed are re-solved alone: with the
+// multigrid at a smaller fine-level damping (after a multigrid solve), 2x2
 // block-Jacobi PCG in the same precision after a multigrid solve, then in
 // fp64 (no stagnation test, the full iteration budget); only what all of
 // them fail stays failed (NaN-filled by k_to_planar). An fp64 solve gets
@@ -286,9 +291,24 @@ void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, c
                      const std::function<void()> &release_f64) {
     auto failed = [&](int32_t b) { return sysi[b * kSysStride + SI_FAILED] != 0; };
     const int32_t budget = std::max(user_max_iter, 10000);  // the full budget, never less than the caller's
-    std::vector<uint32_t> passes;
-    if (sp.precision == MOF_PREC_MIXED && sp.amg) passes.push_back(MOF_PREC_MIXED);
-    if (sp.precision == MOF_PREC_MIXED || !sp.block_jacobi || sp.max_iter < budget) passes.push_back(MOF_PREC_F64);
+    // passes: {precision, multigrid}; after a multigrid solve first the same
+    // multigrid with a more strongly damped fine smoother (kRecoverOmega): a
+    // V-cycle whose damped block Jacobi is not contractive on a system (an
+    // indefinite preconditioner: breakdown after a few iterations -- round 4,
+    // the S1-like patch under an atan2 pinwheel signal, every system at
+    // omega 0.85, none at 0.7) converges in tens of iterations there, where
+    // block Jacobi takes hundreds
+    struct Pass {
+        uint32_t prec;
+        bool amg;
+    };
+    std::vector<Pass> passes;
+    if (sp.precision == MOF_PREC_MIXED && sp.amg) {
+        passes.push_back({MOF_PREC_MIXED, true});
+        passes.push_back({MOF_PREC_MIXED, false});
+    }
+    if (sp.precision == MOF_PREC_MIXED || !sp.block_jacobi || sp.max_iter < budget)
+        passes.push_back({MOF_PREC_F64, false});
     std::vector<uint8_t> first(nb, 0);
     int32_t nfirst = 0;
     for (int32_t b = 0; b < nb; ++b) nfirst += (first[b] = failed(b));
@@ -309,18 +329,23 @@ void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, c
                      why[FW_RESIDUAL], itmin, itmax);
     }
     bool used_f64 = false;
-    for (uint32_t prec : passes) {
+    for (const Pass &ps : passes) {
+        const uint32_t prec = ps.prec;
         int32_t n = 0;
         for (int32_t b = 0; b < nb; ++b) n += (only[b] = failed(b));
         if (!n) break;
         SolveParams rp = sp;
         rp.precision = prec;
-        rp.amg = false;
+        rp.amg = ps.amg;
         rp.block_jacobi = true;
-        rp.stall = 0;
-        rp.fail_at_max_iter = false;
         rp.time_spmv = false;
-        rp.max_iter = budget;
+        if (ps.amg) {  // the first solve's limits (stagnation, max_iter) stand
+            rp.amg_omega = kRecoverOmega;
+        } else {
+            rp.stall = 0;
+            rp.fail_at_max_iter = false;
+            rp.max_iter = budget;
+        }
         if (prec == MOF_PREC_F64 && sp.precision == MOF_PREC_MIXED) {
             try {
                 ensure(prec);
@@ -625,10 +650,6 @@ int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out) {
 int mof_mesh_destroy(mof_mesh *m) {
     if (!m) return MOF_OK;
     return guarded([&] {
-        if (m->twin) {
-            mof_mesh_destroy(m->twin);
-            m->twin = nullptr;
-        }
         {
             DeviceGuard dg(m->device);
             if (m->stream) (void)hipStreamSynchronize(m->stream);
@@ -792,67 +813,8 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 Bmax = (int32_t)std::max(1.0, std::min(512.0, 0.25 * (double)free_b / per_sys));
             }
             const int32_t B = std::min(K, Bmax);
-            const int32_t nbat = (K + B - 1) / B;
-            // two lanes: batches alternate between this handle and its twin
-            // (a clone on the same device: own stream, own workspace), each
-            // driven by its own host thread, so one batch's latency-bound
-            // setup kernels (assembly, fp64 residuals, Galerkin products) run
-            // beside the other's bandwidth-bound iterations. Batch
-            // composition is unchanged, so V is bit-identical to one lane.
-            // Not with a caller stream (the lanes' streams are the handles').
-            const int lanes = ((o.flags & MOF_TWO_LANES) && !o.stream && nbat >= 2) ? 2 : 1;
-            if (lanes == 2 && !m->twin) {
-                mof_mesh *t = nullptr;
-                const int rc2 = mof_mesh_clone(m, m->device, &t);
-                if (rc2 != MOF_OK) throw mof::Error{rc2, "second lane: " + g_err};
-                m->twin = t;
-            }
-            mof::SolveParams sp_l = sp;
-            std::vector<mof_stats> lst(lanes);
-            std::vector<mof::SpmvTiming> ltm(lanes);
-            std::vector<std::string> lerr(lanes);
-            std::vector<int> lrc(lanes, MOF_OK);
-            auto lane = [&](int l) {
-                lrc[l] = guarded([&] {
-                    mof_mesh *L = l == 0 ? m : m->twin;
-                    MOF_HIP(hipSetDevice(L->device));
-                    hipStream_t ls = (l == 0 && o.stream) ? (hipStream_t)o.stream : L->stream;
-                    solve_lane(L, I, I2, t_k, k0, k1, B, l, lanes, lambda, sp_l, o, recovery, dev_io, ls, V_out,
-                               lst[l], ltm[l]);
-                });
-                if (lrc[l] != MOF_OK) lerr[l] = g_err;
-            };
-            if (lanes == 1) {
-                lane(0);
-            } else {
-                auto f1 = std::async(std::launch::async, [&] { lane(1); });
-                lane(0);
-                f1.get();
-            }
-            for (int l = 0; l < lanes; ++l)
-                if (lrc[l] != MOF_OK) throw mof::Error{lrc[l], lerr[l]};
-            for (int l = 0; l < lanes; ++l) {
-                const mof_stats &a = lst[l];
-                st.iterations += a.iterations;
-                st.max_iterations = std::max(st.max_iterations, a.max_iterations);
-                st.failed += a.failed;
-                st.outer_steps = std::max(st.outer_steps, a.outer_steps);
-                st.batches += a.batches;
-                st.max_rel_residual = std::max(st.max_rel_residual, a.max_rel_residual);
-                st.ms_assembly += a.ms_assembly;
-                st.ms_solve += a.ms_solve;
-                st.recovered += a.recovered;
-                st.recovered_f64 += a.recovered_f64;
-                const mof::SpmvTiming &t = ltm[l];
-                timing.launches += t.launches;
-                timing.systems += t.systems;
-                timing.full_launches += t.full_launches;
-                timing.ms += t.ms;
-                timing.bytes += t.bytes;
-                timing.ms_full += t.ms_full;
-                timing.fused_launches += t.fused_launches;
-                timing.ms_fused += t.ms_fused;
-            }
+            hipStream_t s = o.stream ? (hipStream_t)o.stream : m->stream;
+            solve_batches(m, I, I2, t_k, k0, k1, B, lambda, sp, o, recovery, dev_io, s, V_out, st, timing);
         }
         st.systems = K;
         st.spmv_launches = timing.launches;

@@ -1709,6 +1709,13 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
 
 void amg_destroy(AmgDevice *g) { delete g; }
 
+float amg_set_omega(mof_mesh *m, float omega) {
+    if (!m->amg) return 0.f;
+    const float old = m->amg->omega;
+    m->amg->omega = omega;
+    return old;
+}
+
 int32_t amg_levels(const mof_mesh *m) { return m->amg && m->amg->built ? (int32_t)m->amg->lv.size() : 0; }
 
 }  // namespace mof

@@ -167,34 +167,6 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
     }
 }
 
-// lambda L_ij per SELL slot of row i, L_ij = sum over the triangles of edge
-// (i, j) (the diagonal: of vertex i) of A_T (grad w_a . grad w_b): a2's 2x2
-// block (i, j) is (e_i^alpha . e_j^beta) L_ij (compute_a2 :258-270 with e
-// independent of the triangle), so lambda a2 x = E_i sum_j lambda L_ij X_j,
-// X_j = E_j^T x_j -- the form the re-forming residual applies
-// (mof_pcg.hip k_residual_x3). Not bit-exact to anything: the residual only
-// needs an fp64-accurate operator.
-__global__ __launch_bounds__(kWG) void k_lap(int32_t N, const int32_t *__restrict__ vptr,
-                                             const int32_t *__restrict__ vcol, const int32_t *__restrict__ cptr,
-                                             const int32_t *__restrict__ clist, const int32_t *__restrict__ sell_off,
-                                             const double *__restrict__ gw, const double *__restrict__ area,
-                                             double lambda, double *__restrict__ lap) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
-    if (i >= N) return;
-    int32_t td = 0;
-    while (vcol[vptr[i] + td] != i) ++td;
-    for (int32_t p = vptr[i], t = 0; p < vptr[i + 1]; ++p, ++t) {
-        double acc = 0.0;
-        for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
-            const int32_t code = clist[c];
-            const int32_t T = code / 9, a = (code % 9) / 3, b = code % 3;
-            const double *g = gw + 9 * (int64_t)T;
-            acc += dot64(g + 3 * a, g + 3 * b) * area[T];
-        }
-        lap[sell_pos(sell_off, i, sell_slot(t, td))] = lambda * acc;
-    }
-}
-
 // Per-triangle half of worker (:113-126, compute_f :288-311) for B systems:
 // grad_M I and, for each corner a and alpha, u = grad_M I . e_a^alpha and the
 // f term (u (2 dI_a + sum of the other distinct corners' dI) A_T) / 12.
@@ -514,7 +486,7 @@ __device__ __forceinline__ void rows_store(const float (&acc)[WMAX][4], double f
 // Mixed-precision assembly by vertex rows (the PCG row layout and XCD-aware
 // (row block, system) order). Thread i walks the incident triangles of
 // vertex i in the caller's triangle order (tinc, SELL-64) and, per
-// triangle, forms grad_M I, u = grad_M I . e at (i, v_{a+1}, v_{a+2}) and
+// triangle, forms grad_M I, u = grad_M I . e_i and
 // row i's f term in k_tri_step's exact arithmetic (the I0 values in the
 // triangle's own corner order, np.dot's fma chain, the f term's operation
 // order), then adds the
@@ -537,7 +509,9 @@ struct TriGeo {
 // outer product per incident triangle into its slots' G (6 floats each) and
 // projects each stored slot once at the end -- no tangent frames of the two
 // other corners gathered per incidence and no u_j, u_k dots (A32 is an fp32
-// fold of the same operator, rounded differently; f keeps its bits).
+// fold of the same operator, rounded differently; f keeps its bits). C3,
+// B = 512, rocprof on one box (profiles/r04_ab/call1b/): 9047-9163 -> 8630 us
+// per launch against the round-3 per-incidence 2x2 fold.
 // g3_store: the slots' blocks E_i G E_j^T + lambda a2, then rows_store's stores.
 template <int WMAX>
 __device__ __forceinline__ void g3_project(const float (&G)[WMAX][6], const double (&ei)[6], int32_t deg, int64_t o,
@@ -573,7 +547,7 @@ __device__ __forceinline__ void g3_project(const float (&G)[WMAX][6], const doub
                 acc[z][2 * al + be] = eif[3 * al] * H[0][be] + eif[3 * al + 1] * H[1][be] + eif[3 * al + 2] * H[2][be];
     }
 }
-template <int WMAX, bool G3 = false>
+template <int WMAX>
 __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
@@ -590,14 +564,12 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
         if (i >= N) break;
         const int32_t s = i >> 6, l = i & 63;
         float acc[WMAX][4];
-        float G[G3 ? WMAX : 1][6];
+        float G[WMAX][6];  // the slots' 3x3 a1 sums (symmetric: xx xy xz yy yz zz)
         double ei[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) ei[k] = geo.e[6 * (int64_t)i + k];
 #pragma unroll
-        for (int z = 0; z < WMAX; ++z) acc[z][0] = acc[z][1] = acc[z][2] = acc[z][3] = 0.f;
-#pragma unroll
-        for (int z = 0; z < (G3 ? WMAX : 1); ++z)
+        for (int z = 0; z < WMAX; ++z)
 #pragma unroll
             for (int x = 0; x < 6; ++x) G[z][x] = 0.f;
         double f0 = 0.0, f1 = 0.0;
@@ -610,16 +582,9 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
             const bool real = q.x < M;  // padding (T = M): weight 0, no f term
             const int64_t T = min(q.x, M - 1);
             const int32_t c = q.y, vj = q.z, vk = q.w;
-            double g[9], ej[6], ek[6];
+            double g[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) g[k] = geo.gw[9 * T + k];
-            if constexpr (!G3) {
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    ej[k] = geo.e[6 * (int64_t)vj + k];
-                    ek[k] = geo.e[6 * (int64_t)vk + k];
-                }
-            }
             const double At = geo.area[T];
             const float wv = w12[q.x];
             const int32_t sj = sl & 0xff, sk = sl >> 8;
@@ -640,40 +605,21 @@ __global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
                 f0 += ui0 * (2 * pdi + po) * At / 12;
                 f1 += ui1 * (2 * pdi + po) * At / 12;
             }
-            // the a1 terms (u_i^a u_j^b) w (compute_a1's association) in fp32;
-            // a term on the diagonal block takes A/6 = 2 A/12 (a degenerate
-            // triangle's second corner at i included)
+            // the a1 terms (compute_a1's (u_i^a u_j^b) w) as one outer product
+            // of grad_M I per incidence, weighted per slot: A/6 = 2 A/12 on the
+            // diagonal block (a degenerate triangle's second corner at i
+            // included), A/12 on the blocks of the other two corners
             const float wd = wv + wv, wj = sj == 0 ? wd : wv, wk = sk == 0 ? wd : wv;
-            if constexpr (G3) {
-                const float gx = (float)gI[0], gy = (float)gI[1], gz = (float)gI[2];
-                const float op[6] = {gx * gx, gx * gy, gx * gz, gy * gy, gy * gz, gz * gz};
-#pragma unroll
-                for (int z = 0; z < WMAX; ++z) {
-                    const float cz = (z == 0 ? wd : 0.f) + (z == sj ? wj : 0.f) + (z == sk ? wk : 0.f);
-#pragma unroll
-                    for (int x = 0; x < 6; ++x) G[z][x] = __builtin_fmaf(cz, op[x], G[z][x]);
-                }
-                continue;
-            }
-            const float ui[2] = {(float)ui0, (float)ui1};
-            const float uj[2] = {(float)dot64(gI, ej), (float)dot64(gI, ej + 3)};
-            const float uk[2] = {(float)dot64(gI, ek), (float)dot64(gI, ek + 3)};
-            const float d4[4] = {ui[0] * ui[0] * wd, ui[0] * ui[1] * wd, ui[1] * ui[0] * wd, ui[1] * ui[1] * wd};
-            const float cj[4] = {ui[0] * uj[0] * wj, ui[0] * uj[1] * wj, ui[1] * uj[0] * wj, ui[1] * uj[1] * wj};
-            const float ck[4] = {ui[0] * uk[0] * wk, ui[0] * uk[1] * wk, ui[1] * uk[0] * wk, ui[1] * uk[1] * wk};
+            const float gx = (float)gI[0], gy = (float)gI[1], gz = (float)gI[2];
+            const float op[6] = {gx * gx, gx * gy, gx * gz, gy * gy, gy * gz, gz * gz};
 #pragma unroll
             for (int z = 0; z < WMAX; ++z) {
-                const float mj = z == sj ? 1.f : 0.f, mk = z == sk ? 1.f : 0.f;
+                const float cz = (z == 0 ? wd : 0.f) + (z == sj ? wj : 0.f) + (z == sk ? wk : 0.f);
 #pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    float a = z == 0 ? acc[z][x] + d4[x] : acc[z][x];
-                    a = __builtin_fmaf(mj, cj[x], a);
-                    acc[z][x] = __builtin_fmaf(mk, ck[x], a);
-                }
+                for (int x = 0; x < 6; ++x) G[z][x] = __builtin_fmaf(cz, op[x], G[z][x]);
             }
         }
-        if constexpr (G3)
-            g3_project<WMAX>(G, ei, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_col, geo.e, mir, acc);
+        g3_project<WMAX>(G, ei, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_col, geo.e, mir, acc);
         rows_store<WMAX>(acc, f0, f1, i, b, N, vptr[i + 1] - vptr[i], sell_off[s] + l, sell_nb, sell_col, a2s,
                          block_jacobi, A, dinv32, rhs, Ah, nown, mir);
     }
@@ -871,10 +817,6 @@ void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
     if (m->a2s_valid && m->a2s_lambda == lambda) return;
     const int64_t n = 4 * m->pat.sell_nb();
     k_scale_a2<<<grid1(n), kWG, 0, s>>>(n, lambda, m->a2.p, m->a2s64.p, m->a2s32.p);
-    if (m->lap64.n < (size_t)(n / 4)) m->lap64.alloc((size_t)(n / 4));
-    m->lap64.zero(s);  // SELL padding stays 0
-    k_lap<<<grid1(m->N), kWG, 0, s>>>(m->N, m->vptr.p, m->vcol.p, m->cptr.p, m->clist.p, m->sell_off.p, m->gw.p,
-                                      m->area.p, lambda, m->lap64.p);
     MOF_HIP(hipGetLastError());
     m->a2s_lambda = lambda;
     m->a2s_valid = true;
@@ -976,13 +918,8 @@ void launch_assemble(mof_mesh *m, int32_t B, const double *I0, const double *I1,
     if (amg && precision == MOF_PREC_MIXED) bf = amg_bf16_targets(m, B);
     const int32_t nblk_rows = (int32_t)((m->N + kRowsPerWG - 1) / kRowsPerWG);
     const int32_t *mirw = m->sym_reads ? m->sell_mir.p : nullptr;
-    // the a1 fold in ambient 3-D (k_assemble_rows_rc<., true>); MOF_ASM_G3=0/1
-    // forces either (A/B switch, read per batch)
-    constexpr bool kAsmG3 = false;
-    const char *g3e = std::getenv("MOF_ASM_G3");
-    const bool g3 = g3e && *g3e ? std::atoi(g3e) != 0 : kAsmG3;
 #define MOF_ASM_RC_LAUNCH(WM)                                                                                     \
-    (g3 ? k_assemble_rows_rc<WM, true> : k_assemble_rows_rc<WM, false>)<<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>( \
+    k_assemble_rows_rc<WM><<<xcd_grid(nblk_rows, B, kGrpAsm), kWG, 0, s>>>(                                        \
         m->N, m->M, nblk_rows, B, snb, m->sell_off.p, m->sell_col.p, m->vptr.p, m->tsell_off.p,                    \
         reinterpret_cast<const int4 *>(m->tinc.p), m->tslot.p, m->w12_32.p, m->a2s32.p, bj, w.A32.p, w.dinv32.p,   \
         w.rhs.p, bf.A0h, m->n_own, mirw, geo)

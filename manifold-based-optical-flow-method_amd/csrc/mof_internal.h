@@ -137,7 +137,6 @@ struct Workspace {
     DevArray<float> dinv32;
     DevArray<double> rhs;              // [B][N][2] f (interleaved)
     DevArray<double> x64, r64;         // [B][N][2] outer solution / residual
-    DevArray<double> X64;              // [B][N][4] x64 in ambient 3-D, E^T x (k_residual_x3), on first use
     DevArray<double> vx, vr, vz, vp, vq;  // [B][N][2] inner PCG vectors (fp64 sized)
     DevArray<double> part_pq;          // [B][nblk]
     DevArray<double> part_rzrr;        // [2][B][nblk][2]
@@ -235,10 +234,6 @@ struct mof_mesh {
     // operator copies: lambda*a2 (cached per lambda) and A_T/12 with a zero slot M
     mof::DevArray<double> a2s64, w12_64;
     mof::DevArray<float> a2s32, w12_32;
-    // lambda x the scalar Laplacian L_ij = sum_T A_T (grad w_i . grad w_j) per
-    // SELL slot (a2's block (i, j) is (e_i^a . e_j^b) L_ij): the re-forming
-    // fp64 residual's 3-D form (k_residual_x3)
-    mof::DevArray<double> lap64;
     double a2s_lambda = 0.0;
     bool a2s_valid = false;
     // mof_assemble / mof_csr_export(MOF_CSR_A_LAST): one assembled A (SELL) and f
@@ -265,10 +260,6 @@ struct mof_mesh {
     // host state shared with the clones of this mesh on other devices
     std::shared_ptr<mof::MeshShared> shared;
     hipEvent_t hev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    // the second lane of a two-lane solve (mof_solve_range, MOF_TWO_LANES): a
-    // clone of this mesh on the same device with its own stream and
-    // workspace, created on first use, destroyed with this handle
-    mof_mesh *twin = nullptr;
 };
 
 namespace mof {
@@ -341,6 +332,9 @@ struct SolveParams {
     // (k_solve_fused): 0 never, 1 when the batch is eligible, -1 auto (small
     // meshes: row blocks <= MOF_FUSED_MAX_BLK)
     int32_t fused = -1;
+    // > 0: the multigrid's fine-level smoother damping for this solve instead
+    // of the hierarchy's (the recovery's damped multigrid pass)
+    float amg_omega = 0.f;
 };
 // Solve the B assembled systems in the workspace; fills sysd/sysi.
 // Returns total inner iterations; sets *outer to the refinement steps used.
@@ -391,6 +385,9 @@ AmgBf16 amg_bf16_targets(mof_mesh *m, int32_t B);
 void amg_destroy(AmgDevice *g);
 
 int32_t amg_levels(const mof_mesh *m);
+// set the fine-level smoother damping of m's multigrid cycle; returns the
+// previous value (0 and no change when m has no hierarchy)
+float amg_set_omega(mof_mesh *m, float omega);
 
 // every (row block, system) pair of the XCD order (mof_rowkern.h) visited once
 bool xcd_map_covers(int32_t nblk, int32_t B, int32_t grp);

@@ -39,7 +39,6 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
 #include <chrono>
 #include <cmath>
 
@@ -747,20 +746,10 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
 }
 
 // x64 (+)= x_inner for systems active in the inner solve.
-// X = E^T x of vertex i (ambient 3-D; the re-forming residual's operand),
-// a 32-B record {X0, X1, X2, 0}; explicit fma: the same bits in every slot
-__device__ __forceinline__ void st_x3(double *__restrict__ X3, int64_t vi, const double *__restrict__ ei, double x0,
-                                      double x1) {
-    double2 *o = reinterpret_cast<double2 *>(X3 + 4 * vi);
-    o[0] = make_double2(fma(ei[3], x1, ei[0] * x0), fma(ei[4], x1, ei[1] * x0));
-    o[1] = make_double2(fma(ei[5], x1, ei[2] * x0), 0.0);
-}
-
 template <typename V>
 __device__ __forceinline__ void outer_update_rows(int32_t N, int32_t first, const V *__restrict__ xin,
                                                   const int32_t *__restrict__ sysi, double *__restrict__ x64,
-                                                  int32_t blk, int32_t b, const double *__restrict__ e = nullptr,
-                                                  double *__restrict__ X3 = nullptr) {
+                                                  int32_t blk, int32_t b) {
     if (!sysi[b * kSysStride + SI_ACTIVE]) return;
     const int32_t i = blk * kWG + row_tid();
     if (i >= N) return;
@@ -771,31 +760,11 @@ __device__ __forceinline__ void outer_update_rows(int32_t N, int32_t first, cons
     x.x += (double)d.x;
     x.y += (double)d.y;
     *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
-    if (X3) {
-        double ei[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ei[q] = e[6 * (int64_t)i + q];
-        st_x3(X3, vi, ei, x.x, x.y);
-    }
 }
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first, const V *__restrict__ xin,
-                                                      const int32_t *__restrict__ sysi, double *__restrict__ x64,
-                                                      const double *__restrict__ e, double *__restrict__ X3) {
-    outer_update_rows<V>(N, first, xin, sysi, x64, blockIdx.x, blockIdx.y, e, X3);
-}
-// X = E^T x64 for every row (decomposed parts: after the x64 halo)
-__global__ __launch_bounds__(kWG) void k_make_x3(int32_t N, const double *__restrict__ x64,
-                                                 const int32_t *__restrict__ sysi, const double *__restrict__ e,
-                                                 double *__restrict__ X3) {
-    const int32_t b = blockIdx.y, i = blockIdx.x * kWG + threadIdx.x;
-    if (i >= N || !sysi[b * kSysStride + SI_ACTIVE]) return;
-    const int64_t vi = (int64_t)b * N + i;
-    const double2 x = *reinterpret_cast<const double2 *>(x64 + 2 * vi);
-    double ei[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) ei[q] = e[6 * (int64_t)i + q];
-    st_x3(X3, vi, ei, x.x, x.y);
+                                                      const int32_t *__restrict__ sysi, double *__restrict__ x64) {
+    outer_update_rows<V>(N, first, xin, sysi, x64, blockIdx.x, blockIdx.y);
 }
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
@@ -883,159 +852,6 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t
         if (i >= N) break;
         double y[NS][2];
         apply_row_rcn<NS>(op, bs, i, x64, y);
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const int64_t vi = (int64_t)bs[t] * N + i;
-            const double2 f = *reinterpret_cast<const double2 *>(rhs + 2 * vi);
-            const double r0 = f.x - y[t][0], r1 = f.y - y[t][1];
-            if (act[t]) *reinterpret_cast<double2 *>(r64 + 2 * vi) = make_double2(r0, r1);
-            if (i < rd.nown) {
-                v[2 * t] += r0 * r0 + r1 * r1;
-                v[2 * t + 1] += f.x * f.x + f.y * f.y;
-            }
-        }
-    }
-    block_sum<2 * NS>(v, lds);
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            if (!act[t]) continue;
-            double *o = part + 2 * red_rec(rd, B, bs[t], rb);
-            o[0] = v[2 * t];
-            o[1] = v[2 * t + 1];
-        }
-    }
-}
-
-// The re-forming residual in ambient 3-D (round 4): a1 restricted to a
-// triangle is u u^T (x) [A/6, A/12] with u_v = E_v grad I_T, and a2's block
-// (i, j) is (e_i . e_j) L_ij, so with X_v = E_v^T x_v (3-D, k_outer_update)
-//   (A x)_i = E_i [ sum_j lambda L_ij X_j + sum_{T ni i} (A_T/12) (gI_T . Y_T) gI_T ],
-//   Y_T = 2 X_i + X_j + X_k
-// -- the same operator as apply_row_rcn's (compute_optical_flow.py:127-146),
-// with one 3-vector dot per incident triangle instead of six tangent-frame
-// dots, no gathered tangent frames, and one lambda L scalar per slot instead
-// of a 2x2 a2 block. Explicit fma / no contraction: every system slot rounds
-// alike (a system's bits do not depend on the batch split).
-constexpr int kLapU = 4;
-template <int NS>
-__device__ __forceinline__ void apply_row_x3(const OpArgs<double> &op, const double *__restrict__ lap,
-                                             const int32_t (&bs)[NS], int32_t i, const double *__restrict__ X3,
-                                             double (&y)[NS][2]) {
-#pragma clang fp contract(off)
-    const int32_t s = i >> 6, l = i & 63;
-    double acc[NS][3];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = acc[t][2] = 0.0;
-    auto ldX = [&](int t, int32_t v, double (&x)[3]) {
-        const double2 *p = reinterpret_cast<const double2 *>(X3 + 4 * ((int64_t)bs[t] * op.N + v));
-        const double2 a = p[0], c = p[1];
-        x[0] = a.x;
-        x[1] = a.y;
-        x[2] = c.x;
-    };
-    {  // lambda L X over the row's slots (padding slots hold L = 0)
-        const int32_t o = op.sell_off[s];
-        const int32_t w = (op.sell_off[s + 1] - o) >> 6;
-        for (int32_t t0 = 0; t0 < w; t0 += kLapU) {
-            int32_t j[kLapU];
-            double L[kLapU];
-#pragma unroll
-            for (int u = 0; u < kLapU; ++u) {
-                const int64_t pos = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
-                j[u] = op.sell_col[pos];
-                L[u] = t0 + u < w ? lap[pos] : 0.0;
-            }
-            double xj[kLapU][NS][3];
-#pragma unroll
-            for (int u = 0; u < kLapU; ++u)
-#pragma unroll
-                for (int t = 0; t < NS; ++t) ldX(t, j[u], xj[u][t]);
-#pragma unroll
-            for (int u = 0; u < kLapU; ++u)
-#pragma unroll
-                for (int t = 0; t < NS; ++t)
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) acc[t][d] = fma(L[u], xj[u][t][d], acc[t][d]);
-        }
-    }
-    double Xi[NS][3], Ii[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        ldX(t, i, Xi[t]);
-        Ii[t] = op.I0[(int64_t)bs[t] * op.ldI + i];
-    }
-    const int32_t o = op.tsell_off[s];
-    const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
-    for (int32_t t0 = 0; t0 < w; ++t0) {
-        const int4 q = op.tinc[(int64_t)o + t0 * kSlice + l];
-        const int64_t T = min(q.x, op.M - 1);  // padding entries (T = M) have weight 0
-        double g[9], Ij[NS], Ik[NS], xj[NS][3], xk[NS][3];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) g[k] = op.gw[9 * T + k];
-        const double wt = op.w12[q.x];
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const double *Ib = op.I0 + (int64_t)bs[t] * op.ldI;
-            Ij[t] = Ib[q.z];
-            Ik[t] = Ib[q.w];
-            ldX(t, q.z, xj[t]);
-            ldX(t, q.w, xk[t]);
-        }
-        const int c = q.y;
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const double c0 = c == 0 ? Ii[t] : (c == 1 ? Ik[t] : Ij[t]);
-            const double c1 = c == 0 ? Ij[t] : (c == 1 ? Ii[t] : Ik[t]);
-            const double c2 = c == 0 ? Ik[t] : (c == 1 ? Ij[t] : Ii[t]);
-            double gI[3], Y[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                gI[d] = fma(c2, g[6 + d], fma(c1, g[3 + d], c0 * g[d]));
-                Y[d] = ((Xi[t][d] + Xi[t][d]) + xj[t][d]) + xk[t][d];
-            }
-            const double dd = wt * fma(gI[2], Y[2], fma(gI[1], Y[1], gI[0] * Y[0]));
-#pragma unroll
-            for (int d = 0; d < 3; ++d) acc[t][d] = fma(dd, gI[d], acc[t][d]);
-        }
-    }
-    double ei[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) ei[q] = op.e[6 * (int64_t)i + q];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        y[t][0] = fma(ei[2], acc[t][2], fma(ei[1], acc[t][1], ei[0] * acc[t][0]));
-        y[t][1] = fma(ei[5], acc[t][2], fma(ei[4], acc[t][1], ei[3] * acc[t][0]));
-    }
-}
-
-template <int NS>
-__global__ __launch_bounds__(kWG) void k_residual_x3(OpArgs<double> op, const double *__restrict__ lap, int32_t nblk,
-                                                     int32_t B, RedArgs rd, const double *__restrict__ rhs,
-                                                     const double *__restrict__ X3, const int32_t *__restrict__ sysi,
-                                                     double *__restrict__ r64, double *__restrict__ part) {
-    __shared__ double lds[8 * NS];
-    int32_t rb, bp;
-    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bp, kGrpRes)) return;
-    int32_t bs[NS];
-    bool act[NS], any = false;
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        bs[t] = min(NS * bp + t, B - 1);
-        act[t] = NS * bp + t < B && sysi[bs[t] * kSysStride + SI_ACTIVE] != 0;
-        any |= act[t];
-    }
-    if (!any) return;
-    const int32_t N = op.N;
-    double v[2 * NS];
-#pragma unroll
-    for (int t = 0; t < 2 * NS; ++t) v[t] = 0.0;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
-        if (i >= N) break;
-        double y[NS][2];
-        apply_row_x3<NS>(op, lap, bs, i, X3, y);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
             const int64_t vi = (int64_t)bs[t] * N + i;
@@ -1168,39 +984,14 @@ MatArgs<V> make_mat(mof_mesh *m, const V *A) {
 // -- the residuals went 2 x 5.7 -> 2 x 3.6 ms per 512-system batch, the
 // assembly 11.4 -> 15.6 ms (fp64 accumulators: 165 VGPRs, 3 waves, and
 // 10.7 GB of A64 stores): C3 3380-3383 vs 3378-3389 timesteps/s.
-// MOF_RESIDUAL=rcn: the tangent-frame re-forming residual (k_residual_rcn)
-// instead of the 3-D one (k_residual_x3); A/B switch
-bool residual_x3() {
-    static const bool x3 = [] {
-        const char *v = std::getenv("MOF_RESIDUAL");
-        return !(v && std::strcmp(v, "rcn") == 0);
-    }();
-    return x3;
-}
-// X64 of the batch's systems (the 3-D residual's operand), on first use
-double *x3_buffer(mof_mesh *m) {
-    Workspace &w = m->ws;
-    const size_t n = 4 * (size_t)m->N * std::max(w.cap, 1);
-    if (w.X64.n < n) w.X64.alloc(n);
-    return w.X64.p;
-}
-// x3_fresh: k_outer_update has just written X64 from this x64
-void launch_residual(mof_mesh *m, int32_t nblk, int32_t B, hipStream_t s, RedArgs rd, const double *rhs,
-                     const double *x64, const int32_t *sysi, double *r64, double *part, bool x3_fresh) {
+template <typename... Args>
+void launch_residual(mof_mesh *m, int32_t nblk, int32_t B, hipStream_t s, RedArgs rd, Args... args) {
     const OpArgs<double> op = op64(m);
-    if (op.u) {
-        k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, rhs, x64, sysi, r64, part);
-    } else if (residual_x3()) {
-        double *X3 = x3_buffer(m);
-        if (!x3_fresh)
-            k_make_x3<<<dim3((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B), kWG, 0, s>>>(m->N, x64, sysi, m->e.p,
-                                                                                          X3);
-        k_residual_x3<kResNS><<<dim3(xcd_grid(nblk, (B + kResNS - 1) / kResNS, kGrpRes)), kWG, 0, s>>>(
-            op, m->lap64.p, nblk, B, rd, rhs, X3, sysi, r64, part);
-    } else {
+    if (op.u)
+        k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
+    else
         k_residual_rcn<kResNS><<<dim3(xcd_grid(nblk, (B + kResNS - 1) / kResNS, kGrpRes)), kWG, 0, s>>>(
-            op, nblk, B, rd, rhs, x64, sysi, r64, part);
-    }
+            op, nblk, B, rd, args...);
 }
 
 template <typename V>
@@ -1684,16 +1475,28 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && amg_build(m);
     if (amg) {
         amg_ensure(m, B);
-        amg_setup_batch(m, B, s);
+        // a recovery pass (only) re-solves systems of this batch, whose
+        // coarse operators are still in place
+        if (!only) amg_setup_batch(m, B, s);
     }
+    // the recovery's damped pass: its smoother damping for this solve only
+    struct OmegaScope {
+        mof_mesh *m;
+        float old = 0.f;
+        bool on;
+        OmegaScope(mof_mesh *mm, float om, bool use) : m(mm), on(use && om > 0.f) {
+            if (on) old = amg_set_omega(m, om);
+        }
+        ~OmegaScope() {
+            if (on) amg_set_omega(m, old);
+        }
+    } omega_scope(m, sp.amg_omega, amg);
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
     int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
     // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
     static const bool verbose = std::getenv("MOF_SOLVE_VERBOSE") != nullptr;
-    // the 3-D residual's operand X64 comes out of the x64 update
-    double *X3 = (!op64(m).u && residual_x3()) ? x3_buffer(m) : nullptr;
     for (; o < sp.max_outer; ++o) {
         const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
         if (sp.precision == MOF_PREC_MIXED) {
@@ -1702,15 +1505,16 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
                                 max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg,
                                 o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
             k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                    w.sysi.p, w.x64.p, m->e.p, X3);
+                                                    w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
                                  &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
-            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p, m->e.p, X3);
+            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
-        launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p, X3 != nullptr);
+        launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
+                                                              w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
         MOF_HIP(hipGetLastError());
@@ -1904,8 +1708,20 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
     if (amg)
         for (size_t l = 0; l < L; ++l) {
             amg_ensure(d->parts[l], B);
-            amg_setup_batch(d->parts[l], B, s);
+            if (!only) amg_setup_batch(d->parts[l], B, s);  // a recovery pass: still in place
         }
+    // the recovery's damped pass: every part's smoother damping for this solve
+    std::vector<float> om_old(L, 0.f);
+    const bool om_set = amg && sp.amg_omega > 0.f;
+    if (om_set)
+        for (size_t l = 0; l < L; ++l) om_old[l] = amg_set_omega(d->parts[l], sp.amg_omega);
+    struct Restore {
+        std::function<void()> f;
+        ~Restore() { f(); }
+    } restore{[&] {
+        if (om_set)
+            for (size_t l = 0; l < L; ++l) amg_set_omega(d->parts[l], om_old[l]);
+    }};
     int64_t iters = 0;
     int32_t o = 0;
     for (; o < sp.max_outer; ++o) {
@@ -1921,17 +1737,17 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
             dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
             if (sp.precision == MOF_PREC_MIXED)
                 k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                        w.sysi.p, w.x64.p, nullptr, nullptr);
+                                                        w.sysi.p, w.x64.p);
             else
-                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p, nullptr, nullptr);
+                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         dd_halo(d, B, false, 1, s);  // the residual reads x64 at the ghosts
         for (size_t l = 0; l < L; ++l) {
             mof_mesh *m = d->parts[l];
             Workspace &w = m->ws;
             const RedArgs rd{d->P, d->part_ids[l], d->nmax, d->plan.parts[d->part_ids[l]].n_own};
-            // X64 (3-D residual) from the x64 the halo has just completed
-            launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, d->part_rr0.p, false);
+            launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p,
+                                                                  w.sysi.p, w.r64.p, d->part_rr0.p);
         }
         dd_sync_partials(d, d->part_rr0.p, 2 * (int64_t)B * d->nmax, s);
         for (size_t l = 0; l < L; ++l) {

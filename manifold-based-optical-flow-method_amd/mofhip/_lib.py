@@ -39,7 +39,6 @@ MOF_PRECOND_AMG = 8
 MOF_NO_RECOVERY = 16
 MOF_SOLVE_FUSED = 128
 MOF_SOLVE_EAGER = 256
-MOF_TWO_LANES = 512
 MOF_CSV_ROUND_TRIP = 1
 MOF_COORDS_F32 = 32
 MOF_DD_STAGED = 64

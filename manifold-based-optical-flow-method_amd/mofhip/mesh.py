@@ -190,14 +190,13 @@ class DeviceMesh:
     @staticmethod
     def make_opts(precision="f64", batch=0, rtol=0.0, inner_rtol=0.0, max_iter=0, max_outer=0,
                   block_jacobi=True, device_io=False, time_spmv=False, stream=None,
-                  precond="jacobi", recovery=True, fused=None, lanes=1) -> L.MofOpts:
+                  precond="jacobi", recovery=True, fused=None) -> L.MofOpts:
         """precond: "jacobi" (2x2 block Jacobi) or "amg" (aggregation-multigrid
         V-cycle; precision="mixed" only). recovery=False: a failed system is
         NaN-filled at once (MOF_NO_RECOVERY) instead of re-solved with block
         Jacobi and then fp64. fused (precision="f64"): True -- each batch's
         solve in one launch (MOF_SOLVE_FUSED), False -- never, None -- the
-        library's choice (small meshes). lanes=2: two batches in flight on the
-        device (MOF_TWO_LANES)."""
+        library's choice (small meshes)."""
         o = L.MofOpts()
         o.struct_size = ctypes.sizeof(L.MofOpts)
         o.precision = {"f64": L.MOF_PREC_F64, "mixed": L.MOF_PREC_MIXED}[precision]
@@ -206,8 +205,7 @@ class DeviceMesh:
                    | (L.MOF_TIME_SPMV if time_spmv else 0)
                    | {"jacobi": 0, "amg": L.MOF_PRECOND_AMG}[precond]
                    | (0 if recovery else L.MOF_NO_RECOVERY)
-                   | {None: 0, True: L.MOF_SOLVE_FUSED, False: L.MOF_SOLVE_EAGER}[fused]
-                   | (L.MOF_TWO_LANES if int(lanes) >= 2 else 0))
+                   | {None: 0, True: L.MOF_SOLVE_FUSED, False: L.MOF_SOLVE_EAGER}[fused])
         o.batch = int(batch)
         o.max_iter = int(max_iter)
         o.max_outer = int(max_outer)

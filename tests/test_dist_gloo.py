@@ -186,11 +186,3 @@ def test_host_transport_failure_reaches_every_rank():
     assert res[1][4] == bytes([1] * 16)  # rank 1 received rank 0's segment
     assert res[0][4] == bytes(16)  # rank 0 received the placeholder
 
-
-def test_bench_two_lanes_one_call():
-    """--lanes 2: the timed region is one library call over all timed batches
-    (the lanes alternate batches inside it); the counts are unchanged."""
-    line = _bench_dry("--gpus", "2", "--steps", "3", "--warmup", "1", "--config", "C2", "--batch", "8",
-                      "--no-cpu-baseline", "--lanes", "2")
-    assert line["config"]["timesteps_timed"] == 2 * 3 * 8
-    assert [r[2] for r in line["rank_ranges"]] == [24, 24]

@@ -94,8 +94,9 @@ def test_spmv_accounting_systems_equal_iterations(precision, precond, sym, monke
     T = 40
     I = synth.travelling_wave(g["coordinates"], T)
     m = DeviceMesh(g["coordinates"], g["normals"], g["triangles"], g["areas"])
+    # the eager launches (on this small mesh the f64 solve is fused by default)
     _, st = m.solve_range(I, np.arange(float(T)), 0, T - 1, 0.01, precision=precision, precond=precond,
-                          batch=16, time_spmv=True)
+                          batch=16, time_spmv=True, fused=False)
     assert st["failed"] == 0
     assert st["spmv_systems"] == st["iterations"]
     assert st["spmv_launches"] >= st["max_iterations"]
@@ -284,28 +285,24 @@ def test_f64_without_block_jacobi_recovers():
     assert np.abs(V - g["V_k"][:4]).max() < VTOL
 
 
-def test_assembly_g3_fold_matches_spsolve(monkeypatch):
-    """The row assembly's a1 fold in ambient 3-D (MOF_ASM_G3=1: E_i G E_j^T
-    per slot, round 4) assembles the same operator up to fp32 rounding: V
-    within the north-star bar of spsolve, f (fp64) untouched."""
-    from mofhip import DeviceMesh, synth
-    import oracle
+
+def test_damped_multigrid_recovery_on_pinwheel_patch():
+    """The S1-like 3,249-vertex patch under an atan2 pinwheel signal centred
+    on the patch (synth.travelling_wave): the V-cycle with the fine smoother at
+    0.85 is not contractive there and every first solve breaks down within a
+    few iterations; the recovery's damped multigrid pass (fine damping 0.6)
+    re-solves them in tens of iterations -- not the hundreds of block Jacobi --
+    and V matches spsolve (relative to |V|: the patch's |V| ~ 5)."""
     from scipy.sparse.linalg import spsolve
-    p, t = synth.icosphere(20, jitter=0.005)
-    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
-    I = synth.travelling_wave(p, 5)
-    tk = np.arange(5, dtype=np.float64)
-    out = {}
-    for g3 in ("0", "1"):
-        monkeypatch.setenv("MOF_ASM_G3", g3)
-        m = DeviceMesh(p, n, t, a)
-        V, st = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", precond="amg")
-        assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
-        out[g3] = (V, st["iterations"])
-        m.close()
+    p, t, n, a = synth.mesh_for_config("S1s")
+    K = 6
+    I = synth.travelling_wave(p, K + 1)
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(K + 1.0), 0, K, 0.01, precision="mixed", precond="amg", rtol=1e-9)
+    assert st["failed"] == 0 and st["recovered"] == K and st["recovered_f64"] == 0, st
+    assert st["iterations"] / K < 80, st
     a2, gw, e, iw = oracle.geometry(p, n, t, a)
-    for k in (0, 3):
+    for k in (0, K - 1):
         A, f = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
         Vo = spsolve(A.tocsc(), f)
-        assert np.abs(out["1"][0][k] - Vo).max() < 1e-6
-    assert abs(out["1"][1] - out["0"][1]) <= 0.1 * out["0"][1]
+        assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
