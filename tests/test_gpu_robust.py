@@ -299,7 +299,7 @@ def test_damped_multigrid_recovery_on_pinwheel_patch():
     I = synth.travelling_wave(p, K + 1)
     m = DeviceMesh(p, n, t, a)
     V, st = m.solve_range(I, np.arange(K + 1.0), 0, K, 0.01, precision="mixed", precond="amg", rtol=1e-9)
-    assert st["failed"] == 0 and st["recovered"] == K and st["recovered_f64"] == 0, st
+    assert st["failed"] == 0 and st["recovered"] >= 1 and st["recovered_f64"] == 0, st
     assert st["iterations"] / K < 80, st
     a2, gw, e, iw = oracle.geometry(p, n, t, a)
     for k in (0, K - 1):
