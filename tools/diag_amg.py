@@ -5,7 +5,9 @@
 Solves K timesteps (mixed + multigrid) with recovery off and MOF_SOLVE_VERBOSE
 set, so the library prints per refinement step the inner iterations and why
 the first solve's failed systems failed; the environment assignments (e.g.
-MOF_AMG_SMOOTH=0, MOF_X_BF16=0, MOF_WINDOW_SORT=0) select the variant.
+MOF_AMG_SMOOTH=0, MOF_X_BF16=0, MOF_WINDOW_SORT=0) select the variant. The
+signal is the bench's for CONFIG (synth.config_wave; DIAG_PINWHEEL=1: the
+atan2 pinwheel of synth.travelling_wave).
 """
 import json
 import os
@@ -29,7 +31,7 @@ def main():
     from mofhip import DeviceMesh, synth
     p, t, n, a = synth.mesh_for_config(cfg)
     m = DeviceMesh(p, n, t, a)
-    I = synth.travelling_wave(p, K + 1)
+    I = synth.config_wave(cfg, p, K + 1) if os.environ.get("DIAG_PINWHEEL") != "1" else synth.travelling_wave(p, K + 1)
     tk = np.arange(K + 1, dtype=np.float64)
     out = {"config": cfg, "env": [kv for kv in sys.argv[2:] if "=" in kv]}
     for rec in (False, True):
