@@ -267,6 +267,9 @@ def electrode_surface(n_side: int, spacing: float = 10.0, jitter: float = 0.15, 
     Delaunay valences (4-8). Returns (points (V,3) f64, triangles (M,3) int32)
     with consistently oriented triangles (normals towards +z)."""
     from scipy.spatial import Delaunay
+    half = 0.5 * (n_side - 1) * spacing * (1.0 + jitter)
+    if half * 2 ** 0.5 > 0.9 * radius:
+        raise ValueError("the grid (half-width %.1f) must lie well inside the sphere (radius %.1f)" % (half, radius))
     rng = np.random.default_rng(seed)
     g = (np.arange(n_side) - 0.5 * (n_side - 1)) * spacing
     x, y = np.meshgrid(g, g, indexing="ij")
@@ -369,10 +372,12 @@ def mesh_for_config(name: str):
         p, t = random_sphere(163842, 10.0, seed=0)
         return p, t, vertex_normals(p, t), triangle_areas(p, t)
     if name in ("S1", "S1s"):
-        # S1-like surfaces (electrode_surface): S1 = a 51 x 51 grid (160,801
-        # vertices, the 160k class), S1s = an 8 x 8 grid (3,249 vertices, the
-        # size of the reference's real surfaces, find_singularity_point.py:19-20)
-        p, t = electrode_surface(51 if name == "S1" else 8)
+        # S1-like surfaces (electrode_surface): S1s = an 8 x 8 grid at 10 mm
+        # (a clinical ECoG grid, 70 mm across; 3,249 vertices, the size of the
+        # reference's real surfaces, find_singularity_point.py:19-20), S1 = a
+        # 51 x 51 high-density grid at 1.5 mm over the same 75 mm (160,801
+        # vertices, the 160k class)
+        p, t = electrode_surface(51, spacing=1.5) if name == "S1" else electrode_surface(8, spacing=10.0)
         return p, t, vertex_normals(p, t), triangle_areas(p, t)
     if name == "P3":
         p, t, _, _ = mesh_for_config("C3")
