@@ -1079,11 +1079,8 @@ void charge_chunk(const mof_mesh *m, int32_t B, const std::vector<int32_t> &runn
 constexpr int64_t kGraphTiles = 32768;
 constexpr size_t kMaxGraphs = 64;
 bool graphs_wanted(const mof_mesh *m, int32_t B) {
-    static const int forced = [] {
-        const char *v = std::getenv("MOF_GRAPHS");
-        return v && *v ? std::atoi(v) : -1;
-    }();
-    if (forced >= 0) return forced != 0;
+    const char *v = std::getenv("MOF_GRAPHS");  // read per solve (A/B in one process)
+    if (v && *v) return std::atoi(v) != 0;
     return (int64_t)m->ws.nblk * B <= kGraphTiles;
 }
 template <typename V>
