@@ -322,16 +322,12 @@ def main():
                                   "ms_solve", "max_rel_residual", "outer_steps", "fused_launches",
                                   "ms_fused"), 0) | {"systems": b - a}
         if host_io:
-            V, st = mesh.solve_range(I_host, tk, a, b, args.lambda_, device=local,
-                                     time_spmv=timed and args.config not in SMALL_JOBS, **opts)
+            V, st = mesh.solve_range(I_host, tk, a, b, args.lambda_, device=local, time_spmv=timed, **opts)
             if timed:
                 kept.append(V)
             return st
-        # small jobs: no per-launch SpMV events (the library then replays the
-        # iteration chunks from HIP graphs; their SpMV is launch-bound anyway)
         return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), K_rank + 1, tk, a, b, args.lambda_,
-                                       V_dev.data_ptr(), device=local,
-                                       time_spmv=timed and args.config not in SMALL_JOBS, **opts)
+                                       V_dev.data_ptr(), device=local, time_spmv=timed, **opts)
 
     if strong:
         # balanced batches: 625 timesteps per rank at N = 8 run as 2 x 313,

@@ -656,7 +656,6 @@ int mof_mesh_destroy(mof_mesh *m) {
             if (m->h_sysi) (void)hipHostFree(m->h_sysi);
             if (m->h_sysd) (void)hipHostFree(m->h_sysd);
             for (auto e : m->spmv_events) (void)hipEventDestroy(e);
-            mof::clear_graphs(m);
             delete m->stage;
             m->stage = nullptr;
             for (auto &e : m->hev)

@@ -1535,7 +1535,6 @@ void amg_ensure(mof_mesh *m, int32_t B) {
     }
     G.cinv.alloc((size_t)G.nc * G.nc * B);
     G.cap = B;
-    clear_graphs(m);
     MOF_HIP(hipStreamSynchronize(s));
 }
 

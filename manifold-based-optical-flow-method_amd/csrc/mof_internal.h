@@ -19,7 +19,6 @@
 #include <cstdint>
 #include <cstdlib>
 #include <functional>
-#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -261,10 +260,6 @@ struct mof_mesh {
     // host state shared with the clones of this mesh on other devices
     std::shared_ptr<mof::MeshShared> shared;
     hipEvent_t hev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    // small batches: instantiated HIP graphs of PCG iteration chunks, keyed by
-    // the launch arguments (pointers, scalars, first iteration, length); cleared
-    // whenever a buffer they point into is reallocated (mof_pcg.hip)
-    std::map<std::vector<uint64_t>, hipGraphExec_t> graphs;
 };
 
 namespace mof {
@@ -393,8 +388,6 @@ int32_t amg_levels(const mof_mesh *m);
 // set the fine-level smoother damping of m's multigrid cycle; returns the
 // previous value (0 and no change when m has no hierarchy)
 float amg_set_omega(mof_mesh *m, float omega);
-// drop the handle's cached iteration graphs (their buffers are reallocated)
-void clear_graphs(mof_mesh *m);
 
 // every (row block, system) pair of the XCD order (mof_rowkern.h) visited once
 bool xcd_map_covers(int32_t nblk, int32_t B, int32_t grp);

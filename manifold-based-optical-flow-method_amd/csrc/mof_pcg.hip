@@ -39,13 +39,11 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
 #include <chrono>
 #include <cmath>
 
 #include <hip/hip_ext.h>
 
-#include "mof_amg.h"
 #include "mof_dd.h"
 #include "mof_internal.h"
 #include "mof_rowkern.h"
@@ -1071,41 +1069,6 @@ void charge_chunk(const mof_mesh *m, int32_t B, const std::vector<int32_t> &runn
     }
 }
 
-// HIP graphs for the iteration chunks of small batches: MOF_GRAPHS=0/1
-// forces, default on when a launch's (row block, system) tiles are few
-// enough for the launch latency to dominate (nblk B <= kGraphTiles; round 4,
-// tools/graph_probe.py: 4.1 us per dependent tiny kernel launched eagerly,
-// 1.76 us replayed from a graph)
-constexpr int64_t kGraphTiles = 32768;
-constexpr size_t kMaxGraphs = 64;
-bool graphs_wanted(const mof_mesh *m, int32_t B) {
-    const char *v = std::getenv("MOF_GRAPHS");  // read per solve (A/B in one process)
-    if (v && *v) return std::atoi(v) != 0;
-    return (int64_t)m->ws.nblk * B <= kGraphTiles;
-}
-template <typename V>
-std::vector<uint64_t> graph_key(const PcgArgs<V> &a, int32_t B, int32_t it0, int32_t n, const AmgDevice *g) {
-    auto u = [](const void *p) { return (uint64_t)(uintptr_t)p; };
-    std::vector<uint64_t> k = {sizeof(V), (uint64_t)B, (uint64_t)it0, (uint64_t)n, (uint64_t)a.N, (uint64_t)a.nblk,
-                               u(a.mat.A), u(a.mat.sell_mir), u(a.mat.vptr), u(a.dinv), u(a.x), u(a.r), u(a.z),
-                               u(a.p), u(a.q), u(a.part_pq), u(a.part_rzrr), u(a.sysd), u(a.sysi), u(a.sc),
-                               (uint64_t)a.ext, u(a.x0), u(a.dA), u(a.dA_off), (uint64_t)a.dA_nb,
-                               (uint64_t)(uint32_t)a.stall, (uint64_t)a.zh, (uint64_t)a.red.P, (uint64_t)a.red.nmax,
-                               (uint64_t)a.red.nown};
-    double om = (double)a.omega;
-    uint64_t bits = 0;
-    std::memcpy(&bits, &om, sizeof(bits));
-    k.push_back(bits);
-    if (g) {  // the V-cycle reads its damping and level buffers from the hierarchy
-        float w[2] = {g->omega, g->omega1};
-        uint64_t wb = 0;
-        std::memcpy(&wb, w, sizeof(wb));
-        k.push_back(wb);
-        k.push_back(u(g));
-    }
-    return k;
-}
-
 // Inner PCG on all active systems; returns iterations summed over systems.
 template <typename V>
 int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
@@ -1156,7 +1119,6 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     // retire on the device, so overshooting costs only early-exit launches.
     int32_t it = 0;
     int32_t chunk = *hint > 0 ? std::min(*hint, kMaxChunk) : 8;
-    const bool use_graphs = !timing && graphs_wanted(m, B);
     bool done = false;
     std::vector<hipEvent_t> &ev = m->spmv_events;
     std::vector<float> ms;
@@ -1168,38 +1130,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             for (size_t q = old; q < ev.size(); ++q) MOF_HIP(hipEventCreate(&ev[q]));
         }
         const int32_t it0 = it;
-        // small batches (launch-latency-bound): the chunk replayed from an
-        // instantiated HIP graph, captured the first time its launches occur
-        // (the same kernels with the same arguments: the same bits)
-        hipGraphExec_t gx_exec = nullptr;
-        bool capturing = false;
-        std::vector<uint64_t> gkey;
-        if (use_graphs) {
-            gkey = graph_key(a, B, it0, n, amg ? m->amg : nullptr);
-            auto f = m->graphs.find(gkey);
-            if (f != m->graphs.end()) {
-                gx_exec = f->second;
-            } else {
-                MOF_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-                capturing = true;
-            }
-        }
-        struct CaptureGuard {  // an error inside the capture ends it
-            hipStream_t s;
-            bool &on;
-            ~CaptureGuard() {
-                if (on) {
-                    hipGraph_t g = nullptr;
-                    (void)hipStreamEndCapture(s, &g);
-                    if (g) (void)hipGraphDestroy(g);
-                }
-            }
-        } cguard{s, capturing};
-        if (gx_exec) {
-            MOF_HIP(hipGraphLaunch(gx_exec, s));
-            it += n;
-        }
-        for (int32_t c = 0; c < n && !gx_exec; ++c, ++it) {
+        for (int32_t c = 0; c < n; ++c, ++it) {
             if (timing) {
                 // events stamped by the kernel's own dispatch packet (start
                 // and end of its execution, as rocprof's kernel trace), not
@@ -1217,18 +1148,6 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, (it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
-        if (capturing) {
-            hipGraph_t g = nullptr;
-            capturing = false;
-            MOF_HIP(hipStreamEndCapture(s, &g));
-            hipGraphExec_t ex = nullptr;
-            const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(g);
-            MOF_HIP(e);
-            if (m->graphs.size() >= kMaxGraphs) clear_graphs(m);
-            m->graphs.emplace(gkey, ex);
-            MOF_HIP(hipGraphLaunch(ex, s));
-        }
         fetch_flags(m, B, s);
         if (timing) {
             ms.assign(n, 0.f);
@@ -1386,11 +1305,6 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
 
 }  // namespace
 
-void clear_graphs(mof_mesh *m) {
-    for (auto &kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
-    m->graphs.clear();
-}
-
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
     // SURVEY.md 8(d)'s algorithmic bytes of a batched CSR SpMV: per system the
     // nnz values, one read of x and one write of y (R = 2N rows); shared by
@@ -1417,16 +1331,13 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
             arr.zero(m->stream);
         }
     };
-    const void *a32 = w.A32.p, *a64 = w.A64.p;
     need_A(w.A32, precision == MOF_PREC_MIXED);
     need_A(w.A64, precision == MOF_PREC_F64);
-    if (w.A32.p != a32 || w.A64.p != a64) clear_graphs(m);
     if (w.cap >= B) {
         MOF_HIP(hipStreamSynchronize(m->stream));
         return;
     }
     w.cap = B;
-    clear_graphs(m);
     w.nblk = (int32_t)((N + kRowsPerWG - 1) / kRowsPerWG);
     // the per-triangle term arrays are sized on first use (ensure_tri_terms)
     w.u64.release();
