@@ -1341,6 +1341,19 @@ MatH level0_mat(mof_mesh *m) {
 
 bool amg_build(mof_mesh *m) {
     AmgParams prm;
+    // an open surface (boundary edges: 3 M != 2 E) damps the fine smoother
+    // more: at a Neumann boundary vertex the diagonal block lacks the missing
+    // triangles while its couplings stay, and 0.85 leaves the block-Jacobi
+    // sweep non-contractive there -- round 4, the S1-like patches: every
+    // multigrid solve broke down at 0.85 (3,249 and 160,801 vertices), none at
+    // 0.7 (S1s 22.5 PCG its/timestep); on the closed meshes 0.7 costs C3
+    // 17.0 -> 18.5 its (-7 %) and C2 21.6 -> 23.0, R3 51.4 -> 50.6
+    // (profiles/r04_ab/call4/). A decomposed part keeps 0.85 (its ghost rows
+    // are decoupled, not a Neumann boundary).
+    {
+        const int64_t E = ((int64_t)m->pat.nblocks() - m->N) / 2;
+        if (m->n_own == m->N && 3 * (int64_t)m->M != 2 * E) prm.omega = 0.7f;
+    }
     if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
     if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
     if (const char *v = std::getenv("MOF_AMG_SMOOTH")) prm.smooth = std::atoi(v);  // 1 / 0 force, unset auto
