@@ -1350,10 +1350,11 @@ bool amg_build(mof_mesh *m) {
     // 17.0 -> 18.5 its (-7 %) and C2 21.6 -> 23.0, R3 51.4 -> 50.6
     // (profiles/r04_ab/call4/). A decomposed part keeps 0.85 (its ghost rows
     // are decoupled, not a Neumann boundary).
-    {
+    const bool open_surface = [&] {
         const int64_t E = ((int64_t)m->pat.nblocks() - m->N) / 2;
-        if (m->n_own == m->N && 3 * (int64_t)m->M != 2 * E) prm.omega = 0.7f;
-    }
+        return m->n_own == m->N && 3 * (int64_t)m->M != 2 * E;
+    }();
+    if (open_surface) prm.omega = 0.7f;
     if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
     if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
     if (const char *v = std::getenv("MOF_AMG_SMOOTH")) prm.smooth = std::atoi(v);  // 1 / 0 force, unset auto
@@ -1420,7 +1421,9 @@ bool amg_build(mof_mesh *m) {
     // the regular meshes; an irregular mesh keeps fp32 and 1.05 whichever
     // prolongator it runs (round 3: R3 forced onto the tentative P took
     // 146.5 PCG its/timestep with the regular meshes' choices)
-    G.regular = !H.levels[0].smoothed && !amg_auto_smooth(m->pat);
+    // (round 4: and closed -- an open patch's near-null modes suffer from
+    // the bf16 iterates as from the stronger coarse damping)
+    G.regular = !H.levels[0].smoothed && !amg_auto_smooth(m->pat) && !open_surface;
     G.xm = G.regular ? 1 : 2;
     // coarse-level damping: 1.1 on regular meshes (round 2, C3 17.2 -> 17.0
     // its, +1.8 %; C2 mixed +2 %), 1.05 otherwise (R3 as measured; 1.2
