@@ -286,14 +286,16 @@ def test_f64_without_block_jacobi_recovers():
 
 
 
-def test_damped_multigrid_recovery_on_pinwheel_patch():
+def test_damped_multigrid_recovery_on_pinwheel_patch(monkeypatch):
     """The S1-like 3,249-vertex patch under an atan2 pinwheel signal centred
-    on the patch (synth.travelling_wave): the V-cycle with the fine smoother at
-    0.85 is not contractive there and every first solve breaks down within a
-    few iterations; the recovery's damped multigrid pass (fine damping 0.6)
-    re-solves them in tens of iterations -- not the hundreds of block Jacobi --
-    and V matches spsolve (relative to |V|: the patch's |V| ~ 5)."""
+    on the patch (synth.travelling_wave), with the closed meshes' fine
+    damping forced (MOF_AMG_OMEGA=0.85; an open surface gets 0.7 by itself):
+    the V-cycle is not contractive there and the first solves break down
+    within a few iterations; the recovery's damped multigrid pass (fine
+    damping 0.6) re-solves them in tens of iterations -- not the hundreds of
+    block Jacobi -- and V matches spsolve (relative to |V|: |V| ~ 5)."""
     from scipy.sparse.linalg import spsolve
+    monkeypatch.setenv("MOF_AMG_OMEGA", "0.85")  # read when the hierarchy is built
     p, t, n, a = synth.mesh_for_config("S1s")
     K = 6
     I = synth.travelling_wave(p, K + 1)
