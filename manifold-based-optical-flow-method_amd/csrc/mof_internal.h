@@ -137,6 +137,9 @@ struct Workspace {
     DevArray<float> dinv32;
     DevArray<double> rhs;              // [B][N][2] f (interleaved)
     DevArray<double> x64, r64;         // [B][N][2] outer solution / residual
+    // system-interleaved copies for the system-major residual (k_residual_sm):
+    // x64 as [N][B][2], the batch's I rows as [N][B]; allocated on first use
+    DevArray<double> x64t, It;
     DevArray<double> vx, vr, vz, vp, vq;  // [B][N][2] inner PCG vectors (fp64 sized)
     DevArray<double> part_pq;          // [B][nblk]
     DevArray<double> part_rzrr;        // [2][B][nblk][2]

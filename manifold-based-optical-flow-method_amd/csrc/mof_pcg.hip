@@ -876,6 +876,208 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t
     }
 }
 
+// ---- the system-major residual (mixed path, u re-formed) ----
+// k_residual_rcn gathers every row's geometry (a2 blocks, incident
+// triangles' hat gradients, the corners' tangent bases) once per system pair
+// and waits on those gathers 65 % of its wave cycles. Here one wave walks one
+// SELL slice (64 rows) row by row with one SYSTEM per lane: the row's
+// geometry is wave-uniform (scalar loads, once per 64 systems) and the
+// per-system operands come from system-interleaved copies -- x64t [N][B][2]
+// (written by k_outer_update_t beside x64) and It [N][B] (k_transpose_rows of
+// the batch's I rows) -- so each neighbour's x and I for the wave's 64
+// systems is one contiguous 1 KiB / 512 B read. Per (row, system) the
+// arithmetic is apply_row_rcn's in the same order, so r64 keeps its bits; the
+// slice's rows are visited in bit-reversed order and their |r|^2, |f|^2 terms
+// merged pairwise (a binary counter over 6 levels), which is exactly the
+// shfl_down tree of block_sum's wave_sum, and the four waves are added as
+// block_sum adds them: the partial records keep their bits too.
+constexpr int kSmU = 4;  // a2 slots per load batch
+
+__device__ __forceinline__ void sm_merge(int32_t k, double2 c, double2 (&st)[6], double2 &out) {
+    // leaf k of the bit-reversed order: pairwise sums as wave_sum forms them
+    // (selects at every level, no indexed register array: k is wave-uniform)
+    bool done = false;
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        const bool bit = ((k >> lv) & 1) != 0;
+        const double2 m = make_double2(st[lv].x + c.x, st[lv].y + c.y);
+        if (!done && !bit) st[lv] = c;
+        if (!done && bit) c = m;
+        done = done || !bit;
+    }
+    if (!done) out = c;  // k = 63: the slice's sum
+}
+
+__global__ __launch_bounds__(kWG) void k_residual_sm(
+    int32_t N, int32_t M, int32_t nblk, int32_t B, const int32_t *__restrict__ sell_off,
+    const int32_t *__restrict__ sell_col, const double *__restrict__ a2s, const int32_t *__restrict__ tsell_off,
+    const int4 *__restrict__ tinc, const double *__restrict__ w12, const double *__restrict__ gw,
+    const double *__restrict__ e, const double *__restrict__ It, const double *__restrict__ x64t,
+    const double *__restrict__ rhs, const int32_t *__restrict__ sysi, double *__restrict__ r64,
+    double *__restrict__ part) {
+#pragma clang fp contract(off)
+    __shared__ double2 lds[4][64];
+    int32_t rb, g;
+    if (!xcd_map(nblk, (B + 63) >> 6, rb, g, 0)) return;
+    const int32_t lane = threadIdx.x & 63;
+    const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
+    const int32_t b = g * 64 + lane, bc = min(b, B - 1);
+    const bool on = b < B && sysi[bc * kSysStride + SI_ACTIVE] != 0;
+    const int32_t s = rb * 4 + wv, i0 = s * kSlice;
+    double2 st[6], sum = make_double2(0.0, 0.0);
+    if (i0 < N) {
+        const int32_t ao = sell_off[s], aw = (sell_off[s + 1] - ao) >> 6;
+        const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
+        for (int32_t k = 0; k < kSlice; ++k) {
+            const int32_t l = (int32_t)(__builtin_bitreverse32((uint32_t)k) >> 26);
+            const int32_t i = i0 + l;
+            double2 term = make_double2(0.0, 0.0);
+            if (i < N) {
+                double acc0 = 0.0, acc1 = 0.0;
+                // lambda a2 x (rcn_a2)
+                for (int32_t t0 = 0; t0 < aw; t0 += kSmU) {
+                    int32_t j[kSmU];
+                    double blk[kSmU][4];
+                    double2 xj[kSmU];
+#pragma unroll
+                    for (int u = 0; u < kSmU; ++u) {
+                        const int64_t p = (int64_t)ao + (int64_t)min(t0 + u, aw - 1) * kSlice + l;
+                        j[u] = sell_col[p];
+                        ld_blk(a2s, p, blk[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSmU; ++u) xj[u] = ld2(x64t + 2 * ((int64_t)j[u] * B + bc));
+#pragma unroll
+                    for (int u = 0; u < kSmU; ++u) {
+                        const bool in = t0 + u < aw;
+                        acc0 += in ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : 0.0;
+                        acc1 += in ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : 0.0;
+                    }
+                }
+                // a1 x per incident triangle (rcn_row / rcn_tri)
+                const double2 xi = ld2(x64t + 2 * ((int64_t)i * B + bc));
+                const double Ii = It[(int64_t)i * B + bc];
+                double ei[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) ei[q] = e[6 * (int64_t)i + q];
+                for (int32_t t = 0; t < tw; ++t) {
+                    const int4 q = tinc[(int64_t)to + (int64_t)t * kSlice + l];
+                    const int64_t T = min(q.x, M - 1);
+                    double gv[9], ej[6], ek[6];
+#pragma unroll
+                    for (int k2 = 0; k2 < 9; ++k2) gv[k2] = gw[9 * T + k2];
+#pragma unroll
+                    for (int k2 = 0; k2 < 6; ++k2) {
+                        ej[k2] = e[6 * (int64_t)q.z + k2];
+                        ek[k2] = e[6 * (int64_t)q.w + k2];
+                    }
+                    const double Ij = It[(int64_t)q.z * B + bc], Ik = It[(int64_t)q.w * B + bc];
+                    const double2 xj = ld2(x64t + 2 * ((int64_t)q.z * B + bc));
+                    const double2 xk = ld2(x64t + 2 * ((int64_t)q.w * B + bc));
+                    const double wt = w12[q.x];
+                    const int c = q.y;
+                    const double c0 = c == 0 ? Ii : (c == 1 ? Ik : Ij);
+                    const double c1 = c == 0 ? Ij : (c == 1 ? Ii : Ik);
+                    const double c2 = c == 0 ? Ik : (c == 1 ? Ij : Ii);
+                    double gI[3];
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) gI[d] = (c0 * gv[d] + c1 * gv[3 + d]) + c2 * gv[6 + d];
+                    const double2 ui = make_double2(dot3_np(gI, ei), dot3_np(gI, ei + 3));
+                    const double2 uj = make_double2(dot3_np(gI, ej), dot3_np(gI, ej + 3));
+                    const double2 uk = make_double2(dot3_np(gI, ek), dot3_np(gI, ek + 3));
+                    const double si = ui.x * xi.x + ui.y * xi.y;
+                    const double sj = uj.x * xj.x + uj.y * xj.y;
+                    const double sk = uk.x * xk.x + uk.y * xk.y;
+                    const double cc = wt * ((si + si) + sj + sk);
+                    acc0 += ui.x * cc;
+                    acc1 += ui.y * cc;
+                }
+                const double2 f = ld2(rhs + 2 * ((int64_t)bc * N + i));
+                const double r0 = f.x - acc0, r1 = f.y - acc1;
+                if (on) *reinterpret_cast<double2 *>(r64 + 2 * ((int64_t)b * N + i)) = make_double2(r0, r1);
+                term = make_double2(0.0 + (r0 * r0 + r1 * r1), 0.0 + (f.x * f.x + f.y * f.y));
+            }
+            sm_merge(k, term, st, sum);
+        }
+    }
+    lds[wv][lane] = sum;
+    __syncthreads();
+    if (wv == 0 && on) {
+        const double rr = ((lds[0][lane].x + lds[1][lane].x) + lds[2][lane].x) + lds[3][lane].x;
+        const double ff = ((lds[0][lane].y + lds[1][lane].y) + lds[2][lane].y) + lds[3][lane].y;
+        double *o = part + 2 * ((int64_t)b * nblk + rb);
+        o[0] = rr;
+        o[1] = ff;
+    }
+}
+
+// x64 (+)= x_inner as k_outer_update, and the same values into the
+// system-interleaved x64t [N][B][2] through a 32-row x 64-system LDS tile
+// (reads along rows, writes along systems, both coalesced). A system not
+// active in the inner solve keeps x64; its x64t gets that value.
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_outer_update_t(int32_t N, int32_t B, int32_t first,
+                                                        const V *__restrict__ xin, const int32_t *__restrict__ sysi,
+                                                        double *__restrict__ x64, double *__restrict__ x64t) {
+    __shared__ double2 tile[32][65];
+    using V2 = typename VT<V>::V2;
+    const int32_t i0 = blockIdx.x * 32, b0 = blockIdx.y * 64;
+    const int32_t t = threadIdx.x;
+    {
+        const int32_t r = t & 31, sb = t >> 5, i = i0 + r;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int32_t sl = sb + 8 * k, b = b0 + sl;
+            if (b >= B || i >= N) continue;
+            const int64_t vi = (int64_t)b * N + i;
+            double2 x;
+            if (sysi[b * kSysStride + SI_ACTIVE]) {
+                const V2 d = *reinterpret_cast<const V2 *>(xin + 2 * vi);
+                x = first ? make_double2(0.0, 0.0) : *reinterpret_cast<const double2 *>(x64 + 2 * vi);
+                x.x += (double)d.x;
+                x.y += (double)d.y;
+                *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
+            } else {
+                x = *reinterpret_cast<const double2 *>(x64 + 2 * vi);
+            }
+            tile[r][sl] = x;
+        }
+    }
+    __syncthreads();
+    const int32_t sl = t & 63, rq = t >> 6, b = b0 + sl;
+    if (b >= B) return;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t r = rq + 4 * k, i = i0 + r;
+        if (i < N) *reinterpret_cast<double2 *>(x64t + 2 * ((int64_t)i * B + b)) = tile[r][sl];
+    }
+}
+
+// dst [N][B] = src [B][N] (row stride N): the batch's I rows interleaved per
+// vertex for k_residual_sm, through a 32-row x 64-system LDS tile.
+__global__ __launch_bounds__(kWG) void k_transpose_rows(int32_t N, int32_t B, const double *__restrict__ src,
+                                                        double *__restrict__ dst) {
+    __shared__ double tile[32][65];
+    const int32_t i0 = blockIdx.x * 32, b0 = blockIdx.y * 64;
+    const int32_t t = threadIdx.x;
+    {
+        const int32_t r = t & 31, sb = t >> 5, i = i0 + r;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int32_t sl = sb + 8 * k, b = b0 + sl;
+            if (b < B && i < N) tile[r][sl] = src[(int64_t)b * N + i];
+        }
+    }
+    __syncthreads();
+    const int32_t sl = t & 63, rq = t >> 6, b = b0 + sl;
+    if (b >= B) return;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t r = rq + 4 * k, i = i0 + r;
+        if (i < N) dst[(int64_t)i * B + b] = tile[r][sl];
+    }
+}
+
 // One workgroup per system: relative true residual; retire converged systems.
 template <int NT = kWG>
 __device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, const double *__restrict__ part,
@@ -1380,6 +1582,13 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
 // stored u64 (the fp64 path's residual); auto (sp.fused < 0) on meshes of at
 // most MOF_FUSED_MAX_BLK row blocks (default 16: 4096 vertices), where the
 // eager path is launch-bound.
+// MOF_RES_SM=0: the mixed path keeps k_residual_rcn (A/B; the same bits)
+static bool residual_sm(mof_mesh *m) {
+    const char *v = std::getenv("MOF_RES_SM");
+    if (v && *v == '0') return false;
+    return !op64(m).u && m->n_own == m->N;
+}
+
 bool fused_eligible(const mof_mesh *m, const SolveParams &sp, const uint8_t *only) {
     if (sp.fused == 0 || only || sp.precision != MOF_PREC_F64 || sp.amg || sp.fail_at_max_iter) return false;
     if (m->ws.u64_stale || !m->ws.u64.p || m->n_own != m->N) return false;
@@ -1493,6 +1702,18 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     } omega_scope(m, sp.amg_omega, amg);
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
+    // the system-major residual where u is re-formed from the I rows on a
+    // single domain (the mixed path): interleaved x64 / I copies
+    const bool sm = residual_sm(m);
+    const dim3 gt((unsigned)((m->N + 31) / 32), (unsigned)((B + 63) / 64));  // 32-row x 64-system tiles
+    if (sm) {
+        const size_t n = (size_t)m->N * std::max(w.cap, B);
+        if (w.x64t.n < 2 * n) w.x64t.alloc(2 * n);
+        if (w.It.n < n) w.It.alloc(n);
+        MOF_REQUIRE(w.J0 && w.JB >= B, "residual: the batch's I rows are gone");
+        k_transpose_rows<<<gt, kWG, 0, s>>>(m->N, B, w.J0, w.It.p);
+        MOF_HIP(hipGetLastError());
+    }
     int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
     // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
@@ -1504,17 +1725,30 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol, sp, s,
                                 max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg,
                                 o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
-            k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                    w.sysi.p, w.x64.p);
+            if (sm)
+                k_outer_update_t<float><<<gt, kWG, 0, s>>>(m->N, B, o == 0, reinterpret_cast<float *>(w.vx.p),
+                                                          w.sysi.p, w.x64.p, w.x64t.p);
+            else
+                k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
+                                                        w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
                                  &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
-            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+            if (sm)
+                k_outer_update_t<double><<<gt, kWG, 0, s>>>(m->N, B, o == 0, w.vx.p, w.sysi.p, w.x64.p, w.x64t.p);
+            else
+                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
-        launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
-                                                              w.r64.p, w.part_rr0.p);
+        if (sm) {
+            const OpArgs<double> op = op64(m);
+            k_residual_sm<<<dim3(xcd_grid(w.nblk, (B + 63) / 64, 0)), kWG, 0, s>>>(
+                m->N, m->M, w.nblk, B, op.sell_off, op.sell_col, op.a2s, op.tsell_off, op.tinc, op.w12, op.gw,
+                op.e, w.It.p, w.x64t.p, w.rhs.p, w.sysi.p, w.r64.p, w.part_rr0.p);
+        } else {
+            launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
+        }
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
         MOF_HIP(hipGetLastError());
