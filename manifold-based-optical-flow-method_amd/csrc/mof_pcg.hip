@@ -880,19 +880,28 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t
 // k_residual_rcn gathers every row's geometry (a2 blocks, incident
 // triangles' hat gradients, the corners' tangent bases) once per system pair
 // and waits on those gathers 65 % of its wave cycles. Here one wave walks one
-// SELL slice (64 rows) row by row with one SYSTEM per lane: the row's
+// SELL slice (64 rows) row by row with one SYSTEM per lane, so a row's
 // geometry is wave-uniform (scalar loads, once per 64 systems) and the
-// per-system operands come from system-interleaved copies -- x64t [N][B][2]
-// (written by k_outer_update_t beside x64) and It [N][B] (k_transpose_rows of
-// the batch's I rows) -- so each neighbour's x and I for the wave's 64
-// systems is one contiguous 1 KiB / 512 B read. Per (row, system) the
-// arithmetic is apply_row_rcn's in the same order, so r64 keeps its bits; the
-// slice's rows are visited in bit-reversed order and their |r|^2, |f|^2 terms
-// merged pairwise (a binary counter over 6 levels), which is exactly the
-// shfl_down tree of block_sum's wave_sum, and the four waves are added as
-// block_sum adds them: the partial records keep their bits too.
-constexpr int kSmU = 4;  // a2 slots per load batch
-
+// per-system operands come from system-interleaved copies -- each
+// neighbour's operand for the wave's 64 systems is one contiguous read. The
+// operator is applied in ambient 3-D (a1 restricted to a triangle is
+// u u^T (x) [A/6, A/12] with u_v = E_v grad I_T, a2's block (i, j) is
+// (e_i . e_j) L_ij; tests/test_operator_3d.py checks the identity against the
+// reference's A_k):
+//   (A x)_i = E_i [ sum_j lambda L_ij X_j + sum_{T ni i} (A_T/12) (gI_T . Y_T) gI_T ],
+//   X_v = E_v^T x_v,  Y_T = 2 X_i + X_j + X_k,
+// so a triangle needs only its 9 hat-gradient values (no tangent frames of the
+// other corners) and a slot one lambda L scalar: X64t [N][B][3] is written by
+// k_outer_update_t beside x64, It [N][B] by k_transpose_rows from the batch's
+// I rows. Each wave first loads its slice's tables with one coalesced read
+// per slot (lane l holds row l's column ids, lambda L values and incidences),
+// so a row's ids come from v_readlane, not from memory: the neighbour gathers
+// of a row are issued together, then the incident triangles NB at a time
+// (their scalar geometry loads and per-system gathers in flight together).
+// Explicit fma, no contraction: a system's bits do not depend on its lane
+// (the batch split). The slice's rows are visited in bit-reversed order and
+// their |r|^2, |f|^2 terms merged pairwise, which is wave_sum's shfl_down
+// tree, and the four waves are added as block_sum adds them.
 __device__ __forceinline__ void sm_merge(int32_t k, double2 c, double2 (&st)[6], double2 &out) {
     // leaf k of the bit-reversed order: pairwise sums as wave_sum forms them
     // (selects at every level, no indexed register array: k is wave-uniform)
@@ -908,11 +917,19 @@ __device__ __forceinline__ void sm_merge(int32_t k, double2 c, double2 (&st)[6],
     if (!done) out = c;  // k = 63: the slice's sum
 }
 
-__global__ __launch_bounds__(kWG) void k_residual_sm(
+__device__ __forceinline__ void ld3(const double *p, double (&x)[3]) {
+    x[0] = p[0];
+    x[1] = p[1];
+    x[2] = p[2];
+}
+
+constexpr int kSmNB = 3, kSmU = 4;  // incident triangles / slots per load batch
+template <int W, int NB>
+__global__ __launch_bounds__(kWG) void k_residual_x3sm(
     int32_t N, int32_t M, int32_t nblk, int32_t B, const int32_t *__restrict__ sell_off,
-    const int32_t *__restrict__ sell_col, const double *__restrict__ a2s, const int32_t *__restrict__ tsell_off,
+    const int32_t *__restrict__ sell_col, const double *__restrict__ lap, const int32_t *__restrict__ tsell_off,
     const int4 *__restrict__ tinc, const double *__restrict__ w12, const double *__restrict__ gw,
-    const double *__restrict__ e, const double *__restrict__ It, const double *__restrict__ x64t,
+    const double *__restrict__ e, const double *__restrict__ It, const double *__restrict__ X64t,
     const double *__restrict__ rhs, const int32_t *__restrict__ sysi, double *__restrict__ r64,
     double *__restrict__ part) {
 #pragma clang fp contract(off)
@@ -928,72 +945,94 @@ __global__ __launch_bounds__(kWG) void k_residual_sm(
     if (i0 < N) {
         const int32_t ao = sell_off[s], aw = (sell_off[s + 1] - ao) >> 6;
         const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
+        // the slice's tables, lane = row of the slice (padding: L = 0, T = M)
+        int32_t col[W], tT[W], tj[W], tk[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+            col[t] = t < aw ? sell_col[(int64_t)ao + t * kSlice + lane] : 0;
+            const int4 q = t < tw ? tinc[(int64_t)to + t * kSlice + lane] : make_int4(M, 0, 0, 0);
+            tT[t] = (q.x << 2) | q.y;
+            tj[t] = q.z;
+            tk[t] = q.w;
+        }
+        const double *Xb = X64t + 3 * (int64_t)bc;
+        const double *Ib = It + bc;
+        const int64_t sX = 3 * (int64_t)B;
         for (int32_t k = 0; k < kSlice; ++k) {
             const int32_t l = (int32_t)(__builtin_bitreverse32((uint32_t)k) >> 26);
             const int32_t i = i0 + l;
             double2 term = make_double2(0.0, 0.0);
             if (i < N) {
-                double acc0 = 0.0, acc1 = 0.0;
-                // lambda a2 x (rcn_a2)
-                for (int32_t t0 = 0; t0 < aw; t0 += kSmU) {
-                    int32_t j[kSmU];
-                    double blk[kSmU][4];
-                    double2 xj[kSmU];
+                double acc[3] = {0.0, 0.0, 0.0};
+                // sum_j lambda L_ij X_j over the row's slots, kSmU at a time
+#pragma unroll
+                for (int t0 = 0; t0 < W; t0 += kSmU) {
+                    if (t0 >= aw) break;
+                    double xj[kSmU][3], Lj[kSmU];
 #pragma unroll
                     for (int u = 0; u < kSmU; ++u) {
-                        const int64_t p = (int64_t)ao + (int64_t)min(t0 + u, aw - 1) * kSlice + l;
-                        j[u] = sell_col[p];
-                        ld_blk(a2s, p, blk[u]);
+                        const int t = t0 + u;
+                        const bool in = t < aw;
+                        const int32_t j = in ? __builtin_amdgcn_readlane(col[t], l) : i;
+                        Lj[u] = in ? lap[(int64_t)ao + t * kSlice + l] : 0.0;
+                        ld3(Xb + j * sX, xj[u]);
                     }
-#pragma unroll
-                    for (int u = 0; u < kSmU; ++u) xj[u] = ld2(x64t + 2 * ((int64_t)j[u] * B + bc));
 #pragma unroll
                     for (int u = 0; u < kSmU; ++u) {
-                        const bool in = t0 + u < aw;
-                        acc0 += in ? blk[u][0] * xj[u].x + blk[u][1] * xj[u].y : 0.0;
-                        acc1 += in ? blk[u][2] * xj[u].x + blk[u][3] * xj[u].y : 0.0;
+                        if (t0 + u >= aw) break;
+#pragma unroll
+                        for (int d = 0; d < 3; ++d) acc[d] = fma(Lj[u], xj[u][d], acc[d]);
                     }
                 }
-                // a1 x per incident triangle (rcn_row / rcn_tri)
-                const double2 xi = ld2(x64t + 2 * ((int64_t)i * B + bc));
-                const double Ii = It[(int64_t)i * B + bc];
-                double ei[6];
+                // sum_T (A_T/12) (gI . Y) gI over the incident triangles, NB at a time
+                double Xi[3];
+                ld3(Xb + i * sX, Xi);
+                const double Ii = Ib[(int64_t)i * B];
 #pragma unroll
-                for (int q = 0; q < 6; ++q) ei[q] = e[6 * (int64_t)i + q];
-                for (int32_t t = 0; t < tw; ++t) {
-                    const int4 q = tinc[(int64_t)to + (int64_t)t * kSlice + l];
-                    const int64_t T = min(q.x, M - 1);
-                    double gv[9], ej[6], ek[6];
+                for (int t0 = 0; t0 < W; t0 += NB) {
+                    if (t0 >= tw) break;
+                    double gv[NB][9], wt[NB], Ij[NB], Ik[NB], Xj[NB][3], Xk[NB][3];
+                    int32_t c[NB];
 #pragma unroll
-                    for (int k2 = 0; k2 < 9; ++k2) gv[k2] = gw[9 * T + k2];
+                    for (int u = 0; u < NB; ++u) {
+                        const int t = t0 + u;
+                        const bool in = t < tw;
+                        const int32_t Tc = in ? __builtin_amdgcn_readlane(tT[t], l) : (M << 2);
+                        const int32_t vj = in ? __builtin_amdgcn_readlane(tj[t], l) : i;
+                        const int32_t vk = in ? __builtin_amdgcn_readlane(tk[t], l) : i;
+                        const int64_t T = min(Tc >> 2, M - 1);
+                        c[u] = Tc & 3;
 #pragma unroll
-                    for (int k2 = 0; k2 < 6; ++k2) {
-                        ej[k2] = e[6 * (int64_t)q.z + k2];
-                        ek[k2] = e[6 * (int64_t)q.w + k2];
+                        for (int k2 = 0; k2 < 9; ++k2) gv[u][k2] = gw[9 * T + k2];
+                        wt[u] = in ? w12[Tc >> 2] : 0.0;
+                        Ij[u] = Ib[(int64_t)vj * B];
+                        Ik[u] = Ib[(int64_t)vk * B];
+                        ld3(Xb + vj * sX, Xj[u]);
+                        ld3(Xb + vk * sX, Xk[u]);
                     }
-                    const double Ij = It[(int64_t)q.z * B + bc], Ik = It[(int64_t)q.w * B + bc];
-                    const double2 xj = ld2(x64t + 2 * ((int64_t)q.z * B + bc));
-                    const double2 xk = ld2(x64t + 2 * ((int64_t)q.w * B + bc));
-                    const double wt = w12[q.x];
-                    const int c = q.y;
-                    const double c0 = c == 0 ? Ii : (c == 1 ? Ik : Ij);
-                    const double c1 = c == 0 ? Ij : (c == 1 ? Ii : Ik);
-                    const double c2 = c == 0 ? Ik : (c == 1 ? Ij : Ii);
-                    double gI[3];
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) gI[d] = (c0 * gv[d] + c1 * gv[3 + d]) + c2 * gv[6 + d];
-                    const double2 ui = make_double2(dot3_np(gI, ei), dot3_np(gI, ei + 3));
-                    const double2 uj = make_double2(dot3_np(gI, ej), dot3_np(gI, ej + 3));
-                    const double2 uk = make_double2(dot3_np(gI, ek), dot3_np(gI, ek + 3));
-                    const double si = ui.x * xi.x + ui.y * xi.y;
-                    const double sj = uj.x * xj.x + uj.y * xj.y;
-                    const double sk = uk.x * xk.x + uk.y * xk.y;
-                    const double cc = wt * ((si + si) + sj + sk);
-                    acc0 += ui.x * cc;
-                    acc1 += ui.y * cc;
+                    for (int u = 0; u < NB; ++u) {
+                        if (t0 + u >= tw) break;
+                        const int cu = c[u];
+                        const double c0 = cu == 0 ? Ii : (cu == 1 ? Ik[u] : Ij[u]);
+                        const double c1 = cu == 0 ? Ij[u] : (cu == 1 ? Ii : Ik[u]);
+                        const double c2 = cu == 0 ? Ik[u] : (cu == 1 ? Ij[u] : Ii);
+                        double gI[3], Y[3];
+#pragma unroll
+                        for (int d = 0; d < 3; ++d) {
+                            gI[d] = fma(c2, gv[u][6 + d], fma(c1, gv[u][3 + d], c0 * gv[u][d]));
+                            Y[d] = ((Xi[d] + Xi[d]) + Xj[u][d]) + Xk[u][d];
+                        }
+                        const double dd = wt[u] * fma(gI[2], Y[2], fma(gI[1], Y[1], gI[0] * Y[0]));
+#pragma unroll
+                        for (int d = 0; d < 3; ++d) acc[d] = fma(dd, gI[d], acc[d]);
+                    }
                 }
+                const double *ei = e + 6 * (int64_t)i;
+                const double y0 = fma(ei[2], acc[2], fma(ei[1], acc[1], ei[0] * acc[0]));
+                const double y1 = fma(ei[5], acc[2], fma(ei[4], acc[1], ei[3] * acc[0]));
                 const double2 f = ld2(rhs + 2 * ((int64_t)bc * N + i));
-                const double r0 = f.x - acc0, r1 = f.y - acc1;
+                const double r0 = f.x - y0, r1 = f.y - y1;
                 if (on) *reinterpret_cast<double2 *>(r64 + 2 * ((int64_t)b * N + i)) = make_double2(r0, r1);
                 term = make_double2(0.0 + (r0 * r0 + r1 * r1), 0.0 + (f.x * f.x + f.y * f.y));
             }
@@ -1011,14 +1050,16 @@ __global__ __launch_bounds__(kWG) void k_residual_sm(
     }
 }
 
-// x64 (+)= x_inner as k_outer_update, and the same values into the
-// system-interleaved x64t [N][B][2] through a 32-row x 64-system LDS tile
-// (reads along rows, writes along systems, both coalesced). A system not
-// active in the inner solve keeps x64; its x64t gets that value.
+// x64 (+)= x_inner as k_outer_update, and X = E x of the same values into the
+// system-interleaved X64t [N][B][3] through a 32-row x 64-system LDS tile
+// (reads along rows, writes along systems with the row's tangent basis as
+// scalar loads, both coalesced). A system not active in the inner solve
+// keeps x64; its X64t gets that value's X.
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_outer_update_t(int32_t N, int32_t B, int32_t first,
                                                         const V *__restrict__ xin, const int32_t *__restrict__ sysi,
-                                                        double *__restrict__ x64, double *__restrict__ x64t) {
+                                                        const double *__restrict__ e, double *__restrict__ x64,
+                                                        double *__restrict__ X64t) {
     __shared__ double2 tile[32][65];
     using V2 = typename VT<V>::V2;
     const int32_t i0 = blockIdx.x * 32, b0 = blockIdx.y * 64;
@@ -1044,17 +1085,22 @@ __global__ __launch_bounds__(kWG) void k_outer_update_t(int32_t N, int32_t B, in
         }
     }
     __syncthreads();
-    const int32_t sl = t & 63, rq = t >> 6, b = b0 + sl;
+    const int32_t sl = t & 63, rq = __builtin_amdgcn_readfirstlane(t >> 6), b = b0 + sl;
     if (b >= B) return;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int32_t r = rq + 4 * k, i = i0 + r;
-        if (i < N) *reinterpret_cast<double2 *>(x64t + 2 * ((int64_t)i * B + b)) = tile[r][sl];
+        if (i >= N) break;
+        const double *ei = e + 6 * (int64_t)i;
+        const double2 x = tile[r][sl];
+        double *o = X64t + 3 * ((int64_t)i * B + b);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) o[d] = fma(ei[3 + d], x.y, ei[d] * x.x);
     }
 }
 
 // dst [N][B] = src [B][N] (row stride N): the batch's I rows interleaved per
-// vertex for k_residual_sm, through a 32-row x 64-system LDS tile.
+// vertex for k_residual_x3sm, through a 32-row x 64-system LDS tile.
 __global__ __launch_bounds__(kWG) void k_transpose_rows(int32_t N, int32_t B, const double *__restrict__ src,
                                                         double *__restrict__ dst) {
     __shared__ double tile[32][65];
@@ -1586,7 +1632,8 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
 static bool residual_sm(mof_mesh *m) {
     const char *v = std::getenv("MOF_RES_SM");
     if (v && *v == '0') return false;
-    return !op64(m).u && m->n_own == m->N;
+    // the slice tables hold up to 8 slots (tw <= aw <= max_w)
+    return !op64(m).u && m->n_own == m->N && m->pat.max_w <= 8 && m->lap64.p;
 }
 
 bool fused_eligible(const mof_mesh *m, const SolveParams &sp, const uint8_t *only) {
@@ -1708,7 +1755,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     const dim3 gt((unsigned)((m->N + 31) / 32), (unsigned)((B + 63) / 64));  // 32-row x 64-system tiles
     if (sm) {
         const size_t n = (size_t)m->N * std::max(w.cap, B);
-        if (w.x64t.n < 2 * n) w.x64t.alloc(2 * n);
+        if (w.X64t.n < 3 * n) w.X64t.alloc(3 * n);
         if (w.It.n < n) w.It.alloc(n);
         MOF_REQUIRE(w.J0 && w.JB >= B, "residual: the batch's I rows are gone");
         k_transpose_rows<<<gt, kWG, 0, s>>>(m->N, B, w.J0, w.It.p);
@@ -1727,7 +1774,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
                                 o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
             if (sm)
                 k_outer_update_t<float><<<gt, kWG, 0, s>>>(m->N, B, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                          w.sysi.p, w.x64.p, w.x64t.p);
+                                                          w.sysi.p, m->e.p, w.x64.p, w.X64t.p);
             else
                 k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
                                                         w.sysi.p, w.x64.p);
@@ -1736,16 +1783,17 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
                                  &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
             if (sm)
-                k_outer_update_t<double><<<gt, kWG, 0, s>>>(m->N, B, o == 0, w.vx.p, w.sysi.p, w.x64.p, w.x64t.p);
+                k_outer_update_t<double><<<gt, kWG, 0, s>>>(m->N, B, o == 0, w.vx.p, w.sysi.p, m->e.p, w.x64.p,
+                                                           w.X64t.p);
             else
                 k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
         if (sm) {
             const OpArgs<double> op = op64(m);
-            k_residual_sm<<<dim3(xcd_grid(w.nblk, (B + 63) / 64, 0)), kWG, 0, s>>>(
-                m->N, m->M, w.nblk, B, op.sell_off, op.sell_col, op.a2s, op.tsell_off, op.tinc, op.w12, op.gw,
-                op.e, w.It.p, w.x64t.p, w.rhs.p, w.sysi.p, w.r64.p, w.part_rr0.p);
+            k_residual_x3sm<8, kSmNB><<<dim3(xcd_grid(w.nblk, (B + 63) / 64, 0)), kWG, 0, s>>>(
+                m->N, m->M, w.nblk, B, op.sell_off, op.sell_col, m->lap64.p, op.tsell_off, op.tinc, op.w12, op.gw,
+                op.e, w.It.p, w.X64t.p, w.rhs.p, w.sysi.p, w.r64.p, w.part_rr0.p);
         } else {
             launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
         }

@@ -1,13 +1,15 @@
 """The system-major fp64 residual of the mixed path (csrc/mof_pcg.hip
-k_residual_sm: one SELL slice per wave, one system per lane, x64 and the I
-rows read from system-interleaved copies) against the row-major
-k_residual_rcn it replaces (MOF_RES_SM=0). The residual r64 = f - A x64 of
-the refinement (compute_optical_flow.py:147's system) keeps
-its arithmetic per (row, system) and the partial |r|^2 / |f|^2 records keep
-their summation tree, so V, the iteration counts and the residuals must be
-bit-identical -- on full and partial 64-system groups, ragged batches, an
-open surface, a vertex order scattered by a random relabelling, and the
-recovery passes that re-solve failed systems."""
+k_residual_x3sm: one SELL slice per wave, one system per lane, the operator
+applied in ambient 3-D from system-interleaved X = E x and I copies) against
+the row-major tangent-frame k_residual_rcn it replaces (MOF_RES_SM=0). Both
+apply the reference's A_k (compute_optical_flow.py:100-146) in fp64 --
+tests/test_operator_3d.py checks the 3-D identity on the CPU -- so the
+refinement converges to the same V within its tolerance (rtol 1e-8), with
+the same refinement steps; on full and partial 64-system groups, ragged
+batches, an open surface, a vertex order scattered by a random relabelling,
+and the recovery passes that re-solve failed systems. The kernel's partial
+|r|^2 records follow block_sum's tree, and a system's bits do not depend on
+its lane: a batch split leaves V bit-identical."""
 import numpy as np
 import pytest
 
@@ -15,7 +17,16 @@ from mofhip import DeviceMesh, synth
 
 pytestmark = pytest.mark.gpu
 
-_KEYS = ("iterations", "max_iterations", "failed", "recovered", "outer_steps", "max_rel_residual")
+_KEYS = ("failed", "recovered", "outer_steps")
+
+
+def _close(V0, V1, s0, s1):
+    assert s1["failed"] == 0 and s1["max_rel_residual"] <= 1e-8
+    scale = float(np.abs(V0).max())
+    assert np.abs(V1 - V0).max() <= 1e-8 * scale
+    for k in _KEYS:
+        assert s0[k] == s1[k], k
+    assert abs(s0["iterations"] - s1["iterations"]) <= 0.02 * s0["iterations"] + 2
 
 
 def _mesh(p, t, **kw):
@@ -49,10 +60,7 @@ def test_residual_sm_bit_identical(case, opts, monkeypatch):
     # perm: the internal order is the random one (no RCM), so every gather scatters
     m = _mesh(p, t, reorder=case != "perm")
     (V0, s0), (V1, s1) = _both(monkeypatch, m, I, **opts)
-    assert s1["failed"] == 0 and s1["max_rel_residual"] <= 1e-8
-    assert np.array_equal(V0, V1)
-    for k in _KEYS:
-        assert s0[k] == s1[k], k
+    _close(V0, V1, s0, s1)
 
 
 def test_residual_sm_recovery_passes(monkeypatch):
@@ -64,7 +72,20 @@ def test_residual_sm_recovery_passes(monkeypatch):
     m = _mesh(p, t)
     I = synth.travelling_wave(p, 20)
     (V0, s0), (V1, s1) = _both(monkeypatch, m, I, precision="mixed", precond="amg", max_iter=3, max_outer=1)
-    assert s0["recovered"] > 0 and s1["failed"] == 0
-    assert np.array_equal(V0, V1)
-    for k in _KEYS:
-        assert s0[k] == s1[k], k
+    assert s0["recovered"] > 0
+    _close(V0, V1, s0, s1)
+
+
+def test_residual_sm_batch_split_bit_identical(monkeypatch):
+    """A system's bits do not depend on its lane or 64-system group: the
+    same timesteps solved as one batch of 70 and as batches of 33 / 33 / 4
+    (different lanes, groups and partial groups) give the same V."""
+    monkeypatch.setenv("MOF_RES_SM", "1")
+    p, t = synth.icosphere(32, jitter=0.005)
+    m = _mesh(p, t)
+    I = synth.travelling_wave(p, 71)
+    tk = np.arange(71, dtype=np.float64)
+    Va, sa = m.solve_range(I, tk, 0, 70, 0.01, precision="mixed", precond="jacobi", batch=0)
+    Vb, sb = m.solve_range(I, tk, 0, 70, 0.01, precision="mixed", precond="jacobi", batch=33)
+    assert sa["failed"] == sb["failed"] == 0
+    assert np.array_equal(Va, Vb)
