@@ -22,8 +22,10 @@ _KEYS = ("failed", "recovered", "outer_steps")
 
 def _close(V0, V1, s0, s1):
     assert s1["failed"] == 0 and s1["max_rel_residual"] <= 1e-8
+    # two solutions within rtol 1e-8 of the same system: |V1 - V0| is of the
+    # order of either's distance from spsolve (3-9e-8 on these meshes)
     scale = float(np.abs(V0).max())
-    assert np.abs(V1 - V0).max() <= 1e-8 * scale
+    assert np.abs(V1 - V0).max() <= 2e-7 * scale
     for k in _KEYS:
         assert s0[k] == s1[k], k
     assert abs(s0["iterations"] - s1["iterations"]) <= 0.02 * s0["iterations"] + 2
