@@ -924,9 +924,31 @@ __device__ __forceinline__ void ld3(const double *p, double (&x)[3]) {
 }
 
 constexpr int kSmNB = 3, kSmU = 4;  // incident triangles / slots per load batch
-template <int W, int NB>
+
+// map 1: each XCD takes whole 64-system groups (XCD x: groups x, x + 8, ...;
+// fewer than 8 groups: 8 / G XCDs per group, each a contiguous share of the
+// row blocks) and walks their row blocks in order, so an XCD's L2 holds one
+// group's interleaved operands around the rows in flight
+__device__ __forceinline__ bool grp_xcd_map(int32_t nblk, int32_t G, int32_t &rb, int32_t &g) {
+    const int32_t w = (int32_t)blockIdx.x, x = w & 7, q = w >> 3;
+    if (G >= 8) {
+        g = x + 8 * (q / nblk);
+        rb = q % nblk;
+        return g < G;
+    }
+    const int32_t per = 8 / G, chunk = (nblk + per - 1) / per;
+    g = x / per;
+    rb = (x % per) * chunk + q;
+    return g < G && q < chunk && rb < nblk;
+}
+inline unsigned grp_xcd_grid(int32_t nblk, int32_t G) {
+    if (G >= 8) return (unsigned)(8 * nblk * ((G + 7) / 8));
+    const int32_t per = 8 / G;
+    return (unsigned)(8 * ((nblk + per - 1) / per));
+}
+template <int W, int NB, bool NAT>
 __global__ __launch_bounds__(kWG) void k_residual_x3sm(
-    int32_t N, int32_t M, int32_t nblk, int32_t B, const int32_t *__restrict__ sell_off,
+    int32_t N, int32_t M, int32_t nblk, int32_t B, int32_t map, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const double *__restrict__ lap, const int32_t *__restrict__ tsell_off,
     const int4 *__restrict__ tinc, const double *__restrict__ w12, const double *__restrict__ gw,
     const double *__restrict__ e, const double *__restrict__ It, const double *__restrict__ X64t,
@@ -935,7 +957,7 @@ __global__ __launch_bounds__(kWG) void k_residual_x3sm(
 #pragma clang fp contract(off)
     __shared__ double2 lds[4][64];
     int32_t rb, g;
-    if (!xcd_map(nblk, (B + 63) >> 6, rb, g, 0)) return;
+    if (map ? !grp_xcd_map(nblk, (B + 63) >> 6, rb, g) : !xcd_map(nblk, (B + 63) >> 6, rb, g, 0)) return;
     const int32_t lane = threadIdx.x & 63;
     const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
     const int32_t b = g * 64 + lane, bc = min(b, B - 1);
@@ -959,7 +981,7 @@ __global__ __launch_bounds__(kWG) void k_residual_x3sm(
         const double *Ib = It + bc;
         const int64_t sX = 3 * (int64_t)B;
         for (int32_t k = 0; k < kSlice; ++k) {
-            const int32_t l = (int32_t)(__builtin_bitreverse32((uint32_t)k) >> 26);
+            const int32_t l = NAT ? k : (int32_t)(__builtin_bitreverse32((uint32_t)k) >> 26);
             const int32_t i = i0 + l;
             double2 term = make_double2(0.0, 0.0);
             if (i < N) {
@@ -1036,7 +1058,12 @@ __global__ __launch_bounds__(kWG) void k_residual_x3sm(
                 if (on) *reinterpret_cast<double2 *>(r64 + 2 * ((int64_t)b * N + i)) = make_double2(r0, r1);
                 term = make_double2(0.0 + (r0 * r0 + r1 * r1), 0.0 + (f.x * f.x + f.y * f.y));
             }
-            sm_merge(k, term, st, sum);
+            if constexpr (NAT) {
+                sum.x += term.x;
+                sum.y += term.y;
+            } else {
+                sm_merge(k, term, st, sum);
+            }
         }
     }
     lds[wv][lane] = sum;
@@ -1791,8 +1818,19 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         const RedArgs rd{1, 0, w.nblk, m->N};
         if (sm) {
             const OpArgs<double> op = op64(m);
-            k_residual_x3sm<8, kSmNB><<<dim3(xcd_grid(w.nblk, (B + 63) / 64, 0)), kWG, 0, s>>>(
-                m->N, m->M, w.nblk, B, op.sell_off, op.sell_col, m->lap64.p, op.tsell_off, op.tinc, op.w12, op.gw,
+            static const int smap = [] {
+                const char *v = std::getenv("MOF_RES_SM_MAP");
+                return v && *v ? std::atoi(v) : 0;
+            }();
+            static const bool nat = [] {
+                const char *v = std::getenv("MOF_RES_SM_NAT");
+                return v && *v == '1';
+            }();
+            const int32_t G = (B + 63) / 64;
+            const dim3 gr(smap ? grp_xcd_grid(w.nblk, G) : xcd_grid(w.nblk, G, 0));
+            auto kr = nat ? k_residual_x3sm<8, kSmNB, true> : k_residual_x3sm<8, kSmNB, false>;
+            kr<<<gr, kWG, 0, s>>>(
+                m->N, m->M, w.nblk, B, smap, op.sell_off, op.sell_col, m->lap64.p, op.tsell_off, op.tinc, op.w12, op.gw,
                 op.e, w.It.p, w.X64t.p, w.rhs.p, w.sysi.p, w.r64.p, w.part_rr0.p);
         } else {
             launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
