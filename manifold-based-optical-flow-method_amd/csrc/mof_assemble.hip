@@ -167,34 +167,6 @@ __global__ __launch_bounds__(kWG) void k_a2(int32_t N, const int32_t *__restrict
     }
 }
 
-// lambda L_ij per SELL slot of row i, L_ij = sum over the triangles of edge
-// (i, j) (the diagonal: of vertex i) of A_T (grad w_a . grad w_b): a2's 2x2
-// block (i, j) is (e_i^alpha . e_j^beta) L_ij (compute_a2 :258-270 with e
-// independent of the triangle), so lambda a2 x = E_i sum_j lambda L_ij X_j,
-// X_j = E_j^T x_j -- the form the system-major residual applies
-// (mof_pcg.hip k_residual_x3sm). Not bit-exact to anything: the residual only
-// needs an fp64-accurate operator (tests/test_operator_3d.py).
-__global__ __launch_bounds__(kWG) void k_lap(int32_t N, const int32_t *__restrict__ vptr,
-                                             const int32_t *__restrict__ vcol, const int32_t *__restrict__ cptr,
-                                             const int32_t *__restrict__ clist, const int32_t *__restrict__ sell_off,
-                                             const double *__restrict__ gw, const double *__restrict__ area,
-                                             double lambda, double *__restrict__ lap) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x;
-    if (i >= N) return;
-    int32_t td = 0;
-    while (vcol[vptr[i] + td] != i) ++td;
-    for (int32_t p = vptr[i], t = 0; p < vptr[i + 1]; ++p, ++t) {
-        double acc = 0.0;
-        for (int32_t c = cptr[p]; c < cptr[p + 1]; ++c) {
-            const int32_t code = clist[c];
-            const int32_t T = code / 9, a = (code % 9) / 3, b = code % 3;
-            const double *g = gw + 9 * (int64_t)T;
-            acc += dot64(g + 3 * a, g + 3 * b) * area[T];
-        }
-        lap[sell_pos(sell_off, i, sell_slot(t, td))] = lambda * acc;
-    }
-}
-
 // Per-triangle half of worker (:113-126, compute_f :288-311) for B systems:
 // grad_M I and, for each corner a and alpha, u = grad_M I . e_a^alpha and the
 // f term (u (2 dI_a + sum of the other distinct corners' dI) A_T) / 12.
@@ -845,10 +817,6 @@ void prepare_operator(mof_mesh *m, double lambda, hipStream_t s) {
     if (m->a2s_valid && m->a2s_lambda == lambda) return;
     const int64_t n = 4 * m->pat.sell_nb();
     k_scale_a2<<<grid1(n), kWG, 0, s>>>(n, lambda, m->a2.p, m->a2s64.p, m->a2s32.p);
-    if (m->lap64.n < (size_t)(n / 4)) m->lap64.alloc((size_t)(n / 4));
-    m->lap64.zero(s);  // SELL padding stays 0
-    k_lap<<<grid1(m->N), kWG, 0, s>>>(m->N, m->vptr.p, m->vcol.p, m->cptr.p, m->clist.p, m->sell_off.p, m->gw.p,
-                                      m->area.p, lambda, m->lap64.p);
     MOF_HIP(hipGetLastError());
     m->a2s_lambda = lambda;
     m->a2s_valid = true;

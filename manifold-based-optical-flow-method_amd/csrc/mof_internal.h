@@ -137,10 +137,6 @@ struct Workspace {
     DevArray<float> dinv32;
     DevArray<double> rhs;              // [B][N][2] f (interleaved)
     DevArray<double> x64, r64;         // [B][N][2] outer solution / residual
-    // system-interleaved copies for the system-major residual (k_residual_x3sm):
-    // x64 in ambient 3-D, X = E x, as [N][B][3], and the batch's I rows as
-    // [N][B]; allocated on first use
-    DevArray<double> X64t, It;
     DevArray<double> vx, vr, vz, vp, vq;  // [B][N][2] inner PCG vectors (fp64 sized)
     DevArray<double> part_pq;          // [B][nblk]
     DevArray<double> part_rzrr;        // [2][B][nblk][2]
@@ -238,10 +234,6 @@ struct mof_mesh {
     // operator copies: lambda*a2 (cached per lambda) and A_T/12 with a zero slot M
     mof::DevArray<double> a2s64, w12_64;
     mof::DevArray<float> a2s32, w12_32;
-    // lambda x the scalar Laplacian L_ij = sum_T A_T (grad w_i . grad w_j) per
-    // SELL slot (a2's block (i, j) is (e_i^a . e_j^b) L_ij): the system-major
-    // fp64 residual's 3-D form (k_residual_x3sm)
-    mof::DevArray<double> lap64;
     double a2s_lambda = 0.0;
     bool a2s_valid = false;
     // mof_assemble / mof_csr_export(MOF_CSR_A_LAST): one assembled A (SELL) and f

@@ -876,281 +876,6 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t
     }
 }
 
-// ---- the system-major residual (mixed path, u re-formed) ----
-// k_residual_rcn gathers every row's geometry (a2 blocks, incident
-// triangles' hat gradients, the corners' tangent bases) once per system pair
-// and waits on those gathers 65 % of its wave cycles. Here one wave walks one
-// SELL slice (64 rows) row by row with one SYSTEM per lane, so a row's
-// geometry is wave-uniform (scalar loads, once per 64 systems) and the
-// per-system operands come from system-interleaved copies -- each
-// neighbour's operand for the wave's 64 systems is one contiguous read. The
-// operator is applied in ambient 3-D (a1 restricted to a triangle is
-// u u^T (x) [A/6, A/12] with u_v = E_v grad I_T, a2's block (i, j) is
-// (e_i . e_j) L_ij; tests/test_operator_3d.py checks the identity against the
-// reference's A_k):
-//   (A x)_i = E_i [ sum_j lambda L_ij X_j + sum_{T ni i} (A_T/12) (gI_T . Y_T) gI_T ],
-//   X_v = E_v^T x_v,  Y_T = 2 X_i + X_j + X_k,
-// so a triangle needs only its 9 hat-gradient values (no tangent frames of the
-// other corners) and a slot one lambda L scalar: X64t [N][B][3] is written by
-// k_outer_update_t beside x64, It [N][B] by k_transpose_rows from the batch's
-// I rows. Each wave first loads its slice's tables with one coalesced read
-// per slot (lane l holds row l's column ids, lambda L values and incidences),
-// so a row's ids come from v_readlane, not from memory: the neighbour gathers
-// of a row are issued together, then the incident triangles NB at a time
-// (their scalar geometry loads and per-system gathers in flight together).
-// Explicit fma, no contraction: a system's bits do not depend on its lane
-// (the batch split). The slice's rows are visited in bit-reversed order and
-// their |r|^2, |f|^2 terms merged pairwise, which is wave_sum's shfl_down
-// tree, and the four waves are added as block_sum adds them.
-__device__ __forceinline__ void sm_merge(int32_t k, double2 c, double2 (&st)[6], double2 &out) {
-    // leaf k of the bit-reversed order: pairwise sums as wave_sum forms them
-    // (selects at every level, no indexed register array: k is wave-uniform)
-    bool done = false;
-#pragma unroll
-    for (int lv = 0; lv < 6; ++lv) {
-        const bool bit = ((k >> lv) & 1) != 0;
-        const double2 m = make_double2(st[lv].x + c.x, st[lv].y + c.y);
-        if (!done && !bit) st[lv] = c;
-        if (!done && bit) c = m;
-        done = done || !bit;
-    }
-    if (!done) out = c;  // k = 63: the slice's sum
-}
-
-__device__ __forceinline__ void ld3(const double *p, double (&x)[3]) {
-    x[0] = p[0];
-    x[1] = p[1];
-    x[2] = p[2];
-}
-
-constexpr int kSmNB = 3, kSmU = 4;  // incident triangles / slots per load batch
-
-// map 1: each XCD takes whole 64-system groups (XCD x: groups x, x + 8, ...;
-// fewer than 8 groups: 8 / G XCDs per group, each a contiguous share of the
-// row blocks) and walks their row blocks in order, so an XCD's L2 holds one
-// group's interleaved operands around the rows in flight
-__device__ __forceinline__ bool grp_xcd_map(int32_t nblk, int32_t G, int32_t &rb, int32_t &g) {
-    const int32_t w = (int32_t)blockIdx.x, x = w & 7, q = w >> 3;
-    if (G >= 8) {
-        g = x + 8 * (q / nblk);
-        rb = q % nblk;
-        return g < G;
-    }
-    const int32_t per = 8 / G, chunk = (nblk + per - 1) / per;
-    g = x / per;
-    rb = (x % per) * chunk + q;
-    return g < G && q < chunk && rb < nblk;
-}
-inline unsigned grp_xcd_grid(int32_t nblk, int32_t G) {
-    if (G >= 8) return (unsigned)(8 * nblk * ((G + 7) / 8));
-    const int32_t per = 8 / G;
-    return (unsigned)(8 * ((nblk + per - 1) / per));
-}
-template <int W, int NB, bool NAT>
-__global__ __launch_bounds__(kWG) void k_residual_x3sm(
-    int32_t N, int32_t M, int32_t nblk, int32_t B, int32_t map, const int32_t *__restrict__ sell_off,
-    const int32_t *__restrict__ sell_col, const double *__restrict__ lap, const int32_t *__restrict__ tsell_off,
-    const int4 *__restrict__ tinc, const double *__restrict__ w12, const double *__restrict__ gw,
-    const double *__restrict__ e, const double *__restrict__ It, const double *__restrict__ X64t,
-    const double *__restrict__ rhs, const int32_t *__restrict__ sysi, double *__restrict__ r64,
-    double *__restrict__ part) {
-#pragma clang fp contract(off)
-    __shared__ double2 lds[4][64];
-    int32_t rb, g;
-    if (map ? !grp_xcd_map(nblk, (B + 63) >> 6, rb, g) : !xcd_map(nblk, (B + 63) >> 6, rb, g, 0)) return;
-    const int32_t lane = threadIdx.x & 63;
-    const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
-    const int32_t b = g * 64 + lane, bc = min(b, B - 1);
-    const bool on = b < B && sysi[bc * kSysStride + SI_ACTIVE] != 0;
-    const int32_t s = rb * 4 + wv, i0 = s * kSlice;
-    double2 st[6], sum = make_double2(0.0, 0.0);
-    if (i0 < N) {
-        const int32_t ao = sell_off[s], aw = (sell_off[s + 1] - ao) >> 6;
-        const int32_t to = tsell_off[s], tw = (tsell_off[s + 1] - to) >> 6;
-        // the slice's tables, lane = row of the slice (padding: L = 0, T = M)
-        int32_t col[W], tT[W], tj[W], tk[W];
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-            col[t] = t < aw ? sell_col[(int64_t)ao + t * kSlice + lane] : 0;
-            const int4 q = t < tw ? tinc[(int64_t)to + t * kSlice + lane] : make_int4(M, 0, 0, 0);
-            tT[t] = (q.x << 2) | q.y;
-            tj[t] = q.z;
-            tk[t] = q.w;
-        }
-        const double *Xb = X64t + 3 * (int64_t)bc;
-        const double *Ib = It + bc;
-        const int64_t sX = 3 * (int64_t)B;
-        for (int32_t k = 0; k < kSlice; ++k) {
-            const int32_t l = NAT ? k : (int32_t)(__builtin_bitreverse32((uint32_t)k) >> 26);
-            const int32_t i = i0 + l;
-            double2 term = make_double2(0.0, 0.0);
-            if (i < N) {
-                double acc[3] = {0.0, 0.0, 0.0};
-                // sum_j lambda L_ij X_j over the row's slots, kSmU at a time
-#pragma unroll
-                for (int t0 = 0; t0 < W; t0 += kSmU) {
-                    if (t0 >= aw) break;
-                    double xj[kSmU][3], Lj[kSmU];
-#pragma unroll
-                    for (int u = 0; u < kSmU; ++u) {
-                        const int t = t0 + u;
-                        const bool in = t < aw;
-                        const int32_t j = in ? __builtin_amdgcn_readlane(col[t], l) : i;
-                        Lj[u] = in ? lap[(int64_t)ao + t * kSlice + l] : 0.0;
-                        ld3(Xb + j * sX, xj[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kSmU; ++u) {
-                        if (t0 + u >= aw) break;
-#pragma unroll
-                        for (int d = 0; d < 3; ++d) acc[d] = fma(Lj[u], xj[u][d], acc[d]);
-                    }
-                }
-                // sum_T (A_T/12) (gI . Y) gI over the incident triangles, NB at a time
-                double Xi[3];
-                ld3(Xb + i * sX, Xi);
-                const double Ii = Ib[(int64_t)i * B];
-#pragma unroll
-                for (int t0 = 0; t0 < W; t0 += NB) {
-                    if (t0 >= tw) break;
-                    double gv[NB][9], wt[NB], Ij[NB], Ik[NB], Xj[NB][3], Xk[NB][3];
-                    int32_t c[NB];
-#pragma unroll
-                    for (int u = 0; u < NB; ++u) {
-                        const int t = t0 + u;
-                        const bool in = t < tw;
-                        const int32_t Tc = in ? __builtin_amdgcn_readlane(tT[t], l) : (M << 2);
-                        const int32_t vj = in ? __builtin_amdgcn_readlane(tj[t], l) : i;
-                        const int32_t vk = in ? __builtin_amdgcn_readlane(tk[t], l) : i;
-                        const int64_t T = min(Tc >> 2, M - 1);
-                        c[u] = Tc & 3;
-#pragma unroll
-                        for (int k2 = 0; k2 < 9; ++k2) gv[u][k2] = gw[9 * T + k2];
-                        wt[u] = in ? w12[Tc >> 2] : 0.0;
-                        Ij[u] = Ib[(int64_t)vj * B];
-                        Ik[u] = Ib[(int64_t)vk * B];
-                        ld3(Xb + vj * sX, Xj[u]);
-                        ld3(Xb + vk * sX, Xk[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < NB; ++u) {
-                        if (t0 + u >= tw) break;
-                        const int cu = c[u];
-                        const double c0 = cu == 0 ? Ii : (cu == 1 ? Ik[u] : Ij[u]);
-                        const double c1 = cu == 0 ? Ij[u] : (cu == 1 ? Ii : Ik[u]);
-                        const double c2 = cu == 0 ? Ik[u] : (cu == 1 ? Ij[u] : Ii);
-                        double gI[3], Y[3];
-#pragma unroll
-                        for (int d = 0; d < 3; ++d) {
-                            gI[d] = fma(c2, gv[u][6 + d], fma(c1, gv[u][3 + d], c0 * gv[u][d]));
-                            Y[d] = ((Xi[d] + Xi[d]) + Xj[u][d]) + Xk[u][d];
-                        }
-                        const double dd = wt[u] * fma(gI[2], Y[2], fma(gI[1], Y[1], gI[0] * Y[0]));
-#pragma unroll
-                        for (int d = 0; d < 3; ++d) acc[d] = fma(dd, gI[d], acc[d]);
-                    }
-                }
-                const double *ei = e + 6 * (int64_t)i;
-                const double y0 = fma(ei[2], acc[2], fma(ei[1], acc[1], ei[0] * acc[0]));
-                const double y1 = fma(ei[5], acc[2], fma(ei[4], acc[1], ei[3] * acc[0]));
-                const double2 f = ld2(rhs + 2 * ((int64_t)bc * N + i));
-                const double r0 = f.x - y0, r1 = f.y - y1;
-                if (on) *reinterpret_cast<double2 *>(r64 + 2 * ((int64_t)b * N + i)) = make_double2(r0, r1);
-                term = make_double2(0.0 + (r0 * r0 + r1 * r1), 0.0 + (f.x * f.x + f.y * f.y));
-            }
-            if constexpr (NAT) {
-                sum.x += term.x;
-                sum.y += term.y;
-            } else {
-                sm_merge(k, term, st, sum);
-            }
-        }
-    }
-    lds[wv][lane] = sum;
-    __syncthreads();
-    if (wv == 0 && on) {
-        const double rr = ((lds[0][lane].x + lds[1][lane].x) + lds[2][lane].x) + lds[3][lane].x;
-        const double ff = ((lds[0][lane].y + lds[1][lane].y) + lds[2][lane].y) + lds[3][lane].y;
-        double *o = part + 2 * ((int64_t)b * nblk + rb);
-        o[0] = rr;
-        o[1] = ff;
-    }
-}
-
-// x64 (+)= x_inner as k_outer_update, and X = E x of the same values into the
-// system-interleaved X64t [N][B][3] through a 32-row x 64-system LDS tile
-// (reads along rows, writes along systems with the row's tangent basis as
-// scalar loads, both coalesced). A system not active in the inner solve
-// keeps x64; its X64t gets that value's X.
-template <typename V>
-__global__ __launch_bounds__(kWG) void k_outer_update_t(int32_t N, int32_t B, int32_t first,
-                                                        const V *__restrict__ xin, const int32_t *__restrict__ sysi,
-                                                        const double *__restrict__ e, double *__restrict__ x64,
-                                                        double *__restrict__ X64t) {
-    __shared__ double2 tile[32][65];
-    using V2 = typename VT<V>::V2;
-    const int32_t i0 = blockIdx.x * 32, b0 = blockIdx.y * 64;
-    const int32_t t = threadIdx.x;
-    {
-        const int32_t r = t & 31, sb = t >> 5, i = i0 + r;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int32_t sl = sb + 8 * k, b = b0 + sl;
-            if (b >= B || i >= N) continue;
-            const int64_t vi = (int64_t)b * N + i;
-            double2 x;
-            if (sysi[b * kSysStride + SI_ACTIVE]) {
-                const V2 d = *reinterpret_cast<const V2 *>(xin + 2 * vi);
-                x = first ? make_double2(0.0, 0.0) : *reinterpret_cast<const double2 *>(x64 + 2 * vi);
-                x.x += (double)d.x;
-                x.y += (double)d.y;
-                *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
-            } else {
-                x = *reinterpret_cast<const double2 *>(x64 + 2 * vi);
-            }
-            tile[r][sl] = x;
-        }
-    }
-    __syncthreads();
-    const int32_t sl = t & 63, rq = __builtin_amdgcn_readfirstlane(t >> 6), b = b0 + sl;
-    if (b >= B) return;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int32_t r = rq + 4 * k, i = i0 + r;
-        if (i >= N) break;
-        const double *ei = e + 6 * (int64_t)i;
-        const double2 x = tile[r][sl];
-        double *o = X64t + 3 * ((int64_t)i * B + b);
-#pragma unroll
-        for (int d = 0; d < 3; ++d) o[d] = fma(ei[3 + d], x.y, ei[d] * x.x);
-    }
-}
-
-// dst [N][B] = src [B][N] (row stride N): the batch's I rows interleaved per
-// vertex for k_residual_x3sm, through a 32-row x 64-system LDS tile.
-__global__ __launch_bounds__(kWG) void k_transpose_rows(int32_t N, int32_t B, const double *__restrict__ src,
-                                                        double *__restrict__ dst) {
-    __shared__ double tile[32][65];
-    const int32_t i0 = blockIdx.x * 32, b0 = blockIdx.y * 64;
-    const int32_t t = threadIdx.x;
-    {
-        const int32_t r = t & 31, sb = t >> 5, i = i0 + r;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int32_t sl = sb + 8 * k, b = b0 + sl;
-            if (b < B && i < N) tile[r][sl] = src[(int64_t)b * N + i];
-        }
-    }
-    __syncthreads();
-    const int32_t sl = t & 63, rq = t >> 6, b = b0 + sl;
-    if (b >= B) return;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int32_t r = rq + 4 * k, i = i0 + r;
-        if (i < N) dst[(int64_t)i * B + b] = tile[r][sl];
-    }
-}
-
 // One workgroup per system: relative true residual; retire converged systems.
 template <int NT = kWG>
 __device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, const double *__restrict__ part,
@@ -1655,14 +1380,6 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
 // stored u64 (the fp64 path's residual); auto (sp.fused < 0) on meshes of at
 // most MOF_FUSED_MAX_BLK row blocks (default 16: 4096 vertices), where the
 // eager path is launch-bound.
-// MOF_RES_SM=0: the mixed path keeps k_residual_rcn (A/B; the same bits)
-static bool residual_sm(mof_mesh *m) {
-    const char *v = std::getenv("MOF_RES_SM");
-    if (v && *v == '0') return false;
-    // the slice tables hold up to 8 slots (tw <= aw <= max_w)
-    return !op64(m).u && m->n_own == m->N && m->pat.max_w <= 8 && m->lap64.p;
-}
-
 bool fused_eligible(const mof_mesh *m, const SolveParams &sp, const uint8_t *only) {
     if (sp.fused == 0 || only || sp.precision != MOF_PREC_F64 || sp.amg || sp.fail_at_max_iter) return false;
     if (m->ws.u64_stale || !m->ws.u64.p || m->n_own != m->N) return false;
@@ -1776,18 +1493,6 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     } omega_scope(m, sp.amg_omega, amg);
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
-    // the system-major residual where u is re-formed from the I rows on a
-    // single domain (the mixed path): interleaved x64 / I copies
-    const bool sm = residual_sm(m);
-    const dim3 gt((unsigned)((m->N + 31) / 32), (unsigned)((B + 63) / 64));  // 32-row x 64-system tiles
-    if (sm) {
-        const size_t n = (size_t)m->N * std::max(w.cap, B);
-        if (w.X64t.n < 3 * n) w.X64t.alloc(3 * n);
-        if (w.It.n < n) w.It.alloc(n);
-        MOF_REQUIRE(w.J0 && w.JB >= B, "residual: the batch's I rows are gone");
-        k_transpose_rows<<<gt, kWG, 0, s>>>(m->N, B, w.J0, w.It.p);
-        MOF_HIP(hipGetLastError());
-    }
     int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
     // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
@@ -1799,42 +1504,17 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol, sp, s,
                                 max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg,
                                 o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
-            if (sm)
-                k_outer_update_t<float><<<gt, kWG, 0, s>>>(m->N, B, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                          w.sysi.p, m->e.p, w.x64.p, w.X64t.p);
-            else
-                k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                        w.sysi.p, w.x64.p);
+            k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
+                                                    w.sysi.p, w.x64.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
                                  &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
-            if (sm)
-                k_outer_update_t<double><<<gt, kWG, 0, s>>>(m->N, B, o == 0, w.vx.p, w.sysi.p, m->e.p, w.x64.p,
-                                                           w.X64t.p);
-            else
-                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
-        if (sm) {
-            const OpArgs<double> op = op64(m);
-            static const int smap = [] {
-                const char *v = std::getenv("MOF_RES_SM_MAP");
-                return v && *v ? std::atoi(v) : 0;
-            }();
-            static const bool nat = [] {
-                const char *v = std::getenv("MOF_RES_SM_NAT");
-                return v && *v == '1';
-            }();
-            const int32_t G = (B + 63) / 64;
-            const dim3 gr(smap ? grp_xcd_grid(w.nblk, G) : xcd_grid(w.nblk, G, 0));
-            auto kr = nat ? k_residual_x3sm<8, kSmNB, true> : k_residual_x3sm<8, kSmNB, false>;
-            kr<<<gr, kWG, 0, s>>>(
-                m->N, m->M, w.nblk, B, smap, op.sell_off, op.sell_col, m->lap64.p, op.tsell_off, op.tinc, op.w12, op.gw,
-                op.e, w.It.p, w.X64t.p, w.rhs.p, w.sysi.p, w.r64.p, w.part_rr0.p);
-        } else {
-            launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p, w.r64.p, w.part_rr0.p);
-        }
+        launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
+                                                              w.r64.p, w.part_rr0.p);
         k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
                                                         w.sysi.p);
         MOF_HIP(hipGetLastError());
