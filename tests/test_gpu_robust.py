@@ -201,7 +201,9 @@ def test_c3_bench_config_vs_spsolve():
     """The bench's exact configuration (C3 163,842 vertices, mixed + multigrid,
     the default B = 512: 64 XCD system groups of 8, 16 of 32, symmetric
     operator reads) against the reference's spsolve on two sampled timesteps
-    of the batch (north-star bar 1e-6)."""
+    of the batch (north-star bar 1e-6), and the fp64 relative residual of V
+    against the oracle's own A_k and f_k on eight more timesteps spread over
+    the batch's XCD system groups (one every 64 timesteps)."""
     from scipy.sparse.linalg import spsolve
     p, t, n, a = synth.mesh_for_config("C3")
     T = 513
@@ -217,6 +219,11 @@ def test_c3_bench_config_vs_spsolve():
         err = np.abs(V[k] - Vo).max()
         print("C3 B=512 timestep %d: max|V - V_spsolve| = %.3e (max|V| %.3f)" % (k, err, np.abs(Vo).max()))
         assert err < VTOL, (k, err)
+    for k in range(37, 512, 64):
+        Ao, fo = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
+        rel = np.linalg.norm(fo - Ao @ V[k]) / np.linalg.norm(fo)
+        print("C3 B=512 timestep %d: |f - A V| / |f| = %.3e (oracle A_k, f_k)" % (k, rel))
+        assert rel <= 2e-8, (k, rel)
 
 
 @pytest.mark.slow

@@ -55,7 +55,12 @@ def system(cfg, k=0):
         n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
     else:
         p, t, n, a = synth.mesh_for_config(cfg)
-    I = synth.travelling_wave(p, k + 2)
+    # the bench's signal for the config (synth.config_wave: on the S1-like
+    # patches a wave across the grid), PROTO_PINWHEEL=1: the atan2 pinwheel
+    if os.environ.get("PROTO_PINWHEEL") == "1" or cfg.startswith("ico"):
+        I = synth.travelling_wave(p, k + 2)
+    else:
+        I = synth.config_wave(cfg, p, k + 2)
     a2, gw, e, iw = oracle.geometry(p, n, t, a)
     A, f = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
     N = len(p)
