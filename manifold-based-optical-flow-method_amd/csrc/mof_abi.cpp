@@ -577,7 +577,7 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
 
 extern "C" {
 
-const char *mof_version(void) { return "mofhip 0.3 (gfx950, abi 2)"; }
+const char *mof_version(void) { return "mofhip 0.4 (gfx950, abi 3)"; }
 
 int mof_abi_version(void) { return MOF_ABI_VERSION; }
 
