@@ -9,4 +9,5 @@ S=tools/gpu_step.sh
 $S 200 $o/e2e_1.json python3 tools/s3_end_to_end.py S1s C1 || exit 99
 $S 200 $o/e2e_2.json python3 tools/s3_end_to_end.py S1s C1 || exit 99
 MOF_PRECISION=mixed $S 200 $o/e2e_mixed.json python3 tools/s3_end_to_end.py S1s C1 || exit 99
+MOF_PRECISION=f64 $S 200 $o/e2e_f64.json python3 tools/s3_end_to_end.py S1s C1 || exit 99
 bash tools/r04_call10.sh || exit 99
