@@ -112,11 +112,23 @@ int env_int(const char *name, int dflt) {
 
 // Pinned ring, copy stream and the two device slots of a host-pointer solve
 // (mof_hostio.h); kept on the handle across calls.
+// The ring's chunk follows the job: a quarter of the larger per-batch
+// transfer in whole MiB, at most MOF_STAGE_MB (32): pinning the 4 x 32 MiB
+// ring took tens of ms -- longer than a 3k-vertex, 97-timestep job's whole
+// solve -- and a small job's transfers fit a few MiB; a later, larger job
+// replaces the ring.
 void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
+    const size_t mib = (size_t)1 << 20, cap = (size_t)std::max(1, env_int("MOF_STAGE_MB", 32)) * mib;
+    const size_t quarter = (size_t)std::max(in_elems, out_elems) * sizeof(double) / 4;
+    const size_t want = std::min(cap, std::max(mib, (quarter + mib - 1) / mib * mib));
+    if (m->stage && m->stage->chunk() < want) {
+        delete m->stage;  // synchronises its copy stream
+        m->stage = nullptr;
+    }
     if (!m->stage) {
-        m->stage = new mof::HostStage((size_t)env_int("MOF_STAGE_MB", 32) << 20, mof::stage_threads());
+        m->stage = new mof::HostStage(want, mof::stage_threads());
         for (auto &e : m->hev) {
-            MOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            if (!e) MOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             MOF_HIP(hipEventRecord(e, m->stage->stream()));  // every wait has a recorded event
         }
     }
@@ -136,31 +148,50 @@ void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
 // and 3419 vs 3463 at B = 256: the latency-bound setup kernels beside the
 // other batch's bandwidth-bound sweeps slow both.
 void solve_batches(mof_mesh *m, const double *I, const double *I2, const double *t_k, int32_t k0, int32_t k1,
-                   int32_t B, double lambda, const mof::SolveParams &sp, const mof_opts &o, bool recovery,
+                   int32_t B, double lambda, const mof::SolveParams &sp_in, const mof_opts &o, bool recovery,
                    bool dev_io, hipStream_t s, double *V_out, mof_stats &st, mof::SpmvTiming &timing) {
+    mof::SolveParams sp = sp_in;
     const int32_t K = k1 - k0;
     const int32_t nbat = (K + B - 1) / B;
+    // MOF_HOSTIO_VERBOSE: helper-thread and wait times, and the call's setup
+    // steps, on stderr
+    const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
+    double tp[5];
+    tp[0] = now_ms();
     mof::ensure_workspace(m, B, sp.precision);
     mof::Workspace &w = m->ws;
     const int64_t N = m->N;
     Events ev;
     mof::prepare_operator(m, lambda, s);
+    tp[1] = now_ms();
     // multigrid hierarchy before the first assembly (which writes the
     // level-0 smoother's bf16 copies)
     const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && mof::amg_build(m);
+    tp[2] = now_ms();
     if (amg) mof::amg_ensure(m, B);
+    // irregular or open meshes (the smoothed-prolongator hierarchies): the
+    // first refinement step's inner solve to 1e-5 instead of 1e-4 (unless the
+    // caller set one) -- it leaves the second step with the outer target in
+    // reach, so a third step (and its fp64 residual) is rarely needed: S1
+    // 857 -> 889, R3 702 -> 717 timesteps/s; on the regular meshes the
+    // deeper first step only adds iterations (C3 17.0 -> 18.0 its, -5 %;
+    // profiles/r04_ab/call10/)
+    if (amg && o.inner_rtol <= 0 && !mof::amg_fine(m).regular) sp.inner_rtol = 1e-5;
+    tp[3] = now_ms();
     // host pointers: one upload of the nb+1 rows when I2 is I (S3
     // passes I_k twice), else nb rows of each
     const bool shared_I = (I2 == I);
     const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
     if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B);
+    tp[4] = now_ms();
+    if (hostio_verbose)
+        fprintf(stderr, "[mof setup] workspace + operator %.2f ms, hierarchy %.2f ms, its storage %.2f ms, host staging %.2f ms\n",
+                tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3]);
     auto bk = [&](int32_t q) { return k0 + q * B; };
     auto bn = [&](int32_t q) { return std::min(B, k1 - bk(q)); };
     // helper-thread steps of the host pipeline (copy stream): batch q's I rows
     // into slot q&1 once batch q-2's assembly has read it, and batch q's V
     // out of slot q&1 into V_out
-    // MOF_HOSTIO_VERBOSE: helper-thread and wait times on stderr
-    const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
     double t_in = 0.0, t_out = 0.0, t_wait = 0.0;
     const double t_call = now_ms();
     mof::g_fetch_ms = 0.0;

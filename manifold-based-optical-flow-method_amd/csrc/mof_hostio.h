@@ -54,6 +54,7 @@ class HostStage {
     HostStage(const HostStage &) = delete;
     HostStage &operator=(const HostStage &) = delete;
     hipStream_t stream() const { return cs_; }
+    size_t chunk() const { return chunk_; }
     // Enqueue pageable src -> device dst on the copy stream (returns once
     // every chunk is in pinned memory and its DMA is queued).
     void h2d(void *dst_dev, const void *src, size_t bytes);
