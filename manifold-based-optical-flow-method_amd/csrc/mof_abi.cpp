@@ -126,7 +126,8 @@ void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
         m->stage = nullptr;
     }
     if (!m->stage) {
-        m->stage = new mof::HostStage(want, mof::stage_threads());
+        // copy threads: one per MiB of a chunk, at most stage_threads()
+        m->stage = new mof::HostStage(want, std::min<int32_t>(mof::stage_threads(), (int32_t)(want / mib)));
         for (auto &e : m->hev) {
             if (!e) MOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             MOF_HIP(hipEventRecord(e, m->stage->stream()));  // every wait has a recorded event
@@ -169,14 +170,15 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && mof::amg_build(m);
     tp[2] = now_ms();
     if (amg) mof::amg_ensure(m, B);
-    // irregular or open meshes (the smoothed-prolongator hierarchies): the
-    // first refinement step's inner solve to 1e-5 instead of 1e-4 (unless the
-    // caller set one) -- it leaves the second step with the outer target in
-    // reach, so a third step (and its fp64 residual) is rarely needed: S1
-    // 857 -> 889, R3 702 -> 717 timesteps/s; on the regular meshes the
-    // deeper first step only adds iterations (C3 17.0 -> 18.0 its, -5 %;
-    // profiles/r04_ab/call10/)
-    if (amg && o.inner_rtol <= 0 && !mof::amg_fine(m).regular) sp.inner_rtol = 1e-5;
+    // large irregular or open meshes (the smoothed-prolongator hierarchies):
+    // the first refinement step's inner solve to 1e-5 instead of 1e-4
+    // (unless the caller set one) -- it leaves the second step with the outer
+    // target in reach, so a third step (and its fp64 residual) is rarely
+    // needed: S1 857 -> 889, R3 702 -> 717 timesteps/s; on the regular meshes
+    // the deeper first step only adds iterations (C3 17.0 -> 18.0 its, -5 %;
+    // profiles/r04_ab/call10/), and on a small one (S1s, 3,249 vertices,
+    // 30137 -> 28329) a third step costs less than the extra iterations
+    if (amg && o.inner_rtol <= 0 && !mof::amg_fine(m).regular && m->N >= 16384) sp.inner_rtol = 1e-5;
     tp[3] = now_ms();
     // host pointers: one upload of the nb+1 rows when I2 is I (S3
     // passes I_k twice), else nb rows of each
