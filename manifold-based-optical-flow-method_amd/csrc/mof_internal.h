@@ -231,11 +231,6 @@ struct mof_mesh {
     int64_t blocks_read = 0;          // blocks an fp32 / bf16 operator pass reads per system
     bool sym_reads = false;           // the mirror table transposes lower blocks
     mof::DevArray<double> e, gw, iw, area, a2;  // a2: [sell_nb][4] (unscaled, bit-exact)
-    // the re-forming fp64 residual's per-incidence geometry in the incidence
-    // SELL order, plane-major [kRgeoPlanes][tsell_nb]: the triangle's hat
-    // gradients, the tangent bases of the corner's two other vertices and
-    // A_T/12 (mof_pcg.hip residual_geometry), built on first use
-    mof::DevArray<double> rgeo;
     // operator copies: lambda*a2 (cached per lambda) and A_T/12 with a zero slot M
     mof::DevArray<double> a2s64, w12_64;
     mof::DevArray<float> a2s32, w12_32;

@@ -356,99 +356,6 @@ __device__ __forceinline__ void apply_row_rcn(const OpArgs<double> &op, const in
     }
 }
 
-// The same row with the incidences' geometry read from the mesh's rgeo
-// planes (one coalesced read per value and slot) instead of gathered per lane
-// -- 9 hat-gradient values of the triangle, 6 + 6 tangent-basis values of the
-// corner's two other vertices and A_T/12 -- the same values, so the same
-// arithmetic and bits as apply_row_rcn. k_residual_rcn spent 65 % of its
-// wave cycles waiting on those gathers (each lane a different triangle /
-// vertex: ~10 loads of 64 scattered lines per incidence).
-constexpr int kRgeoPlanes = 22;
-template <int NS>
-__device__ __forceinline__ void apply_row_rcn_soa(const OpArgs<double> &op, const double *__restrict__ rgeo,
-                                                  int64_t tnb, const int32_t (&bs)[NS], int32_t i,
-                                                  const double *__restrict__ x64, double (&y)[NS][2]) {
-#pragma clang fp contract(off)
-    const int32_t s = i >> 6, l = i & 63;
-    double acc[NS][2];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) acc[t][0] = acc[t][1] = 0.0;
-    rcn_a2<NS>(op, bs, i, x64, acc);
-    RcnRow<NS> R;
-    rcn_row<NS>(op, bs, i, x64, R);
-    const int32_t o = op.tsell_off[s];
-    const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
-    for (int32_t t0 = 0; t0 < w; ++t0) {
-        const int64_t p = (int64_t)o + t0 * kSlice + l;
-        const int4 q = op.tinc[p];
-        double g[9], ej[6], ek[6];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) g[k] = rgeo[k * tnb + p];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            ej[k] = rgeo[(9 + k) * tnb + p];
-            ek[k] = rgeo[(15 + k) * tnb + p];
-        }
-        const double wt = rgeo[21 * tnb + p];
-        double Ij[NS], Ik[NS];
-        double2 xj[NS], xk[NS];
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const double *Ib = op.I0 + (int64_t)bs[t] * op.ldI;
-            const int64_t vb = (int64_t)bs[t] * op.N;
-            Ij[t] = Ib[q.z];
-            Ik[t] = Ib[q.w];
-            xj[t] = ld2(x64 + 2 * (vb + q.z));
-            xk[t] = ld2(x64 + 2 * (vb + q.w));
-        }
-        const int c = q.y;
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            const double c0 = c == 0 ? R.Ii[t] : (c == 1 ? Ik[t] : Ij[t]);
-            const double c1 = c == 0 ? Ij[t] : (c == 1 ? R.Ii[t] : Ik[t]);
-            const double c2 = c == 0 ? Ik[t] : (c == 1 ? Ij[t] : R.Ii[t]);
-            double gI[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) gI[d] = (c0 * g[d] + c1 * g[3 + d]) + c2 * g[6 + d];
-            const double2 ui = make_double2(dot3_np(gI, R.ei), dot3_np(gI, R.ei + 3));
-            const double2 uj = make_double2(dot3_np(gI, ej), dot3_np(gI, ej + 3));
-            const double2 uk = make_double2(dot3_np(gI, ek), dot3_np(gI, ek + 3));
-            const double si = ui.x * R.xi[t].x + ui.y * R.xi[t].y;
-            const double sj = uj.x * xj[t].x + uj.y * xj[t].y;
-            const double sk = uk.x * xk[t].x + uk.y * xk[t].y;
-            const double cc = wt * ((si + si) + sj + sk);
-            acc[t][0] += ui.x * cc;
-            acc[t][1] += ui.y * cc;
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        y[t][0] = acc[t][0];
-        y[t][1] = acc[t][1];
-    }
-}
-
-// rgeo planes of every incidence slot (padding slots: T = M -> the clamped
-// triangle M-1's gradients, A/12 = 0, as rcn_tri reads them)
-__global__ __launch_bounds__(kWG) void k_residual_geometry(int64_t tnb, int32_t M, const int4 *__restrict__ tinc,
-                                                           const double *__restrict__ gw,
-                                                           const double *__restrict__ e,
-                                                           const double *__restrict__ w12,
-                                                           double *__restrict__ rgeo) {
-    const int64_t p = (int64_t)blockIdx.x * kWG + threadIdx.x;
-    if (p >= tnb) return;
-    const int4 q = tinc[p];
-    const int64_t T = min(q.x, M - 1);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) rgeo[k * tnb + p] = gw[9 * T + k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        rgeo[(9 + k) * tnb + p] = e[6 * (int64_t)q.z + k];
-        rgeo[(15 + k) * tnb + p] = e[6 * (int64_t)q.w + k];
-    }
-    rgeo[21 * tnb + p] = w12[q.x];
-}
-
 constexpr int kForce = 1;  // bench: ignore convergence / activity flags
 
 
@@ -916,9 +823,8 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
 // staged in LDS and added by the row's thread in slot order (bit-identical):
 // 8421 / 5539 vs 5093 us per launch.
 constexpr int kResNS = 2;
-template <int NS, bool SOA>
-__global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, const double *__restrict__ rgeo, int64_t tnb,
-                                                      int32_t nblk, int32_t B, RedArgs rd,
+template <int NS>
+__global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
                                                       const int32_t *__restrict__ sysi,
@@ -945,10 +851,7 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, const d
         const int32_t i = rb * kRowsPerWG + r * kWG + threadIdx.x;
         if (i >= N) break;
         double y[NS][2];
-        if constexpr (SOA)
-            apply_row_rcn_soa<NS>(op, rgeo, tnb, bs, i, x64, y);
-        else
-            apply_row_rcn<NS>(op, bs, i, x64, y);
+        apply_row_rcn<NS>(op, bs, i, x64, y);
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
             const int64_t vi = (int64_t)bs[t] * N + i;
@@ -1081,35 +984,14 @@ MatArgs<V> make_mat(mof_mesh *m, const V *A) {
 // -- the residuals went 2 x 5.7 -> 2 x 3.6 ms per 512-system batch, the
 // assembly 11.4 -> 15.6 ms (fp64 accumulators: 165 VGPRs, 3 waves, and
 // 10.7 GB of A64 stores): C3 3380-3383 vs 3378-3389 timesteps/s.
-// The re-forming residual's incidence geometry (mof_mesh::rgeo), built on
-// first use: 176 B per incidence slot (C3: 173 MB), mesh constants.
-// MOF_RES_GATHER=1: the per-lane gathers instead (A/B; the same bits).
-const double *residual_geometry(mof_mesh *m, hipStream_t s) {
-    const char *v = std::getenv("MOF_RES_GATHER");
-    if (v && *v == '1') return nullptr;
-    const int64_t tnb = m->pat.tsell_nb();
-    if (m->rgeo.n < (size_t)(kRgeoPlanes * tnb)) {
-        m->rgeo.alloc((size_t)(kRgeoPlanes * tnb));
-        k_residual_geometry<<<dim3((unsigned)((tnb + kWG - 1) / kWG)), kWG, 0, s>>>(
-            tnb, m->M, reinterpret_cast<const int4 *>(m->tinc.p), m->gw.p, m->e.p, m->w12_64.p, m->rgeo.p);
-        MOF_HIP(hipGetLastError());
-    }
-    return m->rgeo.p;
-}
-
 template <typename... Args>
 void launch_residual(mof_mesh *m, int32_t nblk, int32_t B, hipStream_t s, RedArgs rd, Args... args) {
     const OpArgs<double> op = op64(m);
-    if (op.u) {
+    if (op.u)
         k_residual<<<dim3(xcd_grid(nblk, B, kGrpRes)), kWG, 0, s>>>(op, nblk, B, rd, args...);
-        return;
-    }
-    const dim3 g(xcd_grid(nblk, (B + kResNS - 1) / kResNS, kGrpRes));
-    const int64_t tnb = m->pat.tsell_nb();
-    if (const double *rgeo = residual_geometry(m, s))
-        k_residual_rcn<kResNS, true><<<g, kWG, 0, s>>>(op, rgeo, tnb, nblk, B, rd, args...);
     else
-        k_residual_rcn<kResNS, false><<<g, kWG, 0, s>>>(op, nullptr, tnb, nblk, B, rd, args...);
+        k_residual_rcn<kResNS><<<dim3(xcd_grid(nblk, (B + kResNS - 1) / kResNS, kGrpRes)), kWG, 0, s>>>(
+            op, nblk, B, rd, args...);
 }
 
 template <typename V>
