@@ -115,19 +115,21 @@ int env_int(const char *name, int dflt) {
 // The ring's chunk follows the job: a quarter of the larger per-batch
 // transfer in whole MiB, at most MOF_STAGE_MB (32): pinning the 4 x 32 MiB
 // ring took tens of ms -- longer than a 3k-vertex, 97-timestep job's whole
-// solve -- and a small job's transfers fit a few MiB; a later, larger job
-// replaces the ring.
+// solve. Transfers of at most MOF_STAGE_DIRECT_MB (16) go straight from / to
+// pageable memory (the runtime stages them; no ring to pin). A later, larger
+// job replaces the stage.
 void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
     const size_t mib = (size_t)1 << 20, cap = (size_t)std::max(1, env_int("MOF_STAGE_MB", 32)) * mib;
-    const size_t quarter = (size_t)std::max(in_elems, out_elems) * sizeof(double) / 4;
-    const size_t want = std::min(cap, std::max(mib, (quarter + mib - 1) / mib * mib));
+    const size_t direct = (size_t)std::max(0, env_int("MOF_STAGE_DIRECT_MB", 16)) * mib;
+    const size_t larger = (size_t)std::max(in_elems, out_elems) * sizeof(double);
+    const size_t want = larger <= direct ? 0 : std::min(cap, (larger / 4 + mib - 1) / mib * mib);
     if (m->stage && m->stage->chunk() < want) {
         delete m->stage;  // synchronises its copy stream
         m->stage = nullptr;
     }
     if (!m->stage) {
         // copy threads: one per MiB of a chunk, at most stage_threads()
-        m->stage = new mof::HostStage(want, std::min<int32_t>(mof::stage_threads(), (int32_t)(want / mib)));
+        m->stage = new mof::HostStage(want, std::max<int32_t>(1, std::min<int32_t>(mof::stage_threads(), (int32_t)(want / mib))));
         for (auto &e : m->hev) {
             if (!e) MOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             MOF_HIP(hipEventRecord(e, m->stage->stream()));  // every wait has a recorded event

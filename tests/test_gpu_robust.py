@@ -162,26 +162,23 @@ def test_symmetric_reads_match_spsolve(precond, monkeypatch):
     assert np.abs(out["0"][0] - out["1"][0]).max() < 5e-7 * np.abs(out["0"][0]).max()
 
 
+@pytest.mark.parametrize("direct", [False, True])
 @pytest.mark.parametrize("same_I2", [True, False])
-def test_host_pipeline_matches_device_path(same_I2):
+def test_host_pipeline_matches_device_path(same_I2, direct, monkeypatch):
     """Host pointers over several batches (double-buffered copy stream,
-    pinned ring smaller than a batch) give the device-pointer path's bits."""
+    pinned ring smaller than a batch; or, for transfers this small by
+    default, straight pageable copies) give the device-pointer path's bits."""
     import torch
     p, t, n, a = synth.mesh_for_config("C2")
     T = 45
     I = synth.travelling_wave(p, T)
     I2 = I if same_I2 else np.ascontiguousarray(I[::-1] * 0.5 + 0.25)
     tk = np.arange(float(T))
-    old = os.environ.get("MOF_STAGE_MB")
-    os.environ["MOF_STAGE_MB"] = "4"  # ring chunks far smaller than one batch's 20 MB
-    try:
-        m = DeviceMesh(p, n, t, a)
-        Vh, sh = m.solve_range(I, tk, 2, T - 1, 0.01, I2=I2, precision="mixed", precond="amg", batch=16)
-    finally:
-        if old is None:
-            os.environ.pop("MOF_STAGE_MB")
-        else:
-            os.environ["MOF_STAGE_MB"] = old
+    # ring chunks (1 MB) far smaller than one batch's 4.4 / 8.3 MB transfers
+    monkeypatch.setenv("MOF_STAGE_DIRECT_MB", "16" if direct else "0")
+    monkeypatch.setenv("MOF_STAGE_MB", "1")
+    m = DeviceMesh(p, n, t, a)
+    Vh, sh = m.solve_range(I, tk, 2, T - 1, 0.01, I2=I2, precision="mixed", precond="amg", batch=16)
     dev = torch.device("cuda", 0)
     Id = torch.from_numpy(I).to(dev)
     I2d = torch.from_numpy(I2).to(dev) if not same_I2 else Id
