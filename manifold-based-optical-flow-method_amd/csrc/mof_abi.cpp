@@ -115,19 +115,17 @@ int env_int(const char *name, int dflt) {
 // The ring's chunk follows the job: a quarter of the larger per-batch
 // transfer in whole MiB, at most MOF_STAGE_MB (32): pinning the 4 x 32 MiB
 // ring took tens of ms -- longer than a 3k-vertex, 97-timestep job's whole
-// solve. Transfers of at most MOF_STAGE_DIRECT_MB (16) go straight from / to
-// pageable memory (the runtime stages them; no ring to pin). A later, larger
-// job replaces the stage.
-void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems) {
+// solve. A later, larger job replaces the stage. direct: only the device
+// slots (the batches' copies run on the compute stream, solve_batches).
+void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems, bool direct) {
     const size_t mib = (size_t)1 << 20, cap = (size_t)std::max(1, env_int("MOF_STAGE_MB", 32)) * mib;
-    const size_t direct = (size_t)std::max(0, env_int("MOF_STAGE_DIRECT_MB", 16)) * mib;
     const size_t larger = (size_t)std::max(in_elems, out_elems) * sizeof(double);
-    const size_t want = larger <= direct ? 0 : std::min(cap, (larger / 4 + mib - 1) / mib * mib);
-    if (m->stage && m->stage->chunk() < want) {
+    const size_t want = std::min(cap, (larger / 4 + mib - 1) / mib * mib);
+    if (!direct && m->stage && m->stage->chunk() < want) {
         delete m->stage;  // synchronises its copy stream
         m->stage = nullptr;
     }
-    if (!m->stage) {
+    if (!direct && !m->stage) {
         // copy threads: one per MiB of a chunk, at most stage_threads()
         m->stage = new mof::HostStage(want, std::max<int32_t>(1, std::min<int32_t>(mof::stage_threads(), (int32_t)(want / mib))));
         for (auto &e : m->hev) {
@@ -186,7 +184,13 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     // passes I_k twice), else nb rows of each
     const bool shared_I = (I2 == I);
     const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
-    if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B);
+    // host transfers of at most MOF_STAGE_DIRECT_MB (16) per batch: straight
+    // pageable copies on the compute stream (the runtime stages them), no
+    // copy stream, helper thread or pinned ring -- creating those cost a
+    // small job 4-12 ms, more than its solve (S1s: 3.8 ms)
+    const bool direct = !dev_io && (size_t)std::max(in_rows, 2 * (int64_t)B) * N * sizeof(double) <=
+                                       ((size_t)std::max(0, env_int("MOF_STAGE_DIRECT_MB", 16)) << 20);
+    if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B, direct);
     tp[4] = now_ms();
     if (hostio_verbose)
         fprintf(stderr, "[mof setup] workspace + operator %.2f ms, hierarchy %.2f ms, its storage %.2f ms, host staging %.2f ms\n",
@@ -233,7 +237,7 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     // declared after everything its tasks reference: its destructor
     // waits for a task still running when an error unwinds
     std::future<void> io;
-    if (!dev_io) io = std::async(std::launch::async, [&] { stage_in(0); });
+    if (!dev_io && !direct) io = std::async(std::launch::async, [&] { stage_in(0); });
     for (int32_t q = 0; q < nbat; ++q) {
         const int32_t k = bk(q), nb = bn(q), sl = q & 1;
         for (int32_t b = 0; b < nb; ++b) dts[b] = t_k[k + b + 1] - t_k[k + b];
@@ -242,6 +246,17 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
         if (dev_io) {
             I0p = I + (int64_t)k * N;
             I1p = I2 + (int64_t)(k + 1) * N;
+        } else if (direct) {
+            double *hin = m->hin[0].p;
+            if (shared_I) {
+                MOF_HIP(hipMemcpyAsync(hin, I + (int64_t)k * N, sizeof(double) * N * (nb + 1), hipMemcpyHostToDevice, s));
+            } else {
+                MOF_HIP(hipMemcpyAsync(hin, I + (int64_t)k * N, sizeof(double) * N * nb, hipMemcpyHostToDevice, s));
+                MOF_HIP(hipMemcpyAsync(hin + N * B, I2 + (int64_t)(k + 1) * N, sizeof(double) * N * nb,
+                                       hipMemcpyHostToDevice, s));
+            }
+            I0p = hin;
+            I1p = shared_I ? I0p + N : I0p + N * B;
         } else {
             const double tw = now_ms();
             io.get();  // batch q staged, batch q-1 drained
@@ -257,7 +272,7 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
         }
         MOF_HIP(hipEventRecord(ev.e[0], s));
         mof::launch_assemble(m, nb, I0p, I1p, N, sp.block_jacobi, sp.precision, s, amg);
-        if (!dev_io) MOF_HIP(hipEventRecord(m->hev[2 + sl], s));
+        if (!dev_io && !direct) MOF_HIP(hipEventRecord(m->hev[2 + sl], s));
         MOF_HIP(hipEventRecord(ev.e[1], s));
         int32_t outer = 0;
         st.iterations += mof::solve_batch(m, nb, sp, s, &outer, &st.max_iterations, &timing);
@@ -274,9 +289,13 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
                     return mof::solve_batch(m, nb, rp, s, &outer_r, &st.max_iterations, nullptr, on);
                 },
                 [&] { mof::release_f64_terms(m); });
-        double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[sl].p;
+        double *Vdst = dev_io ? V_out + (int64_t)(k - k0) * 2 * N : m->hout[direct ? 0 : sl].p;
         mof::launch_to_planar(m, nb, Vdst, s);
-        if (!dev_io) MOF_HIP(hipEventRecord(m->hev[4 + sl], s));
+        if (direct)
+            MOF_HIP(hipMemcpyAsync(V_out + (int64_t)(k - k0) * 2 * N, Vdst, sizeof(double) * 2 * N * nb,
+                                   hipMemcpyDeviceToHost, s));
+        else if (!dev_io)
+            MOF_HIP(hipEventRecord(m->hev[4 + sl], s));
         MOF_HIP(hipEventRecord(ev.e[2], s));
         MOF_HIP(hipEventSynchronize(ev.e[2]));
         st.ms_assembly += ev.ms(0, 1);
@@ -287,10 +306,10 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
         }
         st.batches++;
     }
-    if (dev_io && hostio_verbose)
-        fprintf(stderr, "[mof hostio] device K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n", K, B,
-                now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
-    if (!dev_io) {
+    if ((dev_io || direct) && hostio_verbose)
+        fprintf(stderr, "[mof hostio] %s K=%d B=%d: call %.1f ms, %lld flag fetches %.1f ms\n",
+                dev_io ? "device" : "direct", K, B, now_ms() - t_call, (long long)mof::g_fetch_n, mof::g_fetch_ms);
+    if (!dev_io && !direct) {
         if (io.valid()) io.get();
         drain_out(nbat - 1);
         if (hostio_verbose)

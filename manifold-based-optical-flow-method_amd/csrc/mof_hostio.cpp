@@ -88,7 +88,6 @@ int32_t stage_threads() {
 
 HostStage::HostStage(size_t chunk_bytes, int32_t threads) : chunk_(chunk_bytes), pool_(threads) {
     MOF_HIP(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
-    if (chunk_ == 0) return;  // direct: pageable copies, no ring
     for (int k = 0; k < kSlots; ++k) {
         MOF_HIP(hipHostMalloc(&pin_[k], chunk_, hipHostMallocDefault));
         MOF_HIP(hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming));
@@ -113,10 +112,6 @@ int32_t HostStage::take_slot() {
 }
 
 void HostStage::h2d(void *dst_dev, const void *src, size_t bytes) {
-    if (chunk_ == 0) {  // the runtime stages a pageable source itself
-        MOF_HIP(hipMemcpyAsync(dst_dev, src, bytes, hipMemcpyHostToDevice, cs_));
-        return;
-    }
     for (size_t o = 0; o < bytes; o += chunk_) {
         const size_t len = std::min(chunk_, bytes - o);
         const int32_t k = take_slot();
@@ -129,11 +124,6 @@ void HostStage::h2d(void *dst_dev, const void *src, size_t bytes) {
 
 void HostStage::d2h(void *dst, const void *src_dev, size_t bytes, hipEvent_t ready) {
     if (ready) MOF_HIP(hipStreamWaitEvent(cs_, ready, 0));
-    if (chunk_ == 0) {
-        MOF_HIP(hipMemcpyAsync(dst, src_dev, bytes, hipMemcpyDeviceToHost, cs_));
-        MOF_HIP(hipStreamSynchronize(cs_));
-        return;
-    }
     const size_t nch = (bytes + chunk_ - 1) / chunk_;
     // keep up to kSlots - 1 chunk DMAs in flight ahead of the host copy
     std::vector<int32_t> slot(nch);
