@@ -312,3 +312,29 @@ def test_damped_multigrid_recovery_on_pinwheel_patch(monkeypatch):
         A, f = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
         Vo = spsolve(A.tocsc(), f)
         assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
+
+
+def test_large_irregular_mesh_default_schedule():
+    """A large irregular mesh (smoothed-prolongator hierarchy, >= 16,384
+    vertices) runs its first inner solve to 1e-5 by default:
+    V still meets the bar against the reference's spsolve on sampled
+    timesteps, and an explicit inner_rtol = 1e-4 gives the same V within the
+    solve's tolerance."""
+    from scipy.sparse.linalg import spsolve
+    p, t = synth.random_sphere(20000, 10.0, seed=5)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    T = 9
+    I = synth.travelling_wave(p, T)
+    tk = np.arange(float(T))
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg")
+    assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
+    V4, st4 = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", inner_rtol=1e-4)
+    assert st4["failed"] == 0 and st4["max_rel_residual"] <= 1e-8
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    for k in (0, T - 2):
+        Ao, fo = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
+        Vo = spsolve(Ao.tocsc(), fo)
+        scale = max(1.0, np.abs(Vo).max())
+        assert np.abs(V[k] - Vo).max() < VTOL * scale, k
+        assert np.abs(V4[k] - Vo).max() < VTOL * scale, k
