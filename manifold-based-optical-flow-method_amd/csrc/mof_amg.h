@@ -83,9 +83,6 @@ struct AmgDevLevel {
     int64_t sell_nb = 0;
     DevArray<int32_t> sell_off, sell_col, sell_row, diag_pos;  // level >= 1
     DevArray<uint8_t> dead;                          // level >= 1
-    // level >= 1 with a sweep copy: the mirror table of its SELL layout (a
-    // lower block read as the transposed upper twin, MOF_COARSE_SYM), or empty
-    DevArray<int32_t> mir;
     DevArray<int32_t> agg, mptr, mlist, apos, gptr, gent;  // transition to level + 1
     DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
     DevArray<int32_t> ggrp;                         // level 0, tentative P: Galerkin groups (coarse

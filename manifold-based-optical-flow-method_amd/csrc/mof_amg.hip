@@ -665,7 +665,6 @@ struct Lvl {
     const uint16_t *Dh22;                // and entry (2,2)
     const uint4 *Ah;                     // bf16 A for the sweeps: [B][sell_nb] entries 0..7, or null
     const uint16_t *Ah22;                // [B][sell_nb] entry (2,2)
-    const int32_t *mir;                  // sweep copy read through the mirror table, or null
     float *b, *x, *r, *y;                // [B][n][4] (level 0: x [B][n][2], r bf16 [B][n][2])
     const int32_t *agg, *mptr, *apos;    // transition to level + 1
     const int32_t *mlist;                // aggregate members (level 0: r1 gathered in member order)
@@ -699,15 +698,6 @@ __device__ __forceinline__ void ld_a9(const uint4 *H, const uint16_t *H22, int64
             a[e / 3][e % 3] = (float)((int32_t)((w[e >> 2] >> (8 * (e & 3))) & 0xffu) - 128) * sc;
     }
 }
-// the same block transposed (a lower block read as its upper twin)
-__device__ __forceinline__ void ld_a9t(const uint4 *H, const uint16_t *H22, int64_t q, float (&a)[3][3]) {
-    float t[3][3];
-    ld_a9(H, H22, q, t);
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) a[r][c] = t[c][r];
-}
 // the smoother's 3x3 D^-1 of node i of system b
 __device__ __forceinline__ void ld_dh(const Lvl &L, int32_t b, int32_t i, float (&d)[3][3]) {
     ld_h9(L.Dh, L.Dh22, (int64_t)b * L.n + i, d);
@@ -724,39 +714,6 @@ __device__ __forceinline__ void spmv_row3(const Lvl &L, int32_t b, int32_t i, co
     const int32_t s = i >> 6, l = i & 63;
     const int32_t o = L.sell_off[s], w = (L.sell_off[s + 1] - o) >> 6;
     acc[0] = acc[1] = acc[2] = 0.f;
-    if (half && L.mir) {
-        // symmetric reads: a lower block as its upper twin transposed
-        // (padding: the row's diagonal, masked)
-        for (int32_t t0 = 0; t0 < w; t0 += U) {
-            int32_t j[U], mr[U];
-            float a[U][3][3], xj[U][3];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t pos = (int64_t)o + min(t0 + u, w - 1) * kSlice + l;
-                j[u] = L.sell_col[pos];
-                mr[u] = L.mir[pos];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t q = hb + mir_pos(mr[u], (int64_t)o + l);
-                if (mr[u] >= 0 && (mr[u] & kMirT))
-                    ld_a9t(L.Ah, L.Ah22, q, a[u]);
-                else
-                    ld_a9(L.Ah, L.Ah22, q, a[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) ldv<3>(xb, j[u], xj[u]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool on = t0 + u < w && mr[u] >= 0;
-                float ax[3];
-                matvec<3>(a[u], xj[u], ax);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) acc[c] += on ? ax[c] : 0.f;
-            }
-        }
-        return;
-    }
     for (int32_t t0 = 0; t0 < w; t0 += U) {
         int32_t j[U];
         float a[U][3][3], xj[U][3];
@@ -1382,29 +1339,6 @@ MatH level0_mat(mof_mesh *m) {
 
 // ---- host side ---------------------------------------------------------------
 
-// The mirror table of a coarse level's SELL layout (as sell_mirror for the
-// fine pattern): position of the block itself, or of its upper twin (j, i)
-// with kMirT for a lower block (j < i); -1 for padding. The coarse patterns
-// are symmetric (Galerkin products of a symmetric one).
-static std::vector<int32_t> coarse_mirror(const AmgLevel &L) {
-    const int64_t snb = L.sell_nb();
-    MOF_REQUIRE(snb < kMirT, "coarse SELL layout too large for the mirror table");
-    std::vector<int32_t> mir((size_t)snb, -1);
-    auto pos_of = [&](int32_t i, int32_t j) -> int64_t {
-        const auto b = L.vcol.begin() + L.vptr[i], e = L.vcol.begin() + L.vptr[i + 1];
-        const auto it = std::lower_bound(b, e, j);
-        MOF_REQUIRE(it != e && *it == j, "coarse pattern not symmetric");
-        const int32_t t = (int32_t)(it - b), td = (int32_t)(std::lower_bound(b, e, i) - b);
-        return L.sell_off[i / kSlice] + (int64_t)sell_slot(t, td) * kSlice + i % kSlice;
-    };
-    for (int64_t pos = 0; pos < snb; ++pos) {
-        if (L.sell_blk[pos] < 0) continue;
-        const int32_t i = L.sell_row[pos], j = L.sell_col[pos];
-        mir[pos] = j < i ? (int32_t)pos_of(j, i) | kMirT : (int32_t)pos;
-    }
-    return mir;
-}
-
 bool amg_build(mof_mesh *m) {
     AmgParams prm;
     // an open surface (boundary edges: 3 M != 2 E) damps the fine smoother
@@ -1527,12 +1461,6 @@ bool amg_build(mof_mesh *m) {
             put_i(D.diag_pos, L.diag_pos);
             D.dead.alloc(L.dead.size());
             D.dead.upload(L.dead.data(), L.dead.size(), s);
-            // the sweeps of a level with an int8 copy read its lower blocks as
-            // the transposed upper twins (the Galerkin product is symmetric;
-            // a block and its twin quantise alike): MOF_COARSE_SYM=0 reads
-            // every block in place
-            const char *cs = std::getenv("MOF_COARSE_SYM");
-            if (l + 1 < H.levels.size() && !(cs && *cs == '0')) put_i(D.mir, coarse_mirror(L));
         }
         if (l + 1 < H.levels.size()) {
             put_i(D.agg, L.agg);
@@ -1709,7 +1637,6 @@ Lvl level_view(const AmgDevLevel &D) {
     v.Dh22 = D.Dh22.p;
     v.Ah = D.Ah.n > 1 ? reinterpret_cast<const uint4 *>(D.Ah.p) : nullptr;
     v.Ah22 = D.Ah22.n > 1 ? D.Ah22.p : nullptr;
-    v.mir = D.mir.n > 0 ? D.mir.p : nullptr;
     v.b = D.b.p;
     v.x = D.x.p;
     v.r = D.r.p;

@@ -255,26 +255,3 @@ def test_coarse_galerkin_by_entry_bit_identical(monkeypatch):
         m.close()
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][0], out[1][0])
-
-
-@pytest.mark.parametrize("cfg", ["C2", "S1s"])
-def test_coarse_symmetric_reads(cfg, monkeypatch):
-    """The coarse levels' int8 sweep copies read lower blocks as their upper
-    twins transposed (MOF_COARSE_SYM, the default): the Galerkin operator is
-    symmetric and a block and its twin quantise alike, so the cycle matches
-    the in-place reads to the solve's tolerance with the same iteration
-    counts (within 2 %), and V meets the bar against spsolve (the suite's
-    parity tests run this default)."""
-    p, t, n, a = synth.mesh_for_config(cfg)
-    I = synth.config_wave(cfg, p, 33)
-    tk = np.arange(33.0)
-    out = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("MOF_COARSE_SYM", v)  # read when the hierarchy is uploaded
-        m = DeviceMesh(p, n, t, a)
-        out[v] = m.solve_range(I, tk, 0, 32, 0.01, precision="mixed", precond="amg")
-        m.close()
-    (V0, s0), (V1, s1) = out["0"], out["1"]
-    assert s0["failed"] == s1["failed"] == 0 and s1["max_rel_residual"] <= 1e-8
-    assert abs(s0["iterations"] - s1["iterations"]) <= 0.02 * s0["iterations"] + 2
-    assert np.abs(V1 - V0).max() <= 2e-7 * np.abs(V0).max()
