@@ -857,14 +857,15 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         if (K > 0) {
             int32_t Bmax = o.batch;
             if (Bmax <= 0) {
-                // auto: 512 timesteps per launch sequence (C3: +4.6 % over
-                // 256, within 1 % of 768 / 1024), fewer when a quarter of the
-                // free device memory cannot hold their workspace (~720 B per
-                // vertex and system with the multigrid levels)
+                // auto: 1024 timesteps per launch sequence (C3: +4.6 % for 512
+                // over 256 (round 2), +1-4 % for 1024 over 512 by box (round
+                // 4, profiles/r04_ab/batch/)), fewer when half the free device
+                // memory cannot hold their workspace (~720 B per vertex and
+                // system with the multigrid levels; C3 at 1024: 121 GB)
                 size_t free_b = 0, total_b = 0;
                 MOF_HIP(hipMemGetInfo(&free_b, &total_b));
                 const double per_sys = 720.0 * (double)m->N + 1.0;
-                Bmax = (int32_t)std::max(1.0, std::min(512.0, 0.25 * (double)free_b / per_sys));
+                Bmax = (int32_t)std::max(1.0, std::min(1024.0, 0.5 * (double)free_b / per_sys));
             }
             const int32_t B = std::min(K, Bmax);
             hipStream_t s = o.stream ? (hipStream_t)o.stream : m->stream;
