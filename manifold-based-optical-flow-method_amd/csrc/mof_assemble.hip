@@ -547,8 +547,10 @@ __device__ __forceinline__ void g3_project(const float (&G)[WMAX][6], const doub
                 acc[z][2 * al + be] = eif[3 * al] * H[0][be] + eif[3 * al + 1] * H[1][be] + eif[3 * al + 2] * H[2][be];
     }
 }
+// WMAX = 8 at 4 waves per SIMD (128 VGPRs, no scratch; 130 and 3 waves
+// left to the compiler); WMAX = 16 spills at 4 and keeps its own choice
 template <int WMAX>
-__global__ __launch_bounds__(kWG) void k_assemble_rows_rc(
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(WMAX <= 8 ? 4 : 1))) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
     const int32_t *__restrict__ sell_col, const int32_t *__restrict__ vptr, const int32_t *__restrict__ tsell_off,
     const int4 *__restrict__ tinc, const int32_t *__restrict__ tslot, const float *__restrict__ w12,
