@@ -141,6 +141,12 @@ __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd
 // instead of 2 (round 3): 126 instead of 202 VGPRs, 4 instead of 2 waves
 // per SIMD, 5.73 -> 5.42 ms per 512-system launch (profiles/r03_ab/grp/)
 constexpr int kResU = 4, kRcU = 1;
+// incidence entries of a row preloaded by the re-forming residual (slices up
+// to this wide; 0: off)
+#ifndef MOF_RC_PRE
+#define MOF_RC_PRE 8
+#endif
+constexpr int kRcPre = MOF_RC_PRE;
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
 // U slots / incident triangles at a time as in spmv_row.
@@ -340,13 +346,35 @@ __device__ __forceinline__ void apply_row_rcn(const OpArgs<double> &op, const in
     rcn_row<NS>(op, bs, i, x64, R);
     const int32_t o = op.tsell_off[s];
     const int32_t w = (op.tsell_off[s + 1] - o) >> 6;
-    for (int32_t t0 = 0; t0 < w; ++t0) {
-        double val[NS][2];
-        rcn_tri<NS>(op, bs, op.tinc[(int64_t)o + t0 * kSlice + l], x64, R, val);
+    if (kRcPre && w <= kRcPre) {
+        // the row's incidence entries loaded up front: each incident
+        // triangle's geometry and per-system gathers then wait on one round
+        // trip, not on its entry first (the same terms in the same order)
+        constexpr int P = kRcPre > 0 ? kRcPre : 1;
+        int4 qs[P];
 #pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            acc[t][0] += val[t][0];
-            acc[t][1] += val[t][1];
+        for (int t0 = 0; t0 < P; ++t0)
+            if (t0 < w) qs[t0] = op.tinc[(int64_t)o + t0 * kSlice + l];
+#pragma unroll
+        for (int t0 = 0; t0 < P; ++t0) {
+            if (t0 >= w) break;
+            double val[NS][2];
+            rcn_tri<NS>(op, bs, qs[t0], x64, R, val);
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                acc[t][0] += val[t][0];
+                acc[t][1] += val[t][1];
+            }
+        }
+    } else {
+        for (int32_t t0 = 0; t0 < w; ++t0) {
+            double val[NS][2];
+            rcn_tri<NS>(op, bs, op.tinc[(int64_t)o + t0 * kSlice + l], x64, R, val);
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                acc[t][0] += val[t][0];
+                acc[t][1] += val[t][1];
+            }
         }
     }
 #pragma unroll
@@ -823,8 +851,11 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
 // staged in LDS and added by the row's thread in slot order (bit-identical):
 // 8421 / 5539 vs 5093 us per launch.
 constexpr int kResNS = 2;
+#ifndef MOF_RC_OCC
+#define MOF_RC_OCC
+#endif
 template <int NS>
-__global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
+__global__ __launch_bounds__(kWG) MOF_RC_OCC void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
                                                       const int32_t *__restrict__ sysi,
