@@ -142,7 +142,10 @@ __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd
 // per SIMD, 5.73 -> 5.42 ms per 512-system launch (profiles/r03_ab/grp/)
 constexpr int kResU = 4, kRcU = 1;
 // incidence entries of a row preloaded by the re-forming residual (slices up
-// to this wide; 0: off)
+// to this wide; 0: off): 162 VGPRs and 3 waves instead of 128 and 4, the
+// chains one round trip shorter -- 10.70 -> 10.61 ms per 1024-system launch,
+// C3 +0.25 % (round 4, profiles/r04_ab/res_pre/: the lost wave eats most of
+// the shorter chain)
 #ifndef MOF_RC_PRE
 #define MOF_RC_PRE 8
 #endif
