@@ -14,6 +14,7 @@ mixed solve -- for aggregation-multigrid variants:
               (||A_ij||_F >= X sqrt(||A_ii||_F ||A_jj||_F))
   theta2=X    the same with the strength measured on lambda*a2 (per mesh)
   om=X,Y      smoother damping (fine, coarse)
+  omb=X       level-0 damping X on the boundary rows (open surfaces) only
   l1          l1 block-Jacobi smoother (D + sum_j ||A_ij|| I), undamped
   sa=X        smoothed prolongator P = (I - X D^-1 A) P_tent at level 0,
               with the system's own A (per timestep)
@@ -73,6 +74,13 @@ def system(cfg, k=0):
     dof = np.empty(2 * N, dtype=np.int64)
     dof[0::2] = order
     dof[1::2] = order + N
+    # boundary vertices (on an edge of one triangle), in the RCM order: the
+    # omb=X option's rows
+    ed = np.sort(np.concatenate([t[:, [0, 1]], t[:, [1, 2]], t[:, [2, 0]]]), axis=1)
+    u, cnt = np.unique(ed, axis=0, return_counts=True)
+    bnd = np.zeros(N, dtype=bool)
+    bnd[u[cnt == 1].ravel()] = True
+    system.boundary = bnd[order]
     A = sp.csr_matrix(A)[dof][:, dof].tocsr()
     a2m = sp.csr_matrix(lam_a2)[dof][:, dof].tocsr()
     f = f[dof]
@@ -222,6 +230,9 @@ def build(A, a2m, e, opts):
             L.om = 1.0
         else:
             L.om = opts.get("om", (0.85, 1.05))[0 if lvl == 0 else 1]
+            if lvl == 0 and "omb" in opts:  # per-row damping: boundary rows omb
+                om = np.where(system.boundary, opts["omb"], L.om)
+                L.om = np.repeat(om, bs)
         levels.append(L)
         n = Acur.shape[0] // bs
         if n * bs <= 128 or n * 3 <= 128:
