@@ -142,14 +142,11 @@ __device__ __forceinline__ void reduce_sys(const double *slot, const RedArgs &rd
 // per SIMD, 5.73 -> 5.42 ms per 512-system launch (profiles/r03_ab/grp/)
 constexpr int kResU = 4, kRcU = 1;
 // incidence entries of a row preloaded by the re-forming residual (slices up
-// to this wide; 0: off): 162 VGPRs and 3 waves instead of 128 and 4, the
+// to this wide; wider slices load them one at a time): 162 VGPRs and 3 waves instead of 128 and 4, the
 // chains one round trip shorter -- 10.70 -> 10.61 ms per 1024-system launch,
 // C3 +0.25 % (round 4, profiles/r04_ab/res_pre/: the lost wave eats most of
 // the shorter chain)
-#ifndef MOF_RC_PRE
-#define MOF_RC_PRE 8
-#endif
-constexpr int kRcPre = MOF_RC_PRE;
+constexpr int kRcPre = 8;
 // y_i = (A_b x)_i for vertex row i of system b without materialised blocks
 // (lambda a2 + per-triangle a1; x = that system's vector). Loads are batched
 // U slots / incident triangles at a time as in spmv_row.
@@ -854,11 +851,8 @@ __global__ __launch_bounds__(kWG) void k_residual(OpArgs<double> op, int32_t nbl
 // staged in LDS and added by the row's thread in slot order (bit-identical):
 // 8421 / 5539 vs 5093 us per launch.
 constexpr int kResNS = 2;
-#ifndef MOF_RC_OCC
-#define MOF_RC_OCC
-#endif
 template <int NS>
-__global__ __launch_bounds__(kWG) MOF_RC_OCC void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
+__global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t nblk, int32_t B, RedArgs rd,
                                                       const double *__restrict__ rhs,
                                                       const double *__restrict__ x64,
                                                       const int32_t *__restrict__ sysi,
