@@ -15,6 +15,11 @@ mixed solve -- for aggregation-multigrid variants:
   theta2=X    the same with the strength measured on lambda*a2 (per mesh)
   om=X,Y      smoother damping (fine, coarse)
   omb=X       level-0 damping X on the boundary rows (open surfaces) only
+  sgn=1       level-0 aggregation on the negative couplings of lambda*a2 only
+  amax1=K     coarse-level aggregates of at most K nodes
+  theta1=X    coarse-level aggregation on strong couplings only
+  theta1only=X  the same at level 1 only
+  theta1a2=X  level 1 only, the strength from P^T (lambda a2) P (mesh-only)
   l1          l1 block-Jacobi smoother (D + sum_j ||A_ij|| I), undamped
   sa=X        smoothed prolongator P = (I - X D^-1 A) P_tent at level 0,
               with the system's own A (per timestep)
@@ -158,6 +163,19 @@ def strength_graph(A, bs, theta):
     return sp.csr_matrix((np.ones(keep.sum()), (Fc.row[keep], Fc.col[keep])), shape=(n, n))
 
 
+def sign_graph(A, bs):
+    """Couplings whose 2x2 block has a negative trace (the cotangent weight's
+    sign in lambda*a2: an obtuse triangle's opposite edge couples positively)."""
+    Acoo = A.tocoo()
+    n = A.shape[0] // bs
+    diag_entry = (Acoo.row % bs) == (Acoo.col % bs)
+    T = sp.csr_matrix((Acoo.data * diag_entry, (Acoo.row // bs, Acoo.col // bs)), shape=(n, n))
+    T.sum_duplicates()
+    Tc = T.tocoo()
+    keep = (Tc.row == Tc.col) | (Tc.data < 0)
+    return sp.csr_matrix((np.ones(keep.sum()), (Tc.row[keep], Tc.col[keep])), shape=(n, n))
+
+
 def tentative(agg, na, Bnull, bs):
     """Per aggregate QR of the stacked near-null space (MGS twice, dead
     columns dropped) -> P (n*bs x 3*na), coarse near-null (na, 3, 3)."""
@@ -211,6 +229,7 @@ def build(A, a2m, e, opts):
     bs = 2
     Bnull = e.reshape(-1, bs, 3)
     Acur = A
+    a2cur = a2m
     lvl = 0
     while True:
         L = Level()
@@ -243,9 +262,17 @@ def build(A, a2m, e, opts):
             G = strength_graph(Acur, bs, opts["theta"])
         if lvl == 0 and "theta2" in opts:  # strength from lambda*a2 (per mesh)
             G = strength_graph(a2m, bs, opts["theta2"])
+        if lvl == 0 and "sgn" in opts:  # negative couplings of lambda*a2 only
+            G = sign_graph(a2m, bs)
+        if lvl >= 1 and "theta1" in opts:  # coarse levels: strong couplings only
+            G = strength_graph(Acur, bs, opts["theta1"])
+        if lvl == 1 and "theta1only" in opts:  # level 1 only
+            G = strength_graph(Acur, bs, opts["theta1only"])
+        if lvl == 1 and "theta1a2" in opts:  # level 1, strength from P^T (lambda a2) P (per mesh)
+            G = strength_graph(a2cur, bs, opts["theta1a2"])
         G = (G + sp.eye(G.shape[0])).tocsr()
         G.sort_indices()
-        agg, na = aggregate(G, int(opts.get("amax", 0)) if lvl == 0 else 0)
+        agg, na = aggregate(G, int(opts.get("amax", 0)) if lvl == 0 else int(opts.get("amax1", 0)))
         if na >= n:
             L.coarse = np.linalg.inv(Acur.toarray())
             break
@@ -275,6 +302,7 @@ def build(A, a2m, e, opts):
         rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
         L.gal_terms = int((pc[rows] * pc[Ab.indices]).sum())
         Ac = (P.T @ (L.Aq if hasattr(L, "Aq") else Acur) @ P).tocsr()
+        a2cur = (P.T @ (a2m if lvl == 0 else a2cur) @ P).tocsr()
         dead = np.abs(Ac).sum(1).A1 == 0
         Ac = (Ac + sp.diags(dead * 1.0)).tocsr()
         Acur, bs, Bnull = Ac, 3, Bc
