@@ -285,6 +285,25 @@ def main():
     # --- this rank's timesteps --------------------------------------------
     B = args.batch
     strong = args.fixed_timesteps > 0
+    batch_note = None
+    if not dry:
+        # a batch whose workspace (~720 B per vertex and timestep with the
+        # multigrid levels, the library's own estimate) and signal rows do
+        # not fit 85 % of this GPU's free HBM is halved -- and said so --
+        # rather than failing an allocation mid-run
+        free_b, _ = torch.cuda.mem_get_info(local)
+        steps_rows = (args.warmup + args.steps) if not strong else 0
+
+        def need(b):
+            rows = (steps_rows * b if not strong else args.fixed_timesteps) + 1
+            return 720.0 * N * b + 8.0 * N * rows + 16.0 * N * b
+
+        B0 = B
+        while B > 64 and need(B) > 0.85 * free_b:
+            B //= 2
+        if B != B0:
+            batch_note = "batch %d reduced to %d: %.0f GB of HBM free" % (B0, B, free_b / 1e9)
+            print("[bench] " + batch_note, file=sys.stderr, flush=True)
     if strong:
         # the fixed job, split over the ranks; a step solves all of it
         k_off, k_end = rank_k_range(rank, world, 0, args.fixed_timesteps)
@@ -497,7 +516,8 @@ def main():
                     % synth.wave_phase(args.config, p[:1])[1],
             "config": {"workload": CONFIG_NAMES[args.config], "vertices": N, "triangles": len(t),
                        "timesteps_per_step": args.fixed_timesteps if strong else world * B,
-                       "timesteps_timed": n_ts, "batch": B, "precision": precision,
+                       "timesteps_timed": n_ts, "batch": B, **({"batch_note": batch_note} if batch_note else {}),
+                       "precision": precision,
                        "batch_effective": opts["batch"],
                        "precond": opts["precond"], "rtol": args.rtol,
                        "io": "host (pageable numpy I in, numpy V out; PCIe inclusive)" if host_io
