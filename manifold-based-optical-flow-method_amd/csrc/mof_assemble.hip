@@ -549,7 +549,10 @@ __device__ __forceinline__ void g3_project(const float (&G)[WMAX][6], const doub
 }
 // WMAX = 8 at 4 waves per SIMD (128 VGPRs, no scratch; 130 and 3 waves
 // left to the compiler): 16.87 -> 16.48 ms per 1024-system launch (round 4,
-// profiles/r04_ab/asm_w4/); WMAX = 16 spills at 4 and keeps its own choice
+// profiles/r04_ab/asm_w4/); WMAX = 16 spills at 4 and keeps its own choice.
+// Measured and not kept: the next incidence's tinc / tslot loaded one
+// iteration ahead (127 VGPRs, 2 spilled): 18.6-19.6 vs 16.5 ms
+// (profiles/r04_ab/asm_pre/)
 template <int WMAX>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(WMAX <= 8 ? 4 : 1))) void k_assemble_rows_rc(
     int32_t N, int32_t M, int32_t nblk, int32_t B, int64_t sell_nb, const int32_t *__restrict__ sell_off,
