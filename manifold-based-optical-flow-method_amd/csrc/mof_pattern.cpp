@@ -181,8 +181,11 @@ void build_pattern(const int32_t *tri, int32_t N, int32_t M, Pattern &pat, const
 // have their neighbours in the same slots (regular meshes): `sym` = 1 uses
 // them, 0 keeps every block at its own position (identity table), -1 decides
 // per mesh from the 128-B lines a wave instruction touches (fp32 blocks):
-// symmetric reads when own + mirrored lines stay within 1.25x the lines of
-// the plain layout (C3: 1.09x, irregular hull R3: 2.5x).
+// symmetric reads when own + mirrored lines stay within 2x the lines of the
+// plain layout. Round 4, forced either way on one box (profiles/r04_ab/sym/):
+// C3 1.08x; the S1-like patch 1.43x: +9 % (906 -> 988 timesteps/s, same
+// iterations); S1s 1.53x: +0.8 %; R3 in plain RCM order 2.81x: -6 %
+// (648 -> 610), window-sorted R3 3.37x: -11 % (round 3). The bound was 1.25x.
 std::vector<int32_t> sell_mirror(const Pattern &pat, int32_t nown, int sym, bool *used) {
     const int64_t snb = pat.sell_off[pat.nslices];
     MOF_REQUIRE(snb < kMirT, "SELL layout too large for the mirror table");
@@ -227,7 +230,7 @@ std::vector<int32_t> sell_mirror(const Pattern &pat, int32_t nown, int sym, bool
                 mirrored += std::unique(ln.begin(), ln.end()) - ln.begin();
             }
         }
-        sym = mirrored * 4 <= plain * 5 ? 1 : 0;
+        sym = mirrored <= 2 * plain ? 1 : 0;
         if (!sym)
             for (int64_t q = 0; q < snb; ++q)
                 if (mir[q] >= 0) mir[q] = (int32_t)q;
