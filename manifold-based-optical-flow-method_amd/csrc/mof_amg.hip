@@ -927,11 +927,19 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 // Level 0 with a smoothed prolongator: b_C[I] = sum over I's restriction
 // list (fine node order) of P^T r (r in node order). As k_restrict: a
 // workgroup takes whole coarse nodes with at most kRGS list entries in
-// total and kNS systems; one thread per entry loads the entry and its P block
-// once and forms P_e^T r_i of every system into LDS, then one thread per
-// coarse node sums its entries in list order (per system); with smooth also
-// x_C[I] = w D_C^-1 b_C[I].
-constexpr int kNS = 4;     // systems per workgroup / thread in the smoothed-P kernels
+// total and kNSR systems; one thread per entry loads the entry and its P
+// block once and forms P_e^T r_i of every system into LDS, then one thread
+// per (coarse node, system) sums the node's entries in list order; with
+// smooth also x_C[I] = w D_C^-1 b_C[I].
+// Round 4 (S1, B = 1024, rocprof, profiles/r04_ab/sa_xfer/; V bit-identical,
+// tools/vhash.py): the sums by coarse node alone left most of the
+// workgroup idle behind a few long serial loops -- by (node, system)
+// 1615 -> 1434 us per launch, and 8 instead of 4 systems per workgroup
+// 1344 us (48-KB LDS stage); the prolongation with 8 systems per thread
+// 1263 -> 1112 us: S1 990 -> 1018 timesteps/s. (The tentative k_restrict
+// by (aggregate, system): 397 -> 448 us at C3, not kept.)
+constexpr int kNSR = 8;    // systems per workgroup in the smoothed-P restriction
+constexpr int kNSP = 8;    // systems per thread in the smoothed-P prolongation
 constexpr int kRGS = 512;  // list entries per restriction group (smoothed P)
 __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
                                                       int32_t B, int32_t smooth, float omega,
@@ -939,78 +947,78 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
     // no fp contraction: every system slot of the unrolled loops rounds alike
     // (a system's bits must not depend on its slot, i.e. on the batch split)
 #pragma clang fp contract(off)
-    __shared__ float con[kNS][3][kRGS];
+    __shared__ float con[kNSR][3][kRGS];
     int32_t g, bq;
-    const int32_t nq = (B + kNS - 1) / kNS;
+    const int32_t nq = (B + kNSR - 1) / kNSR;
     if (!xcd_map(ngrp, nq, g, bq, kGrpRestr)) return;
-    const int32_t b0 = bq * kNS;
+    const int32_t b0 = bq * kNSR;
     bool any = false;
 #pragma unroll
-    for (int t = 0; t < kNS; ++t) any |= b0 + t < B && !retired(sysi, b0 + t);
+    for (int t = 0; t < kNSR; ++t) any |= b0 + t < B && !retired(sysi, b0 + t);
     if (!any) return;
     const int32_t I0 = grp[g], I1 = grp[g + 1];
     const int32_t e0 = F.rptr[I0], e1 = F.rptr[I1];
     const bool big = e1 - e0 > kRGS;  // one coarse node with an oversized list: summed from memory
-    auto contrib = [&](int32_t e, float (&c3)[kNS][3]) {
+    auto contrib = [&](int32_t e, float (&c3)[kNSR][3]) {
         const int32_t i = F.rent[2 * (int64_t)e];
         const float *p = F.Q + (int64_t)F.rent[2 * (int64_t)e + 1] * 6;
         float pm[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) pm[k] = p[k];
-        float ri[kNS][2];
+        float ri[kNSR][2];
 #pragma unroll
-        for (int t = 0; t < kNS; ++t) ldr<2>(F.r, min(b0 + t, B - 1), F.n, i, ri[t]);
+        for (int t = 0; t < kNSR; ++t) ldr<2>(F.r, min(b0 + t, B - 1), F.n, i, ri[t]);
 #pragma unroll
-        for (int t = 0; t < kNS; ++t)
+        for (int t = 0; t < kNSR; ++t)
 #pragma unroll
             for (int c = 0; c < 3; ++c) c3[t][c] = pm[c] * ri[t][0] + pm[3 + c] * ri[t][1];
     };
     for (int32_t e = e0 + threadIdx.x; e < e1 && !big; e += kWG) {
-        float c3[kNS][3];
+        float c3[kNSR][3];
         contrib(e, c3);
 #pragma unroll
-        for (int t = 0; t < kNS; ++t)
+        for (int t = 0; t < kNSR; ++t)
 #pragma unroll
             for (int c = 0; c < 3; ++c) con[t][c][e - e0] = c3[t][c];
     }
     __syncthreads();
-    for (int32_t I = I0 + threadIdx.x; I < I1; I += kWG) {
-        float acc[kNS][3] = {};
+    // one thread per (coarse node, system), nodes adjacent across threads:
+    // kNSR times the threads of one per node, each summing its node's
+    // entries in list order (the same per-system sums, bit for bit)
+    const int32_t nI = I1 - I0;
+    for (int32_t q = threadIdx.x; q < nI * kNSR; q += kWG) {
+        const int32_t t = q / nI, I = I0 + q - t * nI, b = b0 + t;
+        if (b >= B || retired(sysi, b)) continue;
+        float acc[3] = {};
         for (int32_t e = F.rptr[I]; e < F.rptr[I + 1]; ++e) {
-            float c3[kNS][3];
+            float c3[3];
             if (big) {
-                contrib(e, c3);
+                float all[kNSR][3];
+                contrib(e, all);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) c3[c] = all[t][c];
             } else {
 #pragma unroll
-                for (int t = 0; t < kNS; ++t)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) c3[t][c] = con[t][c][e - e0];
+                for (int c = 0; c < 3; ++c) c3[c] = con[t][c][e - e0];
             }
 #pragma unroll
-            for (int t = 0; t < kNS; ++t)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) acc[t][c] += c3[t][c];
+            for (int c = 0; c < 3; ++c) acc[c] += c3[c];
         }
+        const int64_t vo = (int64_t)b * C.n * 4;
+        stv<3>(C.b + vo, I, acc);
+        if (smooth) {
+            float d[3][3], x[3];
+            ld_dh(C, b, I, d);
+            matvec<3>(d, acc, x);
 #pragma unroll
-        for (int t = 0; t < kNS; ++t) {
-            const int32_t b = b0 + t;
-            if (b >= B || retired(sysi, b)) continue;
-            const int64_t vo = (int64_t)b * C.n * 4;
-            stv<3>(C.b + vo, I, acc[t]);
-            if (smooth) {
-                float d[3][3], x[3];
-                ld_dh(C, b, I, d);
-                matvec<3>(d, acc[t], x);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) x[c] *= omega;
-                stv<3>(C.x + vo, I, x);
-            }
+            for (int c = 0; c < 3; ++c) x[c] *= omega;
+            stv<3>(C.x + vo, I, x);
         }
     }
 }
 
 // Level 0 with a smoothed prolongator: x_i = x0_i + sum_k P_ik y_C[pcol k],
-// kNS systems per thread (the row's P blocks and columns loaded once)
+// kNSP systems per thread (the row's P blocks and columns loaded once)
 template <int XM>
 __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk, int32_t B,
                                                      const int32_t *__restrict__ sysi) {
@@ -1018,14 +1026,14 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     // (a system's bits must not depend on its slot, i.e. on the batch split)
 #pragma clang fp contract(off)
     int32_t rb, bq;
-    const int32_t nq = (B + kNS - 1) / kNS;
+    const int32_t nq = (B + kNSP - 1) / kNSP;
     if (!xcd_map(nblk, nq, rb, bq, kGrpProl)) return;
-    const int32_t b0 = bq * kNS;
+    const int32_t b0 = bq * kNSP;
     const int32_t i = rb * kWG + threadIdx.x;
     if (i >= F.n) return;
-    float x[kNS][2];
+    float x[kNSP][2];
 #pragma unroll
-    for (int t = 0; t < kNS; ++t) {
+    for (int t = 0; t < kNSP; ++t) {
         const float2 v = ld_x0(F.x, (int64_t)min(b0 + t, B - 1) * F.n + i);
         x[t][0] = v.x;
         x[t][1] = v.y;
@@ -1037,17 +1045,17 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
         float qm[6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) qm[c] = q[c];
-        float y[kNS][3];
+        float y[kNSP][3];
 #pragma unroll
-        for (int t = 0; t < kNS; ++t) ldv<3>(C.y + (int64_t)min(b0 + t, B - 1) * C.n * 4, K, y[t]);
+        for (int t = 0; t < kNSP; ++t) ldv<3>(C.y + (int64_t)min(b0 + t, B - 1) * C.n * 4, K, y[t]);
 #pragma unroll
-        for (int t = 0; t < kNS; ++t) {
+        for (int t = 0; t < kNSP; ++t) {
             x[t][0] += qm[0] * y[t][0] + qm[1] * y[t][1] + qm[2] * y[t][2];
             x[t][1] += qm[3] * y[t][0] + qm[4] * y[t][1] + qm[5] * y[t][2];
         }
     }
 #pragma unroll
-    for (int t = 0; t < kNS; ++t) {
+    for (int t = 0; t < kNSP; ++t) {
         const int32_t b = b0 + t;
         if (b >= B || retired(sysi, b)) continue;
         if constexpr (XM == 2)  // full-precision x for the post-smoothing
@@ -1677,7 +1685,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                                  kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
                                               G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
             if (G.lv[0].smoothed) {
-                k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNS - 1) / kNS, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             } else {
                 k_restrict<2, kRestrS><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kRestrS - 1) / kRestrS, kGrpRestr)), kWG, 0, s>>>(
@@ -1702,7 +1710,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
             const int32_t nb0p = (v[0].n + kWG * kProlR - 1) / (kWG * kProlR);
-            const dim3 gsa(xcd_grid(nb0, (B + kNS - 1) / kNS, kGrpProl)), gp(xcd_grid(nb0p, (B + kProlS - 1) / kProlS, kGrpProl));
+            const dim3 gsa(xcd_grid(nb0, (B + kNSP - 1) / kNSP, kGrpProl)), gp(xcd_grid(nb0p, (B + kProlS - 1) / kProlS, kGrpProl));
             if (G.xm == 2) {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
