@@ -936,10 +936,13 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 // workgroup idle behind a few long serial loops -- by (node, system)
 // 1615 -> 1434 us per launch, and 8 instead of 4 systems per workgroup
 // 1344 us (48-KB LDS stage); the prolongation with 8 systems per thread
-// 1263 -> 1112 us: S1 990 -> 1018 timesteps/s. (The tentative k_restrict
-// by (aggregate, system): 397 -> 448 us at C3, not kept.)
+// 1263 -> 1112 us: S1 990 -> 1018 timesteps/s; 16 per thread (72 VGPRs, no
+// scratch) 1089 -> 975 us, while 16 systems per restriction workgroup over
+// 256-entry groups stay at 1347 us (profiles/r04_ab/sa_xfer/call38/).
+// (The tentative k_restrict by (aggregate, system): 397 -> 448 us at C3,
+// not kept.)
 constexpr int kNSR = 8;    // systems per workgroup in the smoothed-P restriction
-constexpr int kNSP = 8;    // systems per thread in the smoothed-P prolongation
+constexpr int kNSP = 16;   // systems per thread in the smoothed-P prolongation
 constexpr int kRGS = 512;  // list entries per restriction group (smoothed P)
 __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
                                                       int32_t B, int32_t smooth, float omega,
