@@ -255,3 +255,23 @@ def test_coarse_galerkin_by_entry_bit_identical(monkeypatch):
         m.close()
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][0], out[1][0])
+
+
+def test_open_patch_batch_split_bit_identical():
+    """The S1-like open patch (smoothed prolongator, symmetric reads under
+    the 2x line bound, fine damping 0.7): the same bits for one system per
+    launch and for batches of 17 and 41 -- partial groups of the smoothed-P
+    restriction (8 systems per workgroup) and prolongation (16 per thread)."""
+    p, t, n, a = synth.mesh_for_config("S1s")
+    T = 42
+    I = synth.config_wave("S1s", p, T)
+    tk = np.arange(float(T))
+    m = DeviceMesh(p, n, t, a)
+    assert m.info()["blocks_read"] < m.info()["nblocks"]  # symmetric reads chosen
+    V1, s1 = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=1)
+    V17, _ = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=17)
+    V41, s41 = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=41)
+    m.close()
+    assert s1["failed"] == 0 and s41["failed"] == 0 and s41["recovered"] == 0
+    assert np.array_equal(V1, V17) and np.array_equal(V1, V41)
+    assert s1["iterations"] == s41["iterations"]
