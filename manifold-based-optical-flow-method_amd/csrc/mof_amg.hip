@@ -938,7 +938,9 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 // 1344 us (48-KB LDS stage); the prolongation with 8 systems per thread
 // 1263 -> 1112 us: S1 990 -> 1018 timesteps/s; 16 per thread (72 VGPRs, no
 // scratch) 1089 -> 975 us, while 16 systems per restriction workgroup over
-// 256-entry groups stay at 1347 us (profiles/r04_ab/sa_xfer/call38/).
+// 256-entry groups stay at 1347 us (profiles/r04_ab/sa_xfer/call38/); two
+// list entries per thread and pass with their loads in flight together
+// 1347 -> 1300 us (call42/).
 // (The tentative k_restrict by (aggregate, system): 397 -> 448 us at C3,
 // not kept.)
 constexpr int kNSR = 8;    // systems per workgroup in the smoothed-P restriction
@@ -976,13 +978,21 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
 #pragma unroll
             for (int c = 0; c < 3; ++c) c3[t][c] = pm[c] * ri[t][0] + pm[3 + c] * ri[t][1];
     };
-    for (int32_t e = e0 + threadIdx.x; e < e1 && !big; e += kWG) {
-        float c3[kNSR][3];
-        contrib(e, c3);
+    // two entries per thread and pass, both entries' loads in flight together
+    for (int32_t e = e0 + threadIdx.x; e < e1 && !big; e += 2 * kWG) {
+        const bool two = e + kWG < e1;
+        float c3[2][kNSR][3];
+        contrib(e, c3[0]);
+        contrib(two ? e + kWG : e, c3[1]);
 #pragma unroll
         for (int t = 0; t < kNSR; ++t)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) con[t][c][e - e0] = c3[t][c];
+            for (int c = 0; c < 3; ++c) con[t][c][e - e0] = c3[0][t][c];
+        if (two)
+#pragma unroll
+            for (int t = 0; t < kNSR; ++t)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) con[t][c][e + kWG - e0] = c3[1][t][c];
     }
     __syncthreads();
     // one thread per (coarse node, system), nodes adjacent across threads:
