@@ -942,7 +942,8 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 // list entries per thread and pass with their loads in flight together
 // 1347 -> 1300 us (call42/).
 // (The tentative k_restrict by (aggregate, system): 397 -> 448 us at C3,
-// not kept.)
+// and with two members per thread and pass: 360 vs 360 us (call43/); neither
+// kept.)
 constexpr int kNSR = 8;    // systems per workgroup in the smoothed-P restriction
 constexpr int kNSP = 16;   // systems per thread in the smoothed-P prolongation
 constexpr int kRGS = 512;  // list entries per restriction group (smoothed P)
