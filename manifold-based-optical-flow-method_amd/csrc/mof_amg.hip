@@ -1617,9 +1617,19 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
             nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
     }
     G.bf16_fresh = false;
+    // a dispatch's grid is at most 2^32 - 1 work-items: a by-entry product
+    // whose (group, system pair) grid would pass it (a batch of 1024 over
+    // more than ~32k entry groups) takes the per-position kernel -- the same
+    // terms in the same order, bit-identical (round 4: an unsliced by-entry
+    // launch past the bound skipped workgroups)
+    auto ent_fits = [&](const AmgDevLevel &F) {
+        return F.nggrp > 0 &&
+               (int64_t)xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal) * kWG < ((int64_t)1 << 32);
+    };
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
-        if (l == 0 && F.nggrp > 0)
+        const bool ent = ent_fits(F);
+        if (l == 0 && ent)
             k_galerkin0_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
                 F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
                 reinterpret_cast<const uint2 *>(G.A0h.p), m->pat.sell_nb(), C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C),
@@ -1632,7 +1642,7 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                           F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
                                               ? nullptr
                                               : reinterpret_cast<const uint2 *>(G.A0h.p));
-        else if (F.nggrp > 0)
+        else if (ent)
             k_galerkin3_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
                 F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
                 F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
