@@ -1623,8 +1623,8 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     // terms in the same order, bit-identical (round 4: an unsliced by-entry
     // launch past the bound skipped workgroups)
     auto ent_fits = [&](const AmgDevLevel &F) {
-        return F.nggrp > 0 &&
-               (int64_t)xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal) * kWG < ((int64_t)1 << 32);
+        const int64_t G = sys_group((B + kGalENS - 1) / kGalENS, kGrpGal), nq = (B + kGalENS - 1) / kGalENS;
+        return F.nggrp > 0 && 8 * G * ((nq + G - 1) / G) * ((F.nggrp + 7) / 8) * kWG < ((int64_t)1 << 32);
     };
     for (size_t l = 0; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];

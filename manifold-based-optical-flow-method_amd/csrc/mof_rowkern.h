@@ -308,9 +308,14 @@ __device__ __forceinline__ bool xcd_map(int32_t nblk, int32_t B, int32_t &rb, in
     return xcd_map_w((int32_t)blockIdx.x, nblk, B, rb, sys, grp_sz);
 }
 
+// A dispatch's grid is at most 2^32 - 1 work-items (kWG per workgroup): a
+// launch past it would run only part of its workgroups, so it fails loudly
+// here instead (round 4: an unsliced by-entry Galerkin launch at S1's size).
 inline unsigned xcd_grid(int32_t nblk, int32_t B, int32_t grp_sz) {
-    const int32_t G = sys_group(B, grp_sz);
-    return (unsigned)(8 * G * ((B + G - 1) / G) * ((nblk + 7) / 8));
+    const int64_t G = sys_group(B, grp_sz);
+    const int64_t n = 8 * G * ((B + G - 1) / G) * ((nblk + 7) / 8);
+    MOF_REQUIRE(n * kWG < ((int64_t)1 << 32), "launch grid past 2^32 work-items (batch too large for this mesh)");
+    return (unsigned)n;
 }
 
 

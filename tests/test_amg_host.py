@@ -70,3 +70,12 @@ def test_xcd_order_visits_every_pair_once(nblk, batch, group):
     8 / 32 / all) covers every (row block, system) pair exactly once, also
     with partial groups and row-block counts not divisible by 8."""
     L.check(L.lib().mof_xcd_map_check(nblk, batch, group))
+
+
+def test_xcd_grid_past_dispatch_limit_fails_loudly():
+    """A row-kernel grid past 2^32 - 1 work-items (a dispatch would run only
+    part of its workgroups) is refused with an error, never launched."""
+    # 40,000 row blocks x 1024 systems in groups of 8: 41 M workgroups of 256
+    with pytest.raises(L.MofError):
+        L.check(L.lib().mof_xcd_map_check(40000, 1024, 8))
+    L.check(L.lib().mof_xcd_map_check(641, 1024, 8))  # C3's size: fine
