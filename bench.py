@@ -53,6 +53,9 @@ CONFIG_NAMES = {
     "C5": "640k-vertex jittered icosphere (n=253, 640,092 vertices)",
     "R3": "163,842-vertex irregular random-hull sphere (valence 3-14, random vertex order)",
     "P3": "C3 mesh with randomly relabelled vertices (no index locality)",
+    "F3": "163,842-vertex folded cortex-like surface (fsaverage's order-7 icosahedral topology, radially folded "
+          "by a seeded band-limited field: gyral period 16-27 mm at 70 mm radius, sulcal amplitude 15 % of the "
+          "radius; synth.folded_sphere)",
     "S1": "160,801-vertex S1-like reconstructed patch (51 x 51 electrode grid, Delaunay, butterfly x3, smoothed)",
     "S1s": "3,249-vertex S1-like reconstructed patch (8 x 8 electrode grid), T=98 (97 solves), the reference's "
            "real workload size (config.yaml:5, find_singularity_point.py:19-20)",
@@ -94,6 +97,11 @@ def parse():
                     help="timesteps of the last timed batch checked against the oracle + spsolve (0: none)")
     ap.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
                     help="fp64: the one-launch fused solve per batch (auto: the library's choice, small meshes)")
+    ap.add_argument("--allow-recovery", action="store_true",
+                    help="do not treat recovered systems as a defect (experiments that force a failing solver)")
+    ap.add_argument("--etol", type=float, default=0.0,
+                    help="the refinement's error control: estimated error <= etol max|V| (0: the library's "
+                         "1e-7, < 0: the residual test alone)")
     ap.add_argument("--host-batches", type=int, default=4,
                     help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
                          "the device-resident region (0: none)")
@@ -303,6 +311,12 @@ def main():
             B //= 2
         if B != B0:
             batch_note = "batch %d reduced to %d: %.0f GB of HBM free" % (B0, B, free_b / 1e9)
+        # the library clamps every batch to the largest whose launch grids
+        # fit 2^32 work-items (mof_mesh_info.max_batch); say so here
+        if info.get("max_batch") and B > info["max_batch"]:
+            B1, B = B, int(info["max_batch"])
+            batch_note = (batch_note + "; " if batch_note else "") + \
+                "batch %d reduced to %d: launch grids past 2^32 work-items" % (B1, B)
             print("[bench] " + batch_note, file=sys.stderr, flush=True)
     if strong:
         # the fixed job, split over the ranks; a step solves all of it
@@ -336,7 +350,7 @@ def main():
     sync()
     precond = (args.precond or "amg") if precision == "mixed" else "jacobi"
     opts = dict(precision=precision, batch=B, rtol=args.rtol, precond=precond, inner_rtol=args.inner_rtol,
-                fused={"auto": None, "on": True, "off": False}[args.fused])
+                fused={"auto": None, "on": True, "off": False}[args.fused], etol=args.etol)
 
     kept = []  # host V of the timed calls, freed after the clock stops (the caller keeps its result)
 
@@ -346,7 +360,7 @@ def main():
             return dict.fromkeys(("iterations", "failed", "recovered", "ms_spmv", "spmv_bytes", "spmv_launches",
                                   "spmv_systems", "spmv_full_launches", "ms_spmv_full", "ms_assembly",
                                   "ms_solve", "max_rel_residual", "outer_steps", "fused_launches",
-                                  "ms_fused"), 0) | {"systems": b - a}
+                                  "ms_fused", "max_err_est"), 0) | {"systems": b - a}
         if host_io:
             V, st = mesh.solve_range(I_host, tk, a, b, args.lambda_, device=local, time_spmv=timed, **opts)
             if timed:
@@ -385,7 +399,8 @@ def main():
     t0 = time.perf_counter()
     agg = {"iterations": 0, "failed": 0, "recovered": 0, "ms_spmv": 0.0, "spmv_bytes": 0.0, "spmv_launches": 0,
            "spmv_systems": 0, "spmv_full_launches": 0, "ms_spmv_full": 0.0, "max_rel_residual": 0.0,
-           "ms_assembly": 0.0, "ms_solve": 0.0, "systems": 0, "fused_launches": 0, "ms_fused": 0.0}
+           "ms_assembly": 0.0, "ms_solve": 0.0, "systems": 0, "fused_launches": 0, "ms_fused": 0.0,
+           "max_err_est": 0.0}
     for a_, b_ in timed_calls:
         st = solve(a_, b_, True)
         for k in ("iterations", "failed", "recovered", "ms_spmv", "spmv_bytes", "spmv_launches", "spmv_systems",
@@ -393,6 +408,7 @@ def main():
                   "ms_fused"):
             agg[k] += st[k]
         agg["max_rel_residual"] = max(agg["max_rel_residual"], st["max_rel_residual"])
+        agg["max_err_est"] = max(agg["max_err_est"], st["max_err_est"])
         agg["max_outer_steps"] = max(agg.get("max_outer_steps", 0), st["outer_steps"])
     sync()
     elapsed = time.perf_counter() - t0
@@ -414,6 +430,7 @@ def main():
     cdev = torch.device("cpu") if (rehearse or dry) else dev
     elapsed = max_over_ranks(elapsed, dist, cdev)
     agg["failed"] = int(sum_over_ranks(agg["failed"], dist, cdev))
+    agg["recovered"] = int(sum_over_ranks(agg["recovered"], dist, cdev))
     n_ts = int(sum_over_ranks(agg["systems"], dist, cdev))
     value = n_ts / elapsed
     n_local = max(1, agg["systems"])
@@ -531,6 +548,9 @@ def main():
             "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / n_local, 1),
                        "failed": agg["failed"], "recovered": agg["recovered"],
                        "max_rel_residual": agg["max_rel_residual"],
+                       # the refinement's error estimate, max|d_k| |r_k+1| / |r_k|
+                       # over max|V| (the stop rule's)
+                       "max_err_est": agg["max_err_est"],
                        "max_refinement_steps": agg.get("max_outer_steps", 0),
                        "ms_assembly_per_timestep": round(agg["ms_assembly"] / n_local, 4),
                        "ms_solve_per_timestep": round(agg["ms_solve"] / n_local, 4),
@@ -544,6 +564,17 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        # a system the first solve failed and a recovery pass repaired is a
+        # solver defect on these healthy configurations (round 4: a launch that
+        # skipped workgroups was hidden by the recovery) -- marked, and the run
+        # exits non-zero unless --allow-recovery
+        defect = None
+        if agg["recovered"] > 0 or agg["failed"] > 0:
+            defect = {"recovered": agg["recovered"], "failed": agg["failed"],
+                      "why": "the first solve failed on systems of a healthy configuration"}
+            line["defect"] = defect
+        if parity is not None and parity["max_abs_err"] > parity["bar"] * max(1.0, parity["max_abs_V"]):
+            line["defect"] = dict(defect or {}, parity=parity["max_abs_err"])
         if dry:
             line["dry_run"] = True
             line["rank_ranges"] = rank_ranges
@@ -551,7 +582,11 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and "defect" in line and not (args.allow_recovery and "parity" not in line["defect"]):
+        print("[bench] defect: %s" % json.dumps(line["defect"]), file=sys.stderr, flush=True)
+        return 3
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -30,10 +30,11 @@ extern "C" {
 
 /* ABI version: bumped whenever a public struct or signature changes (2:
  * mof_stats grew recovered / recovered_f64 and the SpMV accounting fields,
- * mof_mesh_info blocks_read; mof_mesh_clone). A binding checks
+ * mof_mesh_info blocks_read; mof_mesh_clone; 4: mof_opts.etol, mof_stats
+ * max_err_est -- the refinement's error control; mof_mesh_info max_batch). A binding checks
  * mof_abi_version() == MOF_ABI_VERSION of the header it was built against:
  * the library writes whole structs, so a stale header would be overrun. */
-#define MOF_ABI_VERSION 3
+#define MOF_ABI_VERSION 4
 
 /* status codes */
 #define MOF_OK 0
@@ -118,6 +119,10 @@ typedef struct mof_opts {
     double rtol;           /* stop at ||f - A V||_2 <= rtol ||f||_2 (0: 1e-8) */
     double inner_rtol;     /* MOF_PREC_MIXED inner PCG tolerance (0: 1e-4) */
     void *stream;          /* hipStream_t to run on, NULL: the handle's own */
+    double etol;           /* error control (ABI 4): a system also needs its
+                              estimated error 2 max|d_k| |r_{k+1}| / |r_k|
+                              (d_k the last refinement correction) to be at
+                              most etol max|V| (0: 1e-7; < 0: residual only) */
 } mof_opts;
 
 typedef struct mof_stats {
@@ -148,6 +153,8 @@ typedef struct mof_stats {
     int32_t recovered_f64;    /* of those, solved by the fp64 recovery */
     int64_t fused_launches;   /* MOF_TIME_SPMV: fused solves (one per batch) ... */
     double ms_fused;          /* ... and their summed kernel time */
+    double max_err_est;       /* max over systems of the error estimate
+                                 max|d_k| |r_{k+1}| / |r_k| over max|V| (ABI 4) */
 } mof_stats;
 
 typedef struct mof_mesh_info {
@@ -162,6 +169,10 @@ typedef struct mof_mesh_info {
                                   reads per system: the diagonal and upper
                                   blocks (lower ones are read as transposes),
                                   = nblocks in a build without symmetric reads */
+    int32_t max_batch;         /* the largest batch whose launch grids stay
+                                  within 2^32 - 1 work-items; mof_solve_range
+                                  never exceeds it (ABI 4) */
+    int32_t pad_;
 } mof_mesh_info;
 
 /* Library / device queries. */
@@ -314,6 +325,10 @@ int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int
  * `group` systems (0: all) -- visits every (row block, system) pair exactly
  * once. MOF_OK, or an error with mof_last_error() set. */
 int mof_xcd_map_check(int32_t nblk, int32_t batch, int32_t group);
+/* Diagnostic (host only): the largest batch whose XCD-ordered grid over nblk
+ * blocks per system (groups of `group`) stays within 2^32 - 1 work-items --
+ * the bound mof_solve_range's batch never passes (mof_mesh_info.max_batch). */
+int mof_xcd_batch_cap(int64_t nblk, int32_t group, int32_t *batch);
 
 /* ---- one timestep's system decomposed over P
  * vertex parts (stretch; timestep shards stay the throughput path) --------

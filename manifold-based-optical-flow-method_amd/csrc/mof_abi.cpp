@@ -303,6 +303,8 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
         for (int32_t b = 0; b < nb; ++b) {
             if (m->h_sysi[b * mof::kSysStride + mof::SI_FAILED]) st.failed++;
             st.max_rel_residual = std::max(st.max_rel_residual, m->h_sysd[b * mof::kSysStride + mof::SD_REL]);
+            const double xm = m->h_sysd[b * mof::kSysStride + mof::SD_XMAX];
+            if (xm > 0.0) st.max_err_est = std::max(st.max_err_est, m->h_sysd[b * mof::kSysStride + mof::SD_EST] / xm);
         }
         st.batches++;
     }
@@ -735,6 +737,8 @@ int mof_mesh_get_info(const mof_mesh *m, mof_mesh_info *info) {
         info->ms_geometry = m->ms_geometry;
         info->ms_pattern = m->ms_pattern;
         info->blocks_read = m->blocks_read;
+        info->max_batch = mof::grid_batch_cap(m);
+        info->pad_ = 0;
     });
 }
 
@@ -841,6 +845,8 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
         sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
         sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
+        // error control: etol 0 -> 1e-7 of max|V|, < 0 -> off
+        sp.etol = o.etol > 0 ? o.etol : (o.etol < 0 ? 0.0 : 1e-7);
         // a multigrid-preconditioned inner solve takes tens of iterations:
         // one that stops improving, or hits max_iter, has a bad preconditioner
         sp.stall = sp.amg ? env_int("MOF_PCG_STALL", 64) : 0;
@@ -865,9 +871,17 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
                 size_t free_b = 0, total_b = 0;
                 MOF_HIP(hipMemGetInfo(&free_b, &total_b));
                 const double per_sys = 720.0 * (double)m->N + 1.0;
-                Bmax = (int32_t)std::max(1.0, std::min(1024.0, 0.5 * (double)free_b / per_sys));
+                // a mixed solve's fp64 recovery pass allocates A64, u64 and
+                // fc at the batch size on top (~330 B per vertex and
+                // system): the workspace keeps half the free memory and,
+                // with the recovery's arrays, 85 % of it
+                const double per_rec = per_sys + 8.0 * (4.0 * (double)m->pat.sell_nb() + 6.0 * (m->M + 1.0));
+                Bmax = (int32_t)std::max(1.0, std::min({1024.0, 0.5 * (double)free_b / per_sys,
+                                                        0.85 * (double)free_b / per_rec}));
             }
-            const int32_t B = std::min(K, Bmax);
+            // every launch grid within 2^32 work-items (an explicit batch
+            // too: V does not depend on the batch size)
+            const int32_t B = std::min(K, std::min(Bmax, mof::grid_batch_cap(m)));
             hipStream_t s = o.stream ? (hipStream_t)o.stream : m->stream;
             solve_batches(m, I, I2, t_k, k0, k1, B, lambda, sp, o, recovery, dev_io, s, V_out, st, timing);
         }
@@ -1098,6 +1112,13 @@ int mof_xcd_map_check(int32_t nblk, int32_t batch, int32_t group) {
     return guarded([&] {
         MOF_REQUIRE(nblk > 0 && batch > 0 && group >= 0, "bad arguments");
         MOF_REQUIRE(mof::xcd_map_covers(nblk, batch, group), "XCD order does not cover every (row block, system) once");
+    });
+}
+
+int mof_xcd_batch_cap(int64_t nblk, int32_t group, int32_t *batch) {
+    return guarded([&] {
+        MOF_REQUIRE(nblk > 0 && group >= 0 && batch, "bad arguments");
+        *batch = mof::xcd_batch_cap_host(nblk, group);
     });
 }
 

@@ -74,6 +74,8 @@ struct mof_dd {
     hipStream_t stream = nullptr;
     int32_t cap = 0, nmax = 0;       // systems / workgroups per part the partials hold
     mof::DevArray<double> part_pq, part_rzrr, part_rr0;  // [2][P][B][nmax] (x NV)
+    int32_t nvmax = 0;                   // k_outer_update blocks of the largest part
+    mof::DevArray<double> part_dx;       // [P][B][nvmax][2]: max|d|, max|x64| (error control)
     // in-process halo: one entry per ghost row of every part
     // {dst part, dst row, src part, src row}
     mof::DevArray<int4> halo;
@@ -124,5 +126,6 @@ void dd_gather_v(mof_dd *d, int32_t B, double *V, hipStream_t s);
 // word; in-process: `ok`). Used where one rank can fail alone (a workspace
 // allocation) before collectives every rank must enter.
 bool dd_all_ok(mof_dd *d, bool ok, hipStream_t s);
+double dd_all_min(mof_dd *d, double mine, hipStream_t s);
 
 }  // namespace mof

@@ -225,9 +225,10 @@ void dd_sync_partials(mof_dd *d, double *base, size_t per_part, hipStream_t s) {
                "ncclAllGather(partials)");
 }
 
-bool dd_all_ok(mof_dd *d, bool ok, hipStream_t s) {
-    if (d->rank < 0 || d->P == 1) return ok;
-    const double mine = ok ? 1.0 : 0.0;
+// The minimum of one value over the ranks (every rank gets the same): an
+// all-gather of one double per rank into `agree`.
+double dd_all_min(mof_dd *d, double mine, hipStream_t s) {
+    if (d->rank < 0 || d->P == 1) return mine;
     MOF_HIP(hipMemcpyAsync(d->agree.p + d->rank, &mine, sizeof(double), hipMemcpyHostToDevice, s));
     if (d->hosted)
         host_allgather(d, d->agree.p, 1, sizeof(double), s);
@@ -239,10 +240,12 @@ bool dd_all_ok(mof_dd *d, bool ok, hipStream_t s) {
     std::vector<double> all(d->P);
     MOF_HIP(hipMemcpyAsync(all.data(), d->agree.p, sizeof(double) * d->P, hipMemcpyDeviceToHost, s));
     MOF_HIP(hipStreamSynchronize(s));
-    for (double v : all)
-        if (v != 1.0) return false;
-    return true;
+    double v = mine;
+    for (double x : all) v = std::min(v, x);
+    return v;
 }
+
+bool dd_all_ok(mof_dd *d, bool ok, hipStream_t s) { return dd_all_min(d, ok ? 1.0 : 0.0, s) == 1.0; }
 
 // The pack -> exchange -> unpack path: the RCCL transport, or in-process
 // parts with MOF_DD_STAGED (the same kernels and segment offsets, the
@@ -408,6 +411,10 @@ void dd_ensure(mof_dd *d, int32_t B, uint32_t precision) {
     d->part_pq.alloc(2 * rec);  // by iteration parity
     d->part_rzrr.alloc(4 * rec);
     d->part_rr0.alloc(2 * rec);
+    int32_t nvmax = 0;  // k_outer_update's blocks of the largest part
+    for (const DdPart &D : d->plan.parts) nvmax = std::max(nvmax, (int32_t)((D.n_loc() + kWG - 1) / kWG));
+    d->nvmax = nvmax;
+    d->part_dx.alloc(2 * (size_t)d->P * B * nvmax);
     if (staged(d)) {
         d->sendbuf.alloc(2 * (size_t)B * std::max<int64_t>(1, d->send_base.back()));
         d->recvbuf.alloc(2 * (size_t)B * std::max<int64_t>(1, d->recv_base.back()));
@@ -749,6 +756,8 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
         sp.max_outer = o.max_outer > 0 ? o.max_outer : 10;
         sp.rtol = o.rtol > 0 ? o.rtol : 1e-8;
         sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
+        // error control: etol 0 -> 1e-7 of max|V|, < 0 -> off
+        sp.etol = o.etol > 0 ? o.etol : (o.etol < 0 ? 0.0 : 1e-7);
         sp.stall = sp.amg ? env_int_dd("MOF_PCG_STALL", 64) : 0;
         sp.fail_at_max_iter = sp.amg;
         const bool recovery = !(o.flags & MOF_NO_RECOVERY);
@@ -767,7 +776,13 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                 const double per_sys = 620.0 * (double)N * (d->rank < 0 ? 1.0 : 1.0 / d->P) + 1.0;
                 Bmax = (int32_t)std::max(1.0, std::min(64.0, 0.25 * (double)free_b / per_sys));
             }
-            const int32_t B = std::min(K, Bmax);
+            // every launch grid within 2^32 work-items (xcd_grid), checked for
+            // the largest of this rank's parts and agreed over the ranks, so
+            // that no rank refuses a launch the others go on past
+            int32_t cap = 1 << 30;
+            for (mof_mesh *m : d->parts) cap = std::min(cap, grid_batch_cap(m));
+            cap = (int32_t)dd_all_min(d, (double)cap, d->stream);
+            const int32_t B = std::min(K, std::min(Bmax, cap));
             dd_ensure(d, B, sp.precision);
             DevArray<double> Ibuf, Vbuf;
             if (!dev_io) {
@@ -861,6 +876,8 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                     for (int32_t b = 0; b < nb; ++b) {
                         if (m0->h_sysi[b * kSysStride + SI_FAILED]) st.failed++;
                         st.max_rel_residual = std::max(st.max_rel_residual, m0->h_sysd[b * kSysStride + SD_REL]);
+                        const double xm = m0->h_sysd[b * kSysStride + SD_XMAX];
+                        if (xm > 0.0) st.max_err_est = std::max(st.max_err_est, m0->h_sysd[b * kSysStride + SD_EST] / xm);
                     }
                     st.batches++;
                 }

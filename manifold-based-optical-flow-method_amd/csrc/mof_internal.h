@@ -141,6 +141,7 @@ struct Workspace {
     DevArray<double> part_pq;          // [B][nblk]
     DevArray<double> part_rzrr;        // [2][B][nblk][2]
     DevArray<double> part_rr0;         // [B][nblk][2]
+    DevArray<double> part_dx;          // [B][nvb][2]: max|d|, max|x64| per k_outer_update block
     DevArray<double> sc;               // pre-reduced PCG scalars: r.z, |r|^2 [2][B][2], p.q [2][B]
     DevArray<double> sysd;             // [B][8] per-system scalars
     DevArray<int32_t> sysi;            // [B][8] per-system flags
@@ -164,11 +165,14 @@ struct Workspace {
 //  SI_ITSUM / SI_ITMAX / SD_OUTER: the fused solve's (k_solve_fused) inner
 //  iterations summed over its refinement steps, the largest inner solve, and
 //  the refinement steps taken (the eager path counts these on the host)
-enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST = 5, SD_OUTER = 6 };
+//  SD_EST / SD_XMAX: the error estimate after the last refinement step,
+//  max|d| |r_{k+1}| / |r_k| (k_outer_check), and max|x64| (error control)
+enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST = 5, SD_OUTER = 6, SD_EST = 7,
+            SD_XMAX = 8 };
 enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_ITSUM = 3, SI_BEST_IT = 4, SI_FAIL_IT = 5, SI_FAIL_WHY = 6,
             SI_ITMAX = 7 };
 enum FailWhy { FW_BREAKDOWN = 1, FW_DIVERGED = 2, FW_STALLED = 3, FW_MAXITER = 4, FW_RESIDUAL = 5 };
-constexpr int kSysStride = 8;
+constexpr int kSysStride = 12;
 
 struct AmgDevice;     // mof_amg.h
 struct AmgHierarchy;  // mof_amg.h
@@ -319,6 +323,10 @@ struct SolveParams {
     bool amg;  // mixed precision only: multigrid V-cycle preconditioner
     int32_t max_iter, max_outer;
     double rtol, inner_rtol;
+    // error control: a system retires when its residual meets rtol AND its
+    // estimated error max|d_k| |r_{k+1}| / |r_k| (times the safety factor
+    // kErrSafety) is at most etol max|x64|; 0: the residual alone
+    double etol = 0.0;
     // stagnation window: an inner solve whose |r|^2 sets no new minimum for
     // this many iterations fails (0: off)
     int32_t stall = 0;
@@ -336,6 +344,10 @@ struct SolveParams {
     // of the hierarchy's (the recovery's damped multigrid pass)
     float amg_omega = 0.f;
 };
+// The largest batch whose launch grids all stay within 2^32 - 1 work-items
+// (xcd_grid refuses a larger one): the block-level assembly pass over the
+// SELL slots of every system is the widest grid of a solve.
+int32_t grid_batch_cap(const mof_mesh *m);
 // Solve the B assembled systems in the workspace; fills sysd/sysi.
 // Returns total inner iterations; sets *outer to the refinement steps used.
 // only (B flags, optional): re-solve just these systems; the others keep
@@ -391,6 +403,8 @@ float amg_set_omega(mof_mesh *m, float omega);
 
 // every (row block, system) pair of the XCD order (mof_rowkern.h) visited once
 bool xcd_map_covers(int32_t nblk, int32_t B, int32_t grp);
+// xcd_batch_cap on the host (tests, via mof_xcd_batch_cap)
+int32_t xcd_batch_cap_host(int64_t nblk, int32_t grp);
 double bench_spmv(mof_mesh *m, uint32_t precision, int32_t B, int32_t reps, hipStream_t s,
                   double *bytes);
 

@@ -111,6 +111,11 @@ __device__ __forceinline__ double *sc_pq(double *sc, int32_t B, int32_t slot, in
 // residual is not monotone, but 1e5 in norm is far past any transient)
 constexpr double kDiverge = 1e10;
 
+// Safety factor on the refinement's error estimate (outer_check_sys): the
+// estimate E was 0.5-1.8x the true max|V - V*| after the second step
+// (tools/error_control_study.py).
+constexpr double kErrSafety = 2.0;
+
 // Record of (this part, system b, workgroup w) in a partial array.
 __device__ __forceinline__ int64_t red_rec(const RedArgs &rd, int32_t B, int32_t b, int32_t w) {
     return ((int64_t)rd.part * B + b) * rd.nmax + w;
@@ -475,9 +480,13 @@ __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
 // tolerance is what its own outer residual still needs, 0.3 rtol |f| / |r64|,
 // kept within [rtol, 0.5] -- a system 3x above the outer target (R3 after two
 // steps: the fp32 operator's rounding limits a step to ~3e-4 there) takes a
-// short inner solve, not a full 1e-4 one.
+// short inner solve, not a full 1e-4 one. etol > 0 (error control): no
+// looser than the error estimate of the last step still needs,
+// 0.3 etol max|x64| / (kErrSafety E) -- a step that ends the residual's need
+// but not the error's gets the reduction the error is short of.
 template <typename V, int NT = kWG>
-__device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, double outer_rtol, int32_t b) {
+__device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, double outer_rtol, double etol,
+                                            int32_t b) {
     __shared__ double lds[2 * (NT / 64)];
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) {
@@ -490,7 +499,13 @@ __device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, do
         double t = rtol;
         if (outer_rtol > 0.0) {
             const double ff = a.sysd[b * kSysStride + SD_FF], rr = a.sysd[b * kSysStride + SD_RR];
-            if (ff > 0.0 && rr > 0.0) t = fmax(rtol, fmin(0.5, 0.3 * outer_rtol * sqrt(ff / rr)));
+            if (ff > 0.0 && rr > 0.0) {
+                double need = 0.3 * outer_rtol * sqrt(ff / rr);
+                const double est = a.sysd[b * kSysStride + SD_EST];
+                if (etol > 0.0 && est > 0.0)
+                    need = fmin(need, 0.3 * etol * a.sysd[b * kSysStride + SD_XMAX] / (kErrSafety * est));
+                t = fmax(rtol, fmin(0.5, need));
+            }
         }
         a.sysd[b * kSysStride + SD_TOL2] = t * t * v[1];
         a.sysd[b * kSysStride + SD_RR0] = v[1];
@@ -500,8 +515,8 @@ __device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, do
     }
 }
 template <typename V>
-__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, double outer_rtol) {
-    pcg_tol_sys<V>(a, rtol, outer_rtol, blockIdx.x);
+__global__ __launch_bounds__(kWG) void k_pcg_tol(PcgArgs<V> a, double rtol, double outer_rtol, double etol) {
+    pcg_tol_sys<V>(a, rtol, outer_rtol, etol, blockIdx.x);
 }
 
 template <typename V, bool FIRST, bool ZH = false, int NQ = 1>
@@ -773,26 +788,43 @@ __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
     pcg_update_rows<V>(a, it, blockIdx.x, blockIdx.y);
 }
 
-// x64 (+)= x_inner for systems active in the inner solve.
-template <typename V>
+// x64 (+)= x_inner for systems active in the inner solve, and the block's
+// max|d| and max|x64| over its owned rows (rdx.nown) into part_dx record
+// red_rec(rdx, B, b, blk): the error control's inputs (k_outer_check).
+template <typename V, int NQ = 1>
 __device__ __forceinline__ void outer_update_rows(int32_t N, int32_t first, const V *__restrict__ xin,
                                                   const int32_t *__restrict__ sysi, double *__restrict__ x64,
+                                                  const RedArgs &rdx, int32_t B, double *__restrict__ part_dx,
                                                   int32_t blk, int32_t b) {
+    __shared__ double lds[8 * NQ];
     if (!sysi[b * kSysStride + SI_ACTIVE]) return;
     const int32_t i = blk * kWG + row_tid();
-    if (i >= N) return;
-    const int64_t vi = (int64_t)b * N + i;
-    using V2 = typename VT<V>::V2;
-    const V2 d = *reinterpret_cast<const V2 *>(xin + 2 * vi);
-    double2 x = first ? make_double2(0.0, 0.0) : *reinterpret_cast<const double2 *>(x64 + 2 * vi);
-    x.x += (double)d.x;
-    x.y += (double)d.y;
-    *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
+    double v[2] = {0.0, 0.0};
+    if (i < N) {
+        const int64_t vi = (int64_t)b * N + i;
+        using V2 = typename VT<V>::V2;
+        const V2 d = *reinterpret_cast<const V2 *>(xin + 2 * vi);
+        double2 x = first ? make_double2(0.0, 0.0) : *reinterpret_cast<const double2 *>(x64 + 2 * vi);
+        x.x += (double)d.x;
+        x.y += (double)d.y;
+        *reinterpret_cast<double2 *>(x64 + 2 * vi) = x;
+        if (i < rdx.nown) {
+            v[0] = fmax(fabs((double)d.x), fabs((double)d.y));
+            v[1] = fmax(fabs(x.x), fabs(x.y));
+        }
+    }
+    block_max_q<2, NQ>(v, lds);
+    if (row_tid() == 0 && blk < rdx.nmax) {
+        double *o = part_dx + 2 * red_rec(rdx, B, b, blk);
+        o[0] = v[0];
+        o[1] = v[1];
+    }
 }
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_outer_update(int32_t N, int32_t first, const V *__restrict__ xin,
-                                                      const int32_t *__restrict__ sysi, double *__restrict__ x64) {
-    outer_update_rows<V>(N, first, xin, sysi, x64, blockIdx.x, blockIdx.y);
+                                                      const int32_t *__restrict__ sysi, double *__restrict__ x64,
+                                                      RedArgs rdx, int32_t B, double *__restrict__ part_dx) {
+    outer_update_rows<V>(N, first, xin, sysi, x64, rdx, B, part_dx, blockIdx.x, blockIdx.y);
 }
 
 // r64 = f - A x64 in fp64 (lambda a2 + matrix-free a1 from the fp64 u) with
@@ -904,34 +936,67 @@ __global__ __launch_bounds__(kWG) void k_residual_rcn(OpArgs<double> op, int32_t
     }
 }
 
-// One workgroup per system: relative true residual; retire converged systems.
+// Max over all parts' max|d|, max|x64| records of system b (order-free).
+template <int NT = kWG>
+__device__ __forceinline__ void reduce_max_sys(const double *part, const RedArgs &rdx, int32_t B, int32_t b,
+                                               double (&out)[2], double *lds) {
+    out[0] = out[1] = 0.0;
+    for (int32_t q = 0; q < rdx.P; ++q) {
+        const double *p = part + 2 * ((int64_t)q * B + b) * rdx.nmax;
+        for (int32_t w = threadIdx.x; w < rdx.nmax; w += NT) {
+            out[0] = fmax(out[0], p[2 * (int64_t)w]);
+            out[1] = fmax(out[1], p[2 * (int64_t)w + 1]);
+        }
+    }
+    block_max<2, NT>(out, lds);
+}
+
+// One workgroup per system: relative true residual and error estimate;
+// retire converged systems. The estimate of the error left after step k,
+//   E = max|d_k| |r_{k+1}|_2 / |r_k|_2   (r_0 = f, so first: |r_k|^2 = |f|^2),
+// is the last correction scaled by the step's residual reduction: A^-1's
+// gain along r_k taken for r_{k+1}. From the second step on both residuals
+// lie in the slow modes the first inner solve left, and E is within 0.5-1.8x
+// of max|V - V*| (tools/error_control_study.py: S1-like patch, C2, C3; the
+// first step's E underestimates ~100x on the open patch, but no first step
+// of the mixed solve meets rtol). A system retires when rel <= rtol and, with
+// etol > 0, kErrSafety E <= etol max|x64|.
 template <int NT = kWG>
 __device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, const double *__restrict__ part,
-                                                double rtol, double *__restrict__ sysd, int32_t *__restrict__ sysi,
+                                                const RedArgs &rdx, const double *__restrict__ part_dx,
+                                                int32_t first, double rtol, double etol,
+                                                double *__restrict__ sysd, int32_t *__restrict__ sysi,
                                                 int32_t b) {
     __shared__ double lds[2 * (NT / 64)];
     int32_t *si = sysi + b * kSysStride;
     if (!si[SI_ACTIVE]) return;
-    double v[2];
+    double v[2], dx[2];
     reduce_sys<2, NT>(part, rd, B, b, v, lds);
+    reduce_max_sys<NT>(part_dx, rdx, B, b, dx, lds);
     if (threadIdx.x == 0) {
+        double *sd = sysd + b * kSysStride;
         const double rel = v[1] > 0.0 ? sqrt(v[0] / v[1]) : (v[0] > 0.0 ? INFINITY : 0.0);
-        sysd[b * kSysStride + SD_REL] = rel;
-        sysd[b * kSysStride + SD_RR] = v[0];
-        sysd[b * kSysStride + SD_FF] = v[1];
-        if (!isfinite(rel)) {
+        const double rr_prev = first ? v[1] : sd[SD_RR];
+        const double est = rr_prev > 0.0 ? dx[0] * sqrt(v[0] / rr_prev) : 0.0;
+        sd[SD_REL] = rel;
+        sd[SD_RR] = v[0];
+        sd[SD_FF] = v[1];
+        sd[SD_EST] = est;
+        sd[SD_XMAX] = dx[1];
+        if (!isfinite(rel) || !isfinite(est)) {
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
             si[SI_FAIL_WHY] = FW_RESIDUAL;
-        } else if (rel <= rtol) {
+        } else if (rel <= rtol && (etol <= 0.0 || kErrSafety * est <= etol * dx[1])) {
             si[SI_ACTIVE] = 0;
         }
     }
 }
 __global__ __launch_bounds__(kWG) void k_outer_check(RedArgs rd, int32_t B, const double *__restrict__ part,
-                                                     double rtol, double *__restrict__ sysd,
-                                                     int32_t *__restrict__ sysi) {
-    outer_check_sys<kWG>(rd, B, part, rtol, sysd, sysi, blockIdx.x);
+                                                     RedArgs rdx, const double *__restrict__ part_dx,
+                                                     int32_t first, double rtol, double etol,
+                                                     double *__restrict__ sysd, int32_t *__restrict__ sysi) {
+    outer_check_sys<kWG>(rd, B, part, rdx, part_dx, first, rtol, etol, sysd, sysi, blockIdx.x);
 }
 
 __global__ void k_sys_reset(int32_t B, int32_t *__restrict__ sysi, double *__restrict__ sysd) {
@@ -945,10 +1010,16 @@ __global__ void k_sys_reset(int32_t B, int32_t *__restrict__ sysi, double *__res
     sysi[b * kSysStride + SI_CONV] = -1;
 }
 
-__global__ void k_mark_unconverged(int32_t B, int32_t *__restrict__ sysi) {
+// Systems still active after the last refinement step fail -- except one
+// whose residual met rtol and only the error estimate did not (kept; its
+// estimate is reported through mof_stats.max_err_est).
+__global__ void k_mark_unconverged(int32_t B, double rtol, const double *__restrict__ sysd,
+                                   int32_t *__restrict__ sysi) {
     const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    if (sysi[b * kSysStride + SI_ACTIVE]) {
+    if (sysi[b * kSysStride + SI_ACTIVE] && sysd[b * kSysStride + SD_REL] <= rtol) {
+        sysi[b * kSysStride + SI_ACTIVE] = 0;
+    } else if (sysi[b * kSysStride + SI_ACTIVE]) {
         sysi[b * kSysStride + SI_FAILED] = 1;
         sysi[b * kSysStride + SI_ACTIVE] = 0;
         sysi[b * kSysStride + SI_FAIL_WHY] = FW_MAXITER;
@@ -1101,7 +1172,7 @@ void charge_chunk(const mof_mesh *m, int32_t B, const std::vector<int32_t> &runn
 template <typename V>
 int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const double *rhs,
             double rtol, const SolveParams &sp, hipStream_t s, int32_t *max_iters, SpmvTiming *timing,
-            int32_t *hint, bool amg, double outer_rtol = 0.0) {
+            int32_t *hint, bool amg, double outer_rtol = 0.0, double etol = 0.0) {
     const int32_t max_iter = sp.max_iter;
     PcgArgs<V> a = make_args<V>(m, B, mat, dinv);
     a.ext = amg ? 1 : 0;
@@ -1128,7 +1199,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B, kGrpSpmv));
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
-    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol);
+    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol, etol);
     if (amg) precond(0);
     k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, 0);
     MOF_HIP(hipGetLastError());
@@ -1231,8 +1302,8 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
 // (tests/test_gpu_fused.py). One launch and one flag fetch per batch.
 struct FusedArgs {
     const double *rhs;  // f of every system
-    double *x64, *r64, *part_rr0;
-    double rtol, inner_rtol;
+    double *x64, *r64, *part_rr0, *part_dx;
+    double rtol, inner_rtol, etol;
     int32_t max_iter, max_outer, adaptive;
 };
 
@@ -1266,7 +1337,8 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
         const double *rhs = o == 0 ? f.rhs : f.r64;
         for (int32_t rb = 0; rb < a.nblk; rb += NQ) pcg_init_rows<double, NQ>(a, rhs, rb + q, b);
         __syncthreads();
-        pcg_tol_sys<double, NT>(a, o == 0 ? 0.5 * f.rtol : f.inner_rtol, o > 0 && f.adaptive ? f.rtol : 0.0, b);
+        pcg_tol_sys<double, NT>(a, o == 0 ? 0.5 * f.rtol : f.inner_rtol, o > 0 && f.adaptive ? f.rtol : 0.0, f.etol,
+                                b);
         __syncthreads();
         red_rzrr_sys<double, NT>(a, 0, b);
         __syncthreads();
@@ -1307,12 +1379,14 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
                                           : it);
         itsum += its;
         itmax = max(itmax, its);
-        for (int32_t blk = 0; blk < nvb; blk += NQ) outer_update_rows<double>(a.N, o == 0, a.x, a.sysi, f.x64, blk + q, b);
+        const RedArgs rdx{1, 0, nvb, a.N};
+        for (int32_t blk = 0; blk < nvb; blk += NQ)
+            outer_update_rows<double, NQ>(a.N, o == 0, a.x, a.sysi, f.x64, rdx, a.B, f.part_dx, blk + q, b);
         __syncthreads();
         for (int32_t rb = 0; rb < a.nblk; rb += NQ)
             residual_rows<NQ>(op, a.B, a.red, f.rhs, f.x64, a.sysi, f.r64, f.part_rr0, rb + q, b);
         __syncthreads();
-        outer_check_sys<NT>(a.red, a.B, f.part_rr0, f.rtol, a.sysd, a.sysi, b);
+        outer_check_sys<NT>(a.red, a.B, f.part_rr0, rdx, f.part_dx, o == 0, f.rtol, f.etol, a.sysd, a.sysi, b);
         __syncthreads();
         if (!ld_flag(si + SI_ACTIVE)) {
             ++o;
@@ -1320,7 +1394,9 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
         }
     }
     if (threadIdx.x == 0) {
-        if (si[SI_ACTIVE]) {  // k_mark_unconverged
+        if (si[SI_ACTIVE] && sd[SD_REL] <= f.rtol) {  // k_mark_unconverged
+            si[SI_ACTIVE] = 0;
+        } else if (si[SI_ACTIVE]) {
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
             si[SI_FAIL_WHY] = FW_MAXITER;
@@ -1332,6 +1408,13 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
 }
 
 }  // namespace
+
+int32_t xcd_batch_cap_host(int64_t nblk, int32_t grp) { return xcd_batch_cap(nblk, grp); }
+
+int32_t grid_batch_cap(const mof_mesh *m) {
+    const int64_t per = (m->pat.sell_nb() + kWG - 1) / kWG;  // k_assemble_* / k_tri blocks per system
+    return std::min(xcd_batch_cap(per, kGrpAsm), xcd_batch_cap(m->ws.nblk > 0 ? m->ws.nblk : per, kGrpSpmv));
+}
 
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active) {
     // SURVEY.md 8(d)'s algorithmic bytes of a batched CSR SpMV: per system the
@@ -1386,6 +1469,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.sc.alloc((size_t)6 * B);
     w.sc.zero(m->stream);
     w.part_rr0.alloc((size_t)2 * w.nblk * B);
+    w.part_dx.alloc((size_t)2 * ((N + kWG - 1) / kWG) * B);
     w.sysd.alloc((size_t)kSysStride * B);
     w.sysi.alloc((size_t)kSysStride * B);
     w.dt.alloc(B);
@@ -1439,8 +1523,9 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         // eager loop below
         PcgArgs<double> a = make_args<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p);
         a.stall = sp.stall;
-        const FusedArgs fa{w.rhs.p, w.x64.p, w.r64.p, w.part_rr0.p, sp.rtol, sp.inner_rtol,
-                           sp.max_iter, sp.max_outer, sp.adaptive_inner ? 1 : 0};
+        const FusedArgs fa{w.rhs.p, w.x64.p,   w.r64.p,     w.part_rr0.p, w.part_dx.p,
+                           sp.rtol, sp.inner_rtol, sp.etol,     sp.max_iter, sp.max_outer,
+                           sp.adaptive_inner ? 1 : 0};
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (tm) {
             if (m->spmv_events.size() < 2) {
@@ -1521,6 +1606,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     } omega_scope(m, sp.amg_omega, amg);
     dim3 g((unsigned)w.nblk, (unsigned)B);
     dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);  // one row per thread
+    const RedArgs rdx{1, 0, (int32_t)gv.x, m->N};                 // k_outer_update's max records
     int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
     // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
@@ -1531,33 +1617,39 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             // hints per (precision, preconditioner, refinement step)
             iters += pcg<float>(m, B, make_mat<float>(m, w.A32.p), w.dinv32.p, rhs, sp.inner_rtol, sp, s,
                                 max_iters, tm, &m->iter_hint[(amg ? 16 : 32) + std::min(o, 15)], amg,
-                                o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
+                                o > 0 && sp.adaptive_inner ? sp.rtol : 0.0, sp.etol);
             k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                    w.sysi.p, w.x64.p);
+                                                    w.sysi.p, w.x64.p, rdx, B, w.part_dx.p);
         } else {
             iters += pcg<double>(m, B, make_mat<double>(m, w.A64.p), w.dinv64.p, rhs,
                                  o == 0 ? 0.5 * sp.rtol : sp.inner_rtol, sp, s, max_iters, tm,
-                                 &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0);
-            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+                                 &m->iter_hint[std::min(o, 15)], false, o > 0 && sp.adaptive_inner ? sp.rtol : 0.0,
+                                 sp.etol);
+            k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p, rdx, B,
+                                                     w.part_dx.p);
         }
         const RedArgs rd{1, 0, w.nblk, m->N};
         launch_residual(m, w.nblk, B, s, rd, w.rhs.p, w.x64.p, w.sysi.p,
                                                               w.r64.p, w.part_rr0.p);
-        k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, sp.rtol, w.sysd.p,
-                                                        w.sysi.p);
+        k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, w.part_rr0.p, rdx, w.part_dx.p, o == 0, sp.rtol,
+                                                        sp.etol, w.sysd.p, w.sysi.p);
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
         bool any = false;
         for (int32_t b = 0; b < B; ++b) any |= m->h_sysi[b * kSysStride + SI_ACTIVE] != 0;
         if (verbose) {
-            double worst = 0.0;
+            double worst = 0.0, west = 0.0;
             int32_t act = 0;
             for (int32_t b = 0; b < B; ++b) {
-                worst = std::max(worst, m->h_sysd[b * kSysStride + SD_REL]);
+                const double *sd = m->h_sysd + b * kSysStride;
+                worst = std::max(worst, sd[SD_REL]);
+                if (sd[SD_XMAX] > 0.0) west = std::max(west, sd[SD_EST] / sd[SD_XMAX]);
                 act += m->h_sysi[b * kSysStride + SI_ACTIVE] != 0;
             }
-            std::fprintf(stderr, "[mof solve] B=%d outer %d: %lld inner its (sum), max rel residual %.3e, %d still active\n",
-                         B, o, (long long)(iters - iters_before), worst, act);
+            std::fprintf(stderr,
+                         "[mof solve] B=%d outer %d: %lld inner its (sum), max rel residual %.3e, max error est %.3e "
+                         "of max|V|, %d still active\n",
+                         B, o, (long long)(iters - iters_before), worst, west, act);
             iters_before = iters;
         }
         if (!any) {
@@ -1565,7 +1657,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
             break;
         }
     }
-    k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, w.sysi.p);
+    k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, sp.rtol, w.sysd.p, w.sysi.p);
     MOF_HIP(hipGetLastError());
     fetch_flags(m, B, s);
     *outer = o;
@@ -1640,7 +1732,7 @@ int64_t pcg_dd(mof_dd *d, int32_t B, bool first_outer, double rtol, const SolveP
     dd_sync_partials(d, d->part_rzrr.p, 2 * rec, s);
     // the tolerance step resets the convergence word the cycle's kernels
     // check, so it runs before the first cycle
-    for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol, 0.0);
+    for (size_t l = 0; l < L; ++l) k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(args[l], rtol, 0.0, 0.0);
     if (amg)
         precond(0);
     else
@@ -1712,6 +1804,7 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
     MOF_HIP(hipMemsetAsync(d->part_pq.p, 0, d->part_pq.bytes(), s));
     MOF_HIP(hipMemsetAsync(d->part_rzrr.p, 0, d->part_rzrr.bytes(), s));
     MOF_HIP(hipMemsetAsync(d->part_rr0.p, 0, d->part_rr0.bytes(), s));
+    MOF_HIP(hipMemsetAsync(d->part_dx.p, 0, d->part_dx.bytes(), s));  // a smaller part's tail records stay 0
     if (!only) {
         for (size_t l = 0; l < L; ++l) {
             Workspace &w = d->parts[l]->ws;
@@ -1763,12 +1856,15 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
             mof_mesh *m = d->parts[l];
             Workspace &w = m->ws;
             dim3 gv((unsigned)((m->N + kWG - 1) / kWG), (unsigned)B);
+            const RedArgs rdx{d->P, d->part_ids[l], d->nvmax, d->plan.parts[d->part_ids[l]].n_own};
             if (sp.precision == MOF_PREC_MIXED)
                 k_outer_update<float><<<gv, kWG, 0, s>>>(m->N, o == 0, reinterpret_cast<float *>(w.vx.p),
-                                                        w.sysi.p, w.x64.p);
+                                                        w.sysi.p, w.x64.p, rdx, B, d->part_dx.p);
             else
-                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p);
+                k_outer_update<double><<<gv, kWG, 0, s>>>(m->N, o == 0, w.vx.p, w.sysi.p, w.x64.p, rdx, B,
+                                                         d->part_dx.p);
         }
+        dd_sync_partials(d, d->part_dx.p, 2 * (int64_t)B * d->nvmax, s);
         dd_halo(d, B, false, 1, s);  // the residual reads x64 at the ghosts
         for (size_t l = 0; l < L; ++l) {
             mof_mesh *m = d->parts[l];
@@ -1781,7 +1877,9 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
         for (size_t l = 0; l < L; ++l) {
             Workspace &w = d->parts[l]->ws;
             const RedArgs rd{d->P, d->part_ids[l], d->nmax, 0};
-            k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, d->part_rr0.p, sp.rtol, w.sysd.p, w.sysi.p);
+            const RedArgs rdx{d->P, d->part_ids[l], d->nvmax, 0};
+            k_outer_check<<<dim3((unsigned)B), kWG, 0, s>>>(rd, B, d->part_rr0.p, rdx, d->part_dx.p, o == 0, sp.rtol,
+                                                            sp.etol, w.sysd.p, w.sysi.p);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m0, B, s);
@@ -1793,7 +1891,8 @@ int64_t solve_batch_dd(mof_dd *d, int32_t B, const SolveParams &sp, hipStream_t 
         }
     }
     for (size_t l = 0; l < L; ++l)
-        k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, d->parts[l]->ws.sysi.p);
+        k_mark_unconverged<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, sp.rtol, d->parts[l]->ws.sysd.p,
+                                                                          d->parts[l]->ws.sysi.p);
     MOF_HIP(hipGetLastError());
     fetch_flags(m0, B, s);
     *outer = o;

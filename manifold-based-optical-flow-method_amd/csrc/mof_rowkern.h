@@ -129,6 +129,51 @@ __device__ __forceinline__ void block_sum_q(double (&v)[NV], double *lds) {
 // the thread's index within its group of kWG (row kernels: its row)
 __device__ __forceinline__ int32_t row_tid() { return (int32_t)(threadIdx.x & (kWG - 1)); }
 
+// Maxima of non-negative values (the refinement's error control): the
+// order-free counterparts of wave_sum / block_sum_q.
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
+    return v;  // valid in lane 0
+}
+// over each group of kWG threads of an NQ * kWG workgroup (lds: NQ * 4 * NV
+// doubles); every thread of the group gets its group's maxima
+template <int NV, int NQ>
+__device__ __forceinline__ void block_max_q(double (&v)[NV], double *lds) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_max(v[k]);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+    }
+    __syncthreads();
+    const double *L = lds + (w & ~3) * NV;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = fmax(fmax(L[k], L[NV + k]), fmax(L[2 * NV + k], L[3 * NV + k]));
+    __syncthreads();
+}
+// over the whole NT-thread workgroup (lds: NT / 64 * NV doubles)
+template <int NV, int NT>
+__device__ __forceinline__ void block_max(double (&v)[NV], double *lds) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_max(v[k]);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = lds[k];
+#pragma unroll
+        for (int q = 1; q < NT / 64; ++q) s = fmax(s, lds[q * NV + k]);
+        v[k] = s;
+    }
+    __syncthreads();
+}
+
 // Sum n partials of NV values each (record stride NV) in a fixed order: the
 // first kWG threads load, so any workgroup size NT gets the same bits.
 template <int NV, int NT = kWG>
@@ -316,6 +361,19 @@ inline unsigned xcd_grid(int32_t nblk, int32_t B, int32_t grp_sz) {
     const int64_t n = 8 * G * ((B + G - 1) / G) * ((nblk + 7) / 8);
     MOF_REQUIRE(n * kWG < ((int64_t)1 << 32), "launch grid past 2^32 work-items (batch too large for this mesh)");
     return (unsigned)n;
+}
+// The largest batch whose xcd_grid over `nblk` blocks per system (system
+// groups of grp_sz) stays within 2^32 - 1 work-items.
+inline int32_t xcd_batch_cap(int64_t nblk, int32_t grp_sz) {
+    const int64_t lim = (((int64_t)1 << 32) - 1) / kWG;  // workgroups
+    const int64_t per = 8 * ((nblk + 7) / 8);          // workgroups per system (padded to the 8 XCDs)
+    int64_t B = std::min<int64_t>(lim / per, 1 << 30);
+    auto n = [&](int64_t b) {
+        const int64_t G = b > grp_sz && grp_sz > 0 ? grp_sz : b;
+        return 8 * G * ((b + G - 1) / G) * ((nblk + 7) / 8);
+    };
+    while (B > 1 && n(B) > lim) --B;
+    return (int32_t)std::max<int64_t>(1, B);
 }
 
 

@@ -20,7 +20,7 @@ CSRC_DIR = os.path.join(ROOT_DIR, "csrc")
 LIB_PATH = os.environ.get("MOFHIP_LIB") or os.path.join(PKG_DIR, "libmofhip.so")
 
 # include/mof.h MOF_ABI_VERSION this binding's structs follow
-MOF_ABI_VERSION = 3
+MOF_ABI_VERSION = 4
 
 MOF_OK = 0
 MOF_E_ARG = -1
@@ -54,7 +54,7 @@ EXPORTS = (
     "mof_point_normals", "mof_cell_areas", "mof_singularities", "mof_amg_probe",
     "mof_partition_rcb", "mof_dd_plan_info", "mof_dd_create", "mof_dd_unique_id",
     "mof_dd_create_rank", "mof_dd_destroy", "mof_dd_get_info", "mof_dd_solve_range",
-    "mof_singularities_compact", "mof_xcd_map_check", "mof_dd_create_rank_host",
+    "mof_singularities_compact", "mof_xcd_map_check", "mof_xcd_batch_cap", "mof_dd_create_rank_host",
 )
 
 
@@ -76,6 +76,7 @@ class MofOpts(ctypes.Structure):
         ("flags", ctypes.c_uint32), ("batch", ctypes.c_int32), ("max_iter", ctypes.c_int32),
         ("max_outer", ctypes.c_int32), ("rtol", ctypes.c_double),
         ("inner_rtol", ctypes.c_double), ("stream", ctypes.c_void_p),
+        ("etol", ctypes.c_double),
     ]
 
 
@@ -90,7 +91,7 @@ class MofStats(ctypes.Structure):
         ("spmv_systems", ctypes.c_int64), ("spmv_full_launches", ctypes.c_int64),
         ("ms_spmv_full", ctypes.c_double), ("recovered", ctypes.c_int32),
         ("recovered_f64", ctypes.c_int32), ("fused_launches", ctypes.c_int64),
-        ("ms_fused", ctypes.c_double),
+        ("ms_fused", ctypes.c_double), ("max_err_est", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -103,6 +104,7 @@ class MofMeshInfo(ctypes.Structure):
         ("nblocks", ctypes.c_int32), ("nnz_struct", ctypes.c_int64),
         ("sell_blocks", ctypes.c_int64), ("ms_geometry", ctypes.c_double),
         ("ms_pattern", ctypes.c_double), ("blocks_read", ctypes.c_int64),
+        ("max_batch", ctypes.c_int32), ("pad_", ctypes.c_int32),
     ]
 
 
@@ -181,6 +183,7 @@ def lib():
                                   ctypes.c_int),
             "mof_amg_probe": ([P, P, i32, i32, P, P, P], ctypes.c_int),
             "mof_xcd_map_check": ([i32, i32, i32], ctypes.c_int),
+            "mof_xcd_batch_cap": ([i64, i32, P], ctypes.c_int),
             "mof_singularities_compact": ([i32, P, P, i32, i32, P, i32, f64, u32, P, i64, P, P, P, P, P,
                                            P, P], ctypes.c_int),
             "mof_partition_rcb": ([P, i32, i32, P], ctypes.c_int),

@@ -190,13 +190,15 @@ class DeviceMesh:
     @staticmethod
     def make_opts(precision="f64", batch=0, rtol=0.0, inner_rtol=0.0, max_iter=0, max_outer=0,
                   block_jacobi=True, device_io=False, time_spmv=False, stream=None,
-                  precond="jacobi", recovery=True, fused=None) -> L.MofOpts:
+                  precond="jacobi", recovery=True, fused=None, etol=0.0) -> L.MofOpts:
         """precond: "jacobi" (2x2 block Jacobi) or "amg" (aggregation-multigrid
         V-cycle; precision="mixed" only). recovery=False: a failed system is
         NaN-filled at once (MOF_NO_RECOVERY) instead of re-solved with block
         Jacobi and then fp64. fused (precision="f64"): True -- each batch's
         solve in one launch (MOF_SOLVE_FUSED), False -- never, None -- the
-        library's choice (small meshes)."""
+        library's choice (small meshes). etol: the refinement's error
+        control -- a system also needs its estimated error below etol max|V|
+        (0: the library's 1e-7, < 0: the residual test alone)."""
         o = L.MofOpts()
         o.struct_size = ctypes.sizeof(L.MofOpts)
         o.precision = {"f64": L.MOF_PREC_F64, "mixed": L.MOF_PREC_MIXED}[precision]
@@ -212,6 +214,7 @@ class DeviceMesh:
         o.rtol = float(rtol)
         o.inner_rtol = float(inner_rtol)
         o.stream = stream
+        o.etol = float(etol)
         return o
 
     def fingerprint(self) -> str:

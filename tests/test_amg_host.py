@@ -79,3 +79,22 @@ def test_xcd_grid_past_dispatch_limit_fails_loudly():
     with pytest.raises(L.MofError):
         L.check(L.lib().mof_xcd_map_check(40000, 1024, 8))
     L.check(L.lib().mof_xcd_map_check(641, 1024, 8))  # C3's size: fine
+
+
+def test_batch_cap_keeps_every_grid_within_dispatch_limit():
+    """The batch the library never passes (mof_mesh_info.max_batch: the
+    auto and explicit batches are clamped to it) is the largest whose
+    XCD-ordered grid fits 2^32 - 1 work-items: one more system is refused.
+    40,000 blocks per system is a 10 M-slot operator (the block assembly's
+    grid at ~1.4 M vertices); 4,608 is C3's (1.18 M SELL slots)."""
+    for nblk, grp in ((40000, 8), (4608, 8), (641, 8), (12345, 0)):
+        cap = ctypes.c_int32(0)
+        L.check(L.lib().mof_xcd_batch_cap(nblk, grp, ctypes.byref(cap)))
+        assert cap.value >= 1
+        if nblk * cap.value < 2 ** 31:  # mof_xcd_map_check walks every workgroup: small grids only
+            L.check(L.lib().mof_xcd_map_check(nblk, cap.value, grp))
+        with pytest.raises(L.MofError):
+            L.check(L.lib().mof_xcd_map_check(nblk, cap.value + 8, grp))
+    cap = ctypes.c_int32(0)
+    L.check(L.lib().mof_xcd_batch_cap(4608, 8, ctypes.byref(cap)))
+    assert 3000 < cap.value < 3700  # C3: B = 1024 fits, ~3.6 k would not

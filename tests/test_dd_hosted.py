@@ -69,7 +69,7 @@ def test_host_transport_ranks_match_in_process(P, opts):
     ref = DecomposedMesh(p, n, t, a, P, part=part, staged=True)
     Vr, sr = ref.solve_range(I, np.arange(len(I), dtype=np.float64), 0, len(I) - 1, 0.01, **opts)
     ref.close()
-    assert sr["failed"] == 0
+    assert sr["failed"] == sr["recovered"] == 0
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

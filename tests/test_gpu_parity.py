@@ -67,7 +67,7 @@ def test_velocity_field_vs_spsolve(golden, precision):
                           precision=precision, rtol=1e-10)
     ref = golden["V_k"]
     scale = max(1.0, np.abs(ref).max())  # G5 (dt = 1/512) has |V| ~ 600
-    assert st["failed"] == 0
+    assert st["failed"] == st["recovered"] == 0
     assert st["max_rel_residual"] <= 1e-10
     assert np.abs(V - ref).max() <= VTOL * scale
 
@@ -173,7 +173,7 @@ def test_irregular_meshes_vs_oracle(kind):
     assert np.array_equal(f, fo)
     for prec in ("f64", "mixed"):
         V, st = m.solve_range(I, np.arange(4.0), 0, 3, 0.01, precision=prec)
-        assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8
+        assert st["failed"] == st["recovered"] == 0 and st["max_rel_residual"] <= 1e-8
         for k in range(3):
             Vo = oracle.worker(k, a2, gw, e, iw, t, list(range(4)), a, 0.01, I[k], I[k + 1])
             assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), (prec, k)
@@ -213,7 +213,7 @@ def test_160k_properties():
     V64, s64 = m.solve_range(I, tk, 0, 4, 0.01, precision="f64", batch=4)
     Vmx, smx = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", batch=4)
     Vmx2, _ = m.solve_range(I, tk, 0, 4, 0.01, precision="mixed", batch=2)
-    assert s64["failed"] == 0 and smx["failed"] == 0
+    assert s64["failed"] == s64["recovered"] == 0 and smx["failed"] == smx["recovered"] == 0
     assert s64["max_rel_residual"] <= 1e-8 and smx["max_rel_residual"] <= 1e-8
     assert np.abs(V64 - Vmx).max() < VTOL
     assert np.array_equal(Vmx, Vmx2)

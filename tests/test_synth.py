@@ -47,3 +47,17 @@ def test_icosphere_counts():
         p, t = synth.icosphere(n)
         assert len(p) == 10 * n * n + 2 and len(t) == 20 * n * n
         assert _check_manifold(p, t) == 0
+
+
+def test_folded_sphere():
+    """F3's folded cortex-like surface (synth.folded_sphere) on a small
+    topology: the icosphere's counts, every triangle outward (a radial graph
+    cannot fold), the configured peak-to-trough depth, seeded."""
+    p, t = synth.folded_sphere(16, radius=10.0, depth=0.3)
+    assert p.shape == (10 * 16 ** 2 + 2, 3) and t.shape == (20 * 16 ** 2, 3)
+    r = np.linalg.norm(p, axis=1)
+    assert abs(r.min() - 8.5) < 1e-9 and abs(r.max() - 11.5) < 1e-9
+    c = np.cross(p[t[:, 1]] - p[t[:, 0]], p[t[:, 2]] - p[t[:, 0]])
+    assert ((c * p[t].mean(axis=1)).sum(axis=1) > 0).all()
+    p2, _ = synth.folded_sphere(16, radius=10.0, depth=0.3)
+    assert np.array_equal(p, p2)
