@@ -486,6 +486,16 @@ def main():
                 "kernel_full_launch_frac": round((B * k_sys + k_shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
                 if t_full > 0 else None}
 
+    if agg["spmv_launches"] == 0 and agg["fused_launches"] > 0:
+        # the fused one-launch solve (small meshes) runs its SpMV inside one
+        # kernel per batch with no per-SpMV timing: no SpMV roofline is
+        # measured, and the line says so instead of reporting 0 GB/s
+        roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                    "traffic": None, "kernel": "k_solve_fused (the whole fp64 solve of a batch in one launch)",
+                    "us_per_launch": round(1e3 * agg["ms_fused"] / agg["fused_launches"], 2),
+                    "launches": agg["fused_launches"],
+                    "note": "no per-SpMV timing inside the fused launch: the SpMV roofline is not measured"}
+
     # host-to-host leg (SURVEY.md 8(d)'s metric: host I -> host V_k, the
     # reference's submit -> join, compute_optical_flow.py:160-182), measured in
     # this invocation after the device-resident region: pageable numpy I in,

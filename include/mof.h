@@ -414,6 +414,10 @@ int mof_dd_create_rank_host(const double *xyz, const double *nrm, const int32_t 
                             const mof_dd_transport *transport, int32_t device, uint32_t flags, mof_dd **out);
 int mof_dd_destroy(mof_dd *dd);
 int mof_dd_get_info(const mof_dd *dd, mof_dd_info *info);
+/* Test hook (never read from the environment): the fp64 recovery pass's
+ * workspace allocation reports a failure on rank `rank` of this handle's
+ * solves (-1: off) -- exercises the ranks' agreement on a failed recovery. */
+int mof_dd_test_fail_recovery_alloc(mof_dd *dd, int32_t rank);
 
 /* mof_solve_range on the decomposed system (same arguments and results; with
  * RCCL every rank passes the same k-range and receives the whole V). */

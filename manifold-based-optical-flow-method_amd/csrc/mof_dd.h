@@ -74,6 +74,7 @@ struct mof_dd {
     hipStream_t stream = nullptr;
     int32_t cap = 0, nmax = 0;       // systems / workgroups per part the partials hold
     mof::DevArray<double> part_pq, part_rzrr, part_rr0;  // [2][P][B][nmax] (x NV)
+    int32_t test_oom_rank = -1;          // mof_dd_test_fail_recovery_alloc (tests only)
     int32_t nvmax = 0;                   // k_outer_update blocks of the largest part
     mof::DevArray<double> part_dx;       // [P][B][nvmax][2]: max|d|, max|x64| (error control)
     // in-process halo: one entry per ghost row of every part

@@ -708,6 +708,13 @@ int mof_dd_destroy(mof_dd *d) {
     return mof_io_guard([&] { dd_free(d); });
 }
 
+int mof_dd_test_fail_recovery_alloc(mof_dd *d, int32_t rank) {
+    return mof_io_guard([&] {
+        MOF_REQUIRE(d, "NULL argument");
+        d->test_oom_rank = rank;
+    });
+}
+
 int mof_dd_get_info(const mof_dd *d, mof_dd_info *info) {
     return mof_io_guard([&] {
         MOF_REQUIRE(d && info, "NULL argument");
@@ -845,8 +852,8 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
                                     ok = false;
                                     err = e;
                                 }
-                                if (d->rank >= 0 && env_int_dd("MOF_DD_TEST_OOM_RANK", -1) == d->rank && prec == MOF_PREC_F64) {
-                                    ok = false;  // test hook: this rank's fp64 workspace "fails"
+                                if (d->rank >= 0 && d->test_oom_rank == d->rank && prec == MOF_PREC_F64) {
+                                    ok = false;  // test hook (mof_dd_test_fail_recovery_alloc): this rank's fp64 workspace "fails"
                                     err = Error{MOF_E_HIP, "injected allocation failure"};
                                 }
                                 if (!dd_all_ok(d, ok, s))

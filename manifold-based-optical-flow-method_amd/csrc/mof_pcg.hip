@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
 // steps: the fp32 operator's rounding limits a step to ~3e-4 there) takes a
 // short inner solve, not a full 1e-4 one. etol > 0 (error control): no
 // looser than the error estimate of the last step still needs,
-// 0.3 etol max|x64| / (kErrSafety E) -- a step that ends the residual's need
+// 0.5 etol max|x64| / (kErrSafety E) -- a step that ends the residual's need
 // but not the error's gets the reduction the error is short of.
 template <typename V, int NT = kWG>
 __device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, double outer_rtol, double etol,
@@ -503,7 +503,7 @@ __device__ __forceinline__ void pcg_tol_sys(const PcgArgs<V> &a, double rtol, do
                 double need = 0.3 * outer_rtol * sqrt(ff / rr);
                 const double est = a.sysd[b * kSysStride + SD_EST];
                 if (etol > 0.0 && est > 0.0)
-                    need = fmin(need, 0.3 * etol * a.sysd[b * kSysStride + SD_XMAX] / (kErrSafety * est));
+                    need = fmin(need, 0.5 * etol * a.sysd[b * kSysStride + SD_XMAX] / (kErrSafety * est));
                 t = fmax(rtol, fmin(0.5, need));
             }
         }

@@ -57,9 +57,20 @@ def _digest(*parts) -> str:
     return h.hexdigest()
 
 
+# MOF_* switches that cannot change a saved V: logging, host staging sizes,
+# the fused solve's width and eligibility (bit-identical to the eager path),
+# the checkpoint's own settings, the RCCL library path
+_KEY_NEUTRAL = frozenset((
+    "MOF_CHECKPOINT_DIR", "MOF_CHECKPOINT_CHUNK", "MOF_SOLVE_VERBOSE", "MOF_AMG_VERBOSE", "MOF_HOSTIO_VERBOSE",
+    "MOF_STAGE_MB", "MOF_STAGE_DIRECT_MB", "MOF_IO_THREADS", "MOF_FUSED_NQ", "MOF_FUSED_MAX_BLK", "MOF_RCCL_LIB",
+))
+
+
 def _library_key() -> tuple:
-    """Library version and ABI, and the MOF_* environment switches (sorted):
-    a rebuilt library or another solver setting must not reuse old chunks."""
+    """Library version and ABI, and the MOF_* environment switches that may
+    change V (sorted; _KEY_NEUTRAL excluded): a rebuilt library or another
+    solver setting must not reuse old chunks, a log switch must not discard
+    them."""
     try:
         from . import _lib as L
         lib = L.lib()
@@ -67,7 +78,7 @@ def _library_key() -> tuple:
     except Exception:  # no library (CPU tests with a stand-in mesh)
         ver = ("", 0)
     env = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("MOF_")
-                       and k != "MOF_CHECKPOINT_DIR"))
+                       and k not in _KEY_NEUTRAL))
     return ver, env
 
 

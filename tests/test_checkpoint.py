@@ -124,3 +124,19 @@ def test_environment_switches_invalidate_chunks(tmp_path, monkeypatch):
     m.reorder = False  # another device vertex order: stale as well
     velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
     assert len(m.calls) == 3
+
+
+def test_log_switches_keep_chunks(tmp_path, monkeypatch):
+    """Switches that cannot change V (logging, staging sizes, the fused
+    solve's width) leave the saved chunks valid (round-4 advisor)."""
+    I, tk = _inputs()
+    m = _Mesh()
+    for k in ("MOF_SOLVE_VERBOSE", "MOF_HOSTIO_VERBOSE", "MOF_STAGE_MB", "MOF_FUSED_NQ"):
+        monkeypatch.delenv(k, raising=False)
+    velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
+    monkeypatch.setenv("MOF_SOLVE_VERBOSE", "1")
+    monkeypatch.setenv("MOF_HOSTIO_VERBOSE", "1")
+    monkeypatch.setenv("MOF_STAGE_MB", "8")
+    monkeypatch.setenv("MOF_FUSED_NQ", "2")
+    velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
+    assert len(m.calls) == 1

@@ -33,7 +33,7 @@ def _case():
     return p, t, n, a, synth.travelling_wave(p, 6)
 
 
-def _rank_worker(rank, world, port, part, opts, out, env=None):
+def _rank_worker(rank, world, port, part, opts, out, env=None, oom_rank=-1):
     import sys
     os.environ.update(env or {})
     here = os.path.dirname(os.path.abspath(__file__))
@@ -46,6 +46,9 @@ def _rank_worker(rank, world, port, part, opts, out, env=None):
         from mofhip import DecomposedMesh
         p, t, n, a, I = _case()
         d = DecomposedMesh(p, n, t, a, world, part=part, group=dist.group.WORLD, transport="host")
+        if oom_rank >= 0:
+            from mofhip import _lib as L
+            L.check(L.lib().mof_dd_test_fail_recovery_alloc(d._h, oom_rank))
         info = d.info()
         V, st = d.solve_range(I, np.arange(len(I), dtype=np.float64), 0, len(I) - 1, 0.01, **opts)
         d.close()
@@ -89,7 +92,7 @@ def test_host_transport_ranks_match_in_process(P, opts):
 @pytest.mark.parametrize("oom_rank", [-1, 1])
 def test_recovery_allocation_failure_agreed_by_all_ranks(oom_rank):
     """The fp64 recovery pass allocates its workspace per rank; a failure on
-    one rank (injected: MOF_DD_TEST_OOM_RANK) is agreed by an all-gather of a
+    one rank (injected: mof_dd_test_fail_recovery_alloc) is agreed by an all-gather of a
     status word before the pass's collectives, so every rank skips the pass
     and returns its systems NaN-filled instead of hanging in the halo
     exchange. Without the failure the same pass recovers
@@ -104,8 +107,7 @@ def test_recovery_allocation_failure_agreed_by_all_ranks(oom_rank):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    env = {"MOF_DD_TEST_OOM_RANK": str(oom_rank)}
-    procs = [ctx.Process(target=_rank_worker, args=(r, P, port, part, opts, q, env)) for r in range(P)]
+    procs = [ctx.Process(target=_rank_worker, args=(r, P, port, part, opts, q, None, oom_rank)) for r in range(P)]
     for pr in procs:
         pr.start()
     res = sorted([q.get(timeout=240) for _ in range(P)], key=lambda x: x[0])

@@ -75,7 +75,7 @@ def main():
             rel = np.linalg.norm(r) / nf
             need = 0.3 * rtol / rel
             if est is not None and os.environ.get("ERRTOL", "1") == "1":
-                need = min(need, 0.3 * tau * np.abs(x).max() / (2 * est))
+                need = min(need, float(os.environ.get("NEEDF", "0.3")) * tau * np.abs(x).max() / (2 * est))
             t = inner if o == 0 else max(inner, min(0.5, need))
             d, its = pcg32(A32, r, M, t)
             tot += its
