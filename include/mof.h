@@ -198,6 +198,14 @@ int mof_mesh_create(const double *xyz, const double *nrm, const int32_t *tri,
  * cloned concurrently from different host threads. */
 int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out);
 int mof_mesh_destroy(mof_mesh *mesh);
+/* Start the per-mesh setup that solves with `opts` need -- the multigrid
+ * hierarchy of MOF_PRECOND_AMG + MOF_PREC_MIXED: host build and upload -- on
+ * a host thread of the handle, and return at once (a no-op for other
+ * options). The solves, mof_assemble, mof_mesh_clone and mof_mesh_destroy
+ * wait for it; an error it met is returned by the next of them. The drop-in
+ * starts it in compute_geometrical_quantities, a per-mesh call like the
+ * reference's a2 build (compute_optical_flow.py:27-97). */
+int mof_mesh_prepare(mof_mesh *mesh, const mof_opts *opts);
 int mof_mesh_get_info(const mof_mesh *mesh, mof_mesh_info *info);
 
 /* Host copies of the geometric quantities compute_geometrical_quantities

@@ -633,7 +633,7 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
 
 extern "C" {
 
-const char *mof_version(void) { return "mofhip 0.4 (gfx950, abi 3)"; }
+const char *mof_version(void) { return "mofhip 0.5 (gfx950, abi 4)"; }
 
 int mof_abi_version(void) { return MOF_ABI_VERSION; }
 
@@ -674,6 +674,7 @@ int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out) {
         MOF_REQUIRE(out, "out is NULL");
         *out = nullptr;
         MOF_REQUIRE(src && src->shared, "source mesh is NULL or not a mof_mesh_create handle");
+        mof::mesh_join_prep(const_cast<mof_mesh *>(src));
         int ndev = 0;
         MOF_HIP(hipGetDeviceCount(&ndev));
         MOF_REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
@@ -706,6 +707,7 @@ int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out) {
 int mof_mesh_destroy(mof_mesh *m) {
     if (!m) return MOF_OK;
     return guarded([&] {
+        if (m->prep.valid()) m->prep.wait();  // its error, if any, dies with the handle
         {
             DeviceGuard dg(m->device);
             if (m->stream) (void)hipStreamSynchronize(m->stream);
@@ -722,6 +724,32 @@ int mof_mesh_destroy(mof_mesh *m) {
             m->stream = nullptr;
             delete m;  // DevArray destructors free on the current (guarded) device
         }
+    });
+}
+
+// The multigrid hierarchy (host build and upload) of the options' solves on a
+// host thread of the handle: a per-mesh setup, started by the drop-in's
+// compute_geometrical_quantities (the reference builds a2 there,
+// compute_optical_flow.py:27-97) so that the first compute_velocity_field
+// call finds it built -- round 4: 5-8 ms of that call's 12-16 ms on the
+// reference's 3,249-vertex surfaces. Nothing else on the handle is touched
+// by the thread but its multigrid state and stream (uploads); the calls that
+// use them join it first.
+int mof_mesh_prepare(mof_mesh *m, const mof_opts *opts) {
+    return guarded([&] {
+        MOF_REQUIRE(m, "mesh is NULL");
+        mof::mesh_join_prep(m);
+        mof_opts o{};
+        if (opts) {
+            MOF_REQUIRE(opts->struct_size == 0 || opts->struct_size >= sizeof(mof_opts),
+                        "mof_opts.struct_size too small");
+            o = *opts;
+        }
+        if (!(o.flags & MOF_PRECOND_AMG) || o.precision != MOF_PREC_MIXED || m->n_own != m->N) return;
+        m->prep = std::async(std::launch::async, [m] {
+            DeviceGuard dg(m->device);
+            (void)mof::amg_build(m);
+        });
     });
 }
 
@@ -798,6 +826,7 @@ int mof_assemble(mof_mesh *m, const double *I0, const double *I1, double dt, dou
                  double *f) {
     return guarded([&] {
         MOF_REQUIRE(m && I0 && I1, "NULL argument");
+        mof::mesh_join_prep(m);
         DeviceGuard dg(m->device);
         hipStream_t s = m->stream;
         mof::ensure_workspace(m, 1, MOF_PREC_MIXED);
@@ -827,6 +856,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
     int rc = guarded([&] {
         MOF_REQUIRE(m && I && t_k && V_out, "NULL argument");
         MOF_REQUIRE(T >= 1 && k0 >= 0 && k0 <= k1 && k1 <= T - 1, "need 0 <= k0 <= k1 <= T-1");
+        mof::mesh_join_prep(m);
         mof_opts o{};
         if (opts) {
             MOF_REQUIRE(opts->struct_size == 0 || opts->struct_size >= sizeof(mof_opts),
@@ -1127,6 +1157,7 @@ int mof_bench_spmv(mof_mesh *m, uint32_t precision, int32_t batch, int32_t reps,
     return guarded([&] {
         MOF_REQUIRE(m && ms_per_launch && bytes_per_launch, "NULL argument");
         MOF_REQUIRE(reps > 0, "reps must be positive");
+        mof::mesh_join_prep(m);
         DeviceGuard dg(m->device);
         *ms_per_launch = mof::bench_spmv(m, precision, batch, reps, m->stream, bytes_per_launch);
     });

@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <functional>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -210,6 +211,10 @@ struct RedArgs {
 // The opaque handle of the C ABI.
 struct mof_mesh {
     int32_t N = 0, M = 0, device = 0;
+    // mof_mesh_prepare's per-mesh solver setup running on a host thread;
+    // every call that may use what it builds waits for it first
+    // (mof::mesh_join_prep)
+    std::future<void> prep;
     // rows [n_own, N) are a decomposed part's ghosts (mof_dd.h): the
     // multigrid preconditioner decouples them (identity rows); N otherwise
     int32_t n_own = 0;
@@ -344,6 +349,8 @@ struct SolveParams {
     // of the hierarchy's (the recovery's damped multigrid pass)
     float amg_omega = 0.f;
 };
+// Wait for a pending mof_mesh_prepare on the handle (rethrows its error).
+void mesh_join_prep(mof_mesh *m);
 // The largest batch whose launch grids all stay within 2^32 - 1 work-items
 // (xcd_grid refuses a larger one): the block-level assembly pass over the
 // SELL slots of every system is the widest grid of a solve.

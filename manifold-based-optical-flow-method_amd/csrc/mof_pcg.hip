@@ -1411,6 +1411,10 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
 
 int32_t xcd_batch_cap_host(int64_t nblk, int32_t grp) { return xcd_batch_cap(nblk, grp); }
 
+void mesh_join_prep(mof_mesh *m) {
+    if (m && m->prep.valid()) m->prep.get();
+}
+
 int32_t grid_batch_cap(const mof_mesh *m) {
     const int64_t per = (m->pat.sell_nb() + kWG - 1) / kWG;  // k_assemble_* / k_tri blocks per system
     return std::min(xcd_batch_cap(per, kGrpAsm), xcd_batch_cap(m->ws.nblk > 0 ? m->ws.nblk : per, kGrpSpmv));

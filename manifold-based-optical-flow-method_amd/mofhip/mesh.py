@@ -111,6 +111,14 @@ class DeviceMesh:
             raise errors[0]
         return dict(self.build_seconds)
 
+    def prepare_solver(self, device: int | None = None, **opts):
+        """Start the per-mesh setup the solves with ``opts`` need (the
+        multigrid hierarchy, mof_mesh_prepare) on a host thread of the
+        handle; returns at once, the next solve waits for it."""
+        o = self.make_opts(**{k: v for k, v in opts.items() if k != "batch"})
+        with self.lock(device):
+            L.check(L.lib().mof_mesh_prepare(self.handle(device), ctypes.byref(o)))
+
     def lock(self, device: int | None = None) -> threading.Lock:
         device = self.device if device is None else int(device)
         self.handle(device)

@@ -111,6 +111,9 @@ def compute_geometrical_quantities(coordinates, normals, triangles, areas):
     reference's."""
     start = time.time()
     mesh = DeviceMesh(coordinates, normals, triangles, areas, device=0)
+    # the per-mesh solver setup (the multigrid hierarchy of a2) starts here,
+    # on a host thread of the handle, as a2 is built here in the reference
+    mesh.prepare_solver(**_solver_options(mesh))
     e, grad_w, iw = mesh.geometry()
     return mesh, grad_w, e, iw, time.time() - start
 
