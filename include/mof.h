@@ -206,6 +206,8 @@ int mof_mesh_destroy(mof_mesh *mesh);
  * starts it in compute_geometrical_quantities, a per-mesh call like the
  * reference's a2 build (compute_optical_flow.py:27-97). */
 int mof_mesh_prepare(mof_mesh *mesh, const mof_opts *opts);
+/* Wait for the handle's pending mof_mesh_prepare; its status. */
+int mof_mesh_sync(mof_mesh *mesh);
 int mof_mesh_get_info(const mof_mesh *mesh, mof_mesh_info *info);
 
 /* Host copies of the geometric quantities compute_geometrical_quantities

@@ -753,6 +753,13 @@ int mof_mesh_prepare(mof_mesh *m, const mof_opts *opts) {
     });
 }
 
+int mof_mesh_sync(mof_mesh *m) {
+    return guarded([&] {
+        MOF_REQUIRE(m, "mesh is NULL");
+        mof::mesh_join_prep(m);
+    });
+}
+
 int mof_mesh_get_info(const mof_mesh *m, mof_mesh_info *info) {
     return guarded([&] {
         MOF_REQUIRE(m && info, "NULL argument");

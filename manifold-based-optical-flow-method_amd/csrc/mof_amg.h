@@ -108,6 +108,9 @@ struct AmgDevice {
     float omega = 0.85f, omega1 = 1.05f;
     int32_t xm = 2;  // level 0's corrected iterate: 1 in the x0 format in place, 2 fp32 in lv[0].y
     bool regular = false;  // tentative prolongator on a regular mesh: the bf16 iterates and omega1 1.1
+    // level 1 visits the coarser levels twice per cycle (S C S C S at level
+    // 1, a palindrome of symmetric steps: the preconditioner stays SPD)
+    bool wcycle = false;
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)

@@ -1459,6 +1459,8 @@ bool amg_build(mof_mesh *m) {
     // diverges there with the tentative P)
     if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = G.regular ? 1.1f : 1.05f;
     if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
+    G.wcycle = false;
+    if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
@@ -1700,8 +1702,32 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     // levels S.. run fused in k_subcycle
     int32_t S = 1;
     while (S < L - 1 && G.lv[S].n > kSubNodes) ++S;
-    // down: residual of the pre-smoothed x, restriction (+ next pre-smooth)
-    for (int32_t l = 0; l < S; ++l) {
+    // the cycle below level 0 from level 1's restricted b and pre-smoothed
+    // x: down (residual, restriction + next pre-smooth), the fused tiny
+    // levels, up (prolongation, post-smoothing into y)
+    auto coarse = [&](const Lvl (&u)[kMaxLevels]) {
+        for (int32_t l = 1; l < S; ++l) {
+            const int32_t smooth = l + 1 < L - 1;
+            k_res3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], sysi);
+            k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
+                u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
+        }
+        SubArgs sa;
+        sa.first = S;
+        sa.last = L - 1;
+        for (int32_t l = 0; l < L; ++l) sa.lv[l] = u[l];
+        sa.cinv = G.cinv.p;
+        sa.omega = om1;
+        sa.sysi = sysi;
+        k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
+        for (int32_t l = S - 1; l >= 1; --l) {
+            k_prolong<3><<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
+            k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+        }
+    };
+    // down at level 0: residual of the pre-smoothed x, restriction (+ level
+    // 1's pre-smooth)
+    for (int32_t l = 0; l < 1; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
             k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (B + kRes0NS - 1) / kRes0NS,
@@ -1715,22 +1741,28 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                 k_restrict<2, kRestrS><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kRestrS - 1) / kRestrS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             }
-        } else {
-            k_res3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], sysi);
-            k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
-                v[l], v[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
         }
     }
-    SubArgs sa;
-    sa.first = S;
-    sa.last = L - 1;
-    for (int32_t l = 0; l < L; ++l) sa.lv[l] = v[l];
-    sa.cinv = G.cinv.p;
-    sa.omega = om1;
-    sa.sysi = sysi;
-    k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
-    // up: coarse correction, post-smooth
-    for (int32_t l = S - 1; l >= 0; --l) {
+    if (S == 1) {  // level 1 is already one of the fused tiny levels
+        SubArgs sa;
+        sa.first = 1;
+        sa.last = L - 1;
+        for (int32_t l = 0; l < L; ++l) sa.lv[l] = v[l];
+        sa.cinv = G.cinv.p;
+        sa.omega = om1;
+        sa.sysi = sysi;
+        k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
+    } else {
+        coarse(v);
+        if (G.wcycle) {
+            // the second visit from level 1's post-smoothed y: x and y swap
+            // roles, and level 0's prolongation reads the new result
+            std::swap(v[1].x, v[1].y);
+            coarse(v);
+        }
+    }
+    // up at level 0: coarse correction, post-smooth
+    for (int32_t l = 0; l >= 0; --l) {
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
             const int32_t nb0p = (v[0].n + kWG * kProlR - 1) / (kWG * kProlR);
@@ -1754,9 +1786,6 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                 else
                     launch_post0<1, false>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
             }
-        } else {
-            k_prolong<3><<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], v[l + 1], sysi);
-            k_post3<<<grid2(v[l].n, B), kWG, 0, s>>>(v[l], om1, sysi);
         }
     }
     MOF_HIP(hipGetLastError());

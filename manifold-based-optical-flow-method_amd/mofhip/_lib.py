@@ -54,7 +54,7 @@ EXPORTS = (
     "mof_point_normals", "mof_cell_areas", "mof_singularities", "mof_amg_probe",
     "mof_partition_rcb", "mof_dd_plan_info", "mof_dd_create", "mof_dd_unique_id",
     "mof_dd_create_rank", "mof_dd_destroy", "mof_dd_get_info", "mof_dd_solve_range",
-    "mof_dd_test_fail_recovery_alloc", "mof_mesh_prepare",
+    "mof_dd_test_fail_recovery_alloc", "mof_mesh_prepare", "mof_mesh_sync",
     "mof_singularities_compact", "mof_xcd_map_check", "mof_xcd_batch_cap", "mof_dd_create_rank_host",
 )
 
@@ -198,6 +198,7 @@ def lib():
             "mof_dd_destroy": ([P], ctypes.c_int),
             "mof_dd_get_info": ([P, P], ctypes.c_int),
             "mof_mesh_prepare": ([P, P], ctypes.c_int),
+            "mof_mesh_sync": ([P], ctypes.c_int),
             "mof_dd_test_fail_recovery_alloc": ([P, i32], ctypes.c_int),
             "mof_dd_solve_range": ([P, P, P, P, i32, i32, i32, f64, P, P, P], ctypes.c_int),
         }

@@ -119,6 +119,11 @@ class DeviceMesh:
         with self.lock(device):
             L.check(L.lib().mof_mesh_prepare(self.handle(device), ctypes.byref(o)))
 
+    def sync_solver(self, device: int | None = None):
+        """Wait for the setup prepare_solver started (raises its error)."""
+        with self.lock(device):
+            L.check(L.lib().mof_mesh_sync(self.handle(device)))
+
     def lock(self, device: int | None = None) -> threading.Lock:
         device = self.device if device is None else int(device)
         self.handle(device)

@@ -111,10 +111,12 @@ def compute_geometrical_quantities(coordinates, normals, triangles, areas):
     reference's."""
     start = time.time()
     mesh = DeviceMesh(coordinates, normals, triangles, areas, device=0)
-    # the per-mesh solver setup (the multigrid hierarchy of a2) starts here,
-    # on a host thread of the handle, as a2 is built here in the reference
+    # the per-mesh solver setup (the multigrid hierarchy of a2) belongs to
+    # this per-mesh call, as a2 itself does in the reference: built on a host
+    # thread of the handle beside the geometry export, finished before return
     mesh.prepare_solver(**_solver_options(mesh))
     e, grad_w, iw = mesh.geometry()
+    mesh.sync_solver()
     return mesh, grad_w, e, iw, time.time() - start
 
 
