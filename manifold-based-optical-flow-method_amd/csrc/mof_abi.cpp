@@ -1113,7 +1113,7 @@ int mof_singularities_compact(int32_t device, const void *coords, const int32_t 
 }
 
 int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
-                  int32_t *level_nodes, double *qtq_err) {
+                  int32_t *level_nodes, double *qtq_err, double *max_curl) {
     return guarded([&] {
         MOF_REQUIRE(tri && e && n_levels && level_nodes && N > 0 && M > 0, "bad arguments");
         for (int64_t q = 0; q < 3 * (int64_t)M; ++q)
@@ -1123,6 +1123,7 @@ int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int
         mof::AmgHierarchy H;
         mof::build_amg(pat, e, mof::AmgParams{}, H);
         *n_levels = (int32_t)std::min<size_t>(16, H.levels.size());
+        if (max_curl) *max_curl = H.max_curl;
         for (int32_t l = 0; l < *n_levels; ++l) level_nodes[l] = H.levels[l].n;
         if (qtq_err) {
             double err = 0.0;

@@ -69,6 +69,12 @@ struct AmgLevel {
 struct AmgHierarchy {
     std::vector<AmgLevel> levels;
     int32_t coarse_dofs = 0;
+    // per transition l -> l+1: the median over the aggregates of
+    // sigma_3 / sigma_1 of the stacked near-null block (how much the tangent
+    // planes turn inside an aggregate; 0 on a flat one), and the largest of
+    // these over transitions with >= 64 aggregates (amg_build's W-cycle choice)
+    std::vector<double> curl;
+    double max_curl = 0.0;
 };
 
 void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,

@@ -1459,7 +1459,16 @@ bool amg_build(mof_mesh *m) {
     // diverges there with the tentative P)
     if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = G.regular ? 1.1f : 1.05f;
     if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
-    G.wcycle = false;
+    // level 1 visits the levels below twice (W) where the coarse levels are
+    // weakest: on open surfaces, and on surfaces whose aggregates turn
+    // strongly at some coarse level (median sigma_3 / sigma_1 of an
+    // aggregate's near-null block >= kWCurl: folds at the coarse levels'
+    // scale). Round 5, same box (profiles/r05_ab/wcycle/): F3 (folded,
+    // curl 0.46 at level 2) 1727 -> 1934 timesteps/s (40.5 -> 30.1 PCG its),
+    // S1 (open) 858 -> 905 (59.5 -> 47.2); the spheres lose (C3, curl <= 0.24:
+    // 3652 -> 3370, 17.0 -> 15.9 its; R3 748 -> 657). MOF_AMG_W=0/1 forces.
+    constexpr double kWCurl = 0.35;
+    G.wcycle = m->n_own == m->N && (open_surface || H.max_curl >= kWCurl);
     if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
@@ -1542,9 +1551,10 @@ bool amg_build(mof_mesh *m) {
     G.cap = 0;
     if (std::getenv("MOF_AMG_VERBOSE")) {
         for (size_t l = 0; l < H.levels.size(); ++l)
-            std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld%s\n", l, H.levels[l].n,
-                         H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb(),
-                         H.levels[l].smoothed ? " (smoothed P)" : "");
+            std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld%s curl %.3f%s\n", l,
+                         H.levels[l].n, H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb(),
+                         H.levels[l].smoothed ? " (smoothed P)" : "", l < H.curl.size() ? H.curl[l] : 0.0,
+                         l == 0 && G.wcycle ? " (W-cycle at level 1)" : "");
     }
     MOF_HIP(hipStreamSynchronize(s));
     return true;

@@ -218,9 +218,47 @@ bool amg_auto_smooth(const Pattern &fine) {
     return std::sqrt(var) > 0.5;
 }
 
+// sigma_3 / sigma_1 of a 3-column block from its QR factor R (3x3, upper
+// triangular, row-major): the eigenvalues of R^T R by cyclic Jacobi
+static double sv_ratio(const double R[9]) {
+    double a[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 3; ++k) s += R[3 * k + i] * R[3 * k + j];
+            a[i][j] = s;
+        }
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        double off = std::fabs(a[0][1]) + std::fabs(a[0][2]) + std::fabs(a[1][2]);
+        if (off <= 1e-300) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                if (std::fabs(a[p][q]) <= 1e-300) continue;
+                const double th = 0.5 * (a[q][q] - a[p][p]) / a[p][q];
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
+                for (int k = 0; k < 3; ++k) {  // columns p, q
+                    const double kp = a[k][p], kq = a[k][q];
+                    a[k][p] = c * kp - sn * kq;
+                    a[k][q] = sn * kp + c * kq;
+                }
+                for (int k = 0; k < 3; ++k) {  // rows p, q
+                    const double pk = a[p][k], qk = a[q][k];
+                    a[p][k] = c * pk - sn * qk;
+                    a[q][k] = sn * pk + c * qk;
+                }
+            }
+    }
+    const double l0 = std::max(0.0, a[0][0]), l1 = std::max(0.0, a[1][1]), l2 = std::max(0.0, a[2][2]);
+    const double mx = std::max({l0, l1, l2}), mn = std::min({l0, l1, l2});
+    return mx > 0.0 ? std::sqrt(mn / mx) : 0.0;
+}
+
 void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,
                AmgHierarchy &H) {
     H.levels.clear();
+    H.curl.clear();
+    H.max_curl = 0.0;
     // level 0: the fine pattern (SELL already built by build_pattern)
     {
         AmgLevel L0;
@@ -260,7 +298,7 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         F.Q.assign((size_t)F.n * bs * 3, 0.f);
         std::vector<double> Bc(9 * (size_t)nc, 0.0);
         std::vector<uint8_t> dead(3 * (size_t)nc, 0);
-        std::vector<double> Bm, Qm;
+        std::vector<double> Bm, Qm, ratio(nc);
         for (int32_t I = 0; I < nc; ++I) {
             const int32_t m = F.mptr[I + 1] - F.mptr[I];
             Bm.assign(3 * (size_t)m * bs, 0.0);
@@ -280,7 +318,11 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
             }
             for (int k = 0; k < 9; ++k) Bc[9 * (size_t)I + k] = R[k];
             for (int c = 0; c < 3; ++c) dead[3 * (size_t)I + c] = dd[c];
+            ratio[I] = sv_ratio(R);
         }
+        std::nth_element(ratio.begin(), ratio.begin() + nc / 2, ratio.end());
+        H.curl.push_back(ratio[nc / 2]);
+        if (nc >= 64) H.max_curl = std::max(H.max_curl, ratio[nc / 2]);
         // member-order copy (restriction reads members contiguously)
         F.Qm.assign(F.Q.size(), 0.f);
         for (int32_t q = 0; q < F.n; ++q)

@@ -182,7 +182,7 @@ def lib():
             "mof_cell_areas": ([P, P, i64, i64, P], ctypes.c_int),
             "mof_singularities": ([i32, P, P, i32, i32, P, i32, f64, u32, P, P, P, P, P],
                                   ctypes.c_int),
-            "mof_amg_probe": ([P, P, i32, i32, P, P, P], ctypes.c_int),
+            "mof_amg_probe": ([P, P, i32, i32, P, P, P, P], ctypes.c_int),
             "mof_xcd_map_check": ([i32, i32, i32], ctypes.c_int),
             "mof_xcd_batch_cap": ([i64, i32, P], ctypes.c_int),
             "mof_singularities_compact": ([i32, P, P, i32, i32, P, i32, f64, u32, P, i64, P, P, P, P, P,

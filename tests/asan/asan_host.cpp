@@ -206,11 +206,11 @@ static void test_mesh_host(void) {
     }
     int32_t nl = 0, ln[16];
     double qerr = 1.0;
-    CHECK(mof_amg_probe(tri.data(), e.data(), N, M, &nl, ln, &qerr) == MOF_OK && nl >= 2 && ln[0] == N);
+    CHECK(mof_amg_probe(tri.data(), e.data(), N, M, &nl, ln, &qerr, nullptr) == MOF_OK && nl >= 2 && ln[0] == N);
     CHECK(qerr < 1e-5);
     std::vector<int32_t> badtri = tri;
     badtri[7] = N + 3;
-    CHECK(mof_amg_probe(badtri.data(), e.data(), N, M, &nl, ln, &qerr) != MOF_OK);
+    CHECK(mof_amg_probe(badtri.data(), e.data(), N, M, &nl, ln, &qerr, nullptr) != MOF_OK);
     for (int32_t P : {1, 2, 3, 8}) {
         std::vector<int32_t> part(N, -1);
         CHECK(mof_partition_rcb(xyz.data(), N, P, part.data()) == MOF_OK);

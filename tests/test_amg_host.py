@@ -21,8 +21,10 @@ def probe(p, t):
     nl = ctypes.c_int32(0)
     sizes = np.zeros(16, dtype=np.int32)
     err = ctypes.c_double(0.0)
+    curl = ctypes.c_double(0.0)
     L.check(L.lib().mof_amg_probe(L.ptr(T), L.ptr(E), len(p), len(t), ctypes.byref(nl), L.ptr(sizes),
-                                  ctypes.byref(err)))
+                                  ctypes.byref(err), ctypes.byref(curl)))
+    probe.curl = curl.value
     return list(sizes[:nl.value]), err.value
 
 
@@ -51,13 +53,32 @@ def test_hierarchy_deterministic_and_tiny():
     assert sizes == [len(p1)]
 
 
+def test_wcycle_criterion_separates_folded_from_spheres():
+    """The multigrid's W-cycle choice (amg_build, kWCurl = 0.35): the median
+    turn of the tangent planes inside the coarse aggregates (sigma_3 /
+    sigma_1 of their near-null blocks) is large on a folded surface (the
+    F3 class, synth.folded_sphere) and stays small on jittered and random
+    spheres, at any resolution (round 5: F3 0.46, C3 0.24, R3 0.09 at 163,842
+    vertices)."""
+    p, t = synth.folded_sphere(64)
+    probe(p, t)
+    folded = probe.curl
+    p, t = synth.icosphere(64, 10.0, jitter=0.005)
+    probe(p, t)
+    sphere = probe.curl
+    p, t = synth.random_sphere(40962, 10.0, seed=0)
+    probe(p, t)
+    hull = probe.curl
+    assert folded >= 0.35 > max(sphere, hull), (folded, sphere, hull)
+
+
 def test_probe_rejects_bad_input():
     p, t = synth.icosphere(2, 10.0)
     bad = np.ascontiguousarray(t, dtype=np.int32)
     bad[0, 0] = len(p)
     E = np.zeros((len(p), 2, 3))
     nl, sizes = ctypes.c_int32(0), np.zeros(16, dtype=np.int32)
-    rc = L.lib().mof_amg_probe(L.ptr(bad), L.ptr(E), len(p), len(t), ctypes.byref(nl), L.ptr(sizes), None)
+    rc = L.lib().mof_amg_probe(L.ptr(bad), L.ptr(E), len(p), len(t), ctypes.byref(nl), L.ptr(sizes), None, None)
     with pytest.raises(L.MofError):
         L.check(rc)
 
