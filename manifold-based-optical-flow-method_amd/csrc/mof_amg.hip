@@ -1612,6 +1612,7 @@ AmgFine amg_fine(mof_mesh *m) {
     f.omega = G.omega;
     f.smoothed = G.lv[0].smoothed;
     f.regular = G.regular;
+    f.wcycle = G.wcycle;
     return f;
 }
 
