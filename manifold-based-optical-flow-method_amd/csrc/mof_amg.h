@@ -29,6 +29,15 @@ struct AmgParams {
     // terms and a level-1 operator with 2x the blocks per row.
     int32_t smooth = -1;
     float smooth_omega = 0.66f;
+    // smoothed aggregation at level 1 (the transition 1 -> 2), with the
+    // Galerkin image P0^T a2 P0 of the mesh's a2 (per mesh, fp64 on the
+    // host): P1 = (I - w D1^-1 a2_1) P1_tent. 1 on, 0 off; applied when level
+    // 1 has more than kSubNodes nodes (the fused tiny levels keep the
+    // tentative transfers). CPU prototype (tools/amg_proto.py sa1a2=0.66
+    // sa1only=1, PCG its to 1e-4): the two-grid bound with an exact level-1
+    // solve is 8 its on F3 and 7 on C3, the V-cycle 18 / 8 -- the recursion
+    // below level 1 was F3's weakness; with P1 smoothed 12 / 7.
+    int32_t smooth1 = 1;
     const double *a2 = nullptr;  // [sell_nb][4] level-0 a2 in the fine SELL layout (smoothing)
     // the fine level's mirror table when its operators are read symmetrically
     // (sell_mirror): level-0 gather entries of lower blocks then point at the
@@ -43,6 +52,10 @@ struct AmgParams {
 // One level of the hierarchy. Level 0 is the fine mesh (bs = 2); coarser
 // levels have 3 dofs per node. The transition fields (agg ... gent) describe
 // the restriction to the next level and are empty on the coarsest level.
+// levels of at most this many nodes run fused in one launch per cycle
+// (k_subcycle) with the tentative transfers
+constexpr int32_t kSubNodes = 512;
+
 struct AmgLevel {
     int32_t n = 0, bs = 0;
     std::vector<int32_t> vptr, vcol;               // block adjacency (self included, sorted)
@@ -63,6 +76,9 @@ struct AmgLevel {
     // tentative prolongator is the special case pptr = 0..n, pcol = agg.
     bool smoothed = false;
     std::vector<int32_t> pptr, pcol, rptr, rent;
+    // level 1 (host build only): the Galerkin image of the mesh's a2, 9
+    // doubles per adjacency block (vptr / vcol order), for its smoothing
+    std::vector<double> a2img;
     int64_t sell_nb() const { return sell_off.empty() ? 0 : sell_off.back(); }
 };
 

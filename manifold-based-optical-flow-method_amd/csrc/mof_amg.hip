@@ -1079,6 +1079,57 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     }
 }
 
+// Level 1 with a smoothed prolongator (AmgParams::smooth1): the coarse
+// node's restriction list {fine node, P block} summed in list order, one
+// (coarse node, system) per thread -- level 1 is small (C3: 21,701 nodes;
+// the lists average 20 entries); with smooth also x_C = w D_C^-1 b_C.
+__global__ __launch_bounds__(kWG) void k_restrict3_sa(Lvl F, Lvl C, int32_t smooth, float omega,
+                                                      const int32_t *__restrict__ sysi) {
+#pragma clang fp contract(off)
+    const int32_t I = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    if (I >= C.n || retired(sysi, b)) return;
+    const int64_t fo = (int64_t)b * F.n * 4;
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int32_t e = F.rptr[I]; e < F.rptr[I + 1]; ++e) {
+        const int32_t i = F.rent[2 * (int64_t)e];
+        const float *p = F.Q + (int64_t)F.rent[2 * (int64_t)e + 1] * 9;
+        float r[3];
+        ldv<3>(F.r + fo, i, r);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] += p[c] * r[0] + p[3 + c] * r[1] + p[6 + c] * r[2];
+    }
+    const int64_t vo = (int64_t)b * C.n * 4;
+    stv<3>(C.b + vo, I, acc);
+    if (smooth) {
+        float d[3][3], x[3];
+        ld_dh(C, b, I, d);
+        matvec<3>(d, acc, x);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] *= omega;
+        stv<3>(C.x + vo, I, x);
+    }
+}
+
+// x_i += sum over the fine node's P blocks of P_ik y_C[pcol k] (level 1,
+// smoothed prolongator), in place
+__global__ __launch_bounds__(kWG) void k_prolong3_sa(Lvl F, Lvl C, const int32_t *__restrict__ sysi) {
+#pragma clang fp contract(off)
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    if (i >= F.n || retired(sysi, b)) return;
+    float *xb = F.x + (int64_t)b * F.n * 4;
+    const float *yb = C.y + (int64_t)b * C.n * 4;
+    float xi[3];
+    ldv<3>(xb, i, xi);
+    for (int32_t k = F.pptr[i]; k < F.pptr[i + 1]; ++k) {
+        const float *p = F.Q + (int64_t)k * 9;
+        float y[3];
+        ldv<3>(yb, F.pcol[k], y);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) xi[r] += p[3 * r] * y[0] + p[3 * r + 1] * y[1] + p[3 * r + 2] * y[2];
+    }
+    stv<3>(xb, i, xi);
+}
+
 template <int BSF>
 __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__restrict__ sysi) {
     const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
@@ -1156,7 +1207,7 @@ __global__ __launch_bounds__(kWG) void k_post3(Lvl L, float omega, const int32_t
 // one workgroup per system walks the tiny levels with barriers in between,
 // replacing ~4 launches per level.
 constexpr int kSubWG = 256;
-constexpr int kSubNodes = 512;
+// kSubNodes: mof_amg.h
 constexpr int kMaxLevels = 12;
 
 struct SubArgs {
@@ -1387,6 +1438,7 @@ bool amg_build(mof_mesh *m) {
     if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
     if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
     if (const char *v = std::getenv("MOF_AMG_SMOOTH")) prm.smooth = std::atoi(v);  // 1 / 0 force, unset auto
+    if (const char *v = std::getenv("MOF_AMG_SMOOTH1")) prm.smooth1 = std::atoi(v);  // level 1: 1 / 0
     if (m->n_own < m->N) prm.nown = m->n_own;
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
@@ -1397,8 +1449,8 @@ bool amg_build(mof_mesh *m) {
     // (pattern, e, a2) are the same on every device, bit for bit
     MeshShared *sh = m->shared.get();
     char key[160];
-    std::snprintf(key, sizeof(key), "%a/%a/%d/%d/%a/%d", (double)prm.omega, (double)prm.omega1, prm.smooth,
-                  prm.nown, (double)prm.smooth_omega, (int)m->sym_reads);
+    std::snprintf(key, sizeof(key), "%a/%a/%d/%d/%a/%d/%d", (double)prm.omega, (double)prm.omega1, prm.smooth,
+                  prm.nown, (double)prm.smooth_omega, (int)m->sym_reads, prm.smooth1);
     std::unique_lock<std::mutex> build_lock;
     std::shared_ptr<const AmgHierarchy> Hp;
     if (sh) {
@@ -1413,7 +1465,7 @@ bool amg_build(mof_mesh *m) {
         MOF_HIP(hipStreamSynchronize(s));
         // the mesh's a2 (unscaled, fine SELL layout) for the smoothed prolongator
         std::vector<double> a2;
-        if (prm.nown < 0 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) {
+        if (prm.nown < 0 && ((prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) || prm.smooth1 > 0)) {
             a2.resize(4 * (size_t)m->pat.sell_nb());
             MOF_HIP(hipMemcpyAsync(a2.data(), m->a2.p, a2.size() * sizeof(double), hipMemcpyDeviceToHost, s));
             MOF_HIP(hipStreamSynchronize(s));
@@ -1531,7 +1583,7 @@ bool amg_build(mof_mesh *m) {
             const char *ge = std::getenv("MOF_GAL_ENT");
             const char *ge3 = std::getenv("MOF_GAL3_ENT");
             const bool ent_here = l == 0 || !(ge3 && *ge3 && std::atoi(ge3) == 0);
-            if (!L.smoothed && ent_here && !(ge && *ge && std::atoi(ge) == 0)) {
+            if ((!L.smoothed || l >= 1) && ent_here && !(ge && *ge && std::atoi(ge) == 0)) {
                 const std::vector<int32_t> &gq = L.gptr;
                 const int32_t npos = (int32_t)gq.size() - 1;
                 bool ok = true;
@@ -1720,8 +1772,11 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         for (int32_t l = 1; l < S; ++l) {
             const int32_t smooth = l + 1 < L - 1;
             k_res3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], sysi);
-            k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
-                u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
+            if (G.lv[l].smoothed)
+                k_restrict3_sa<<<grid2(u[l + 1].n, B), kWG, 0, s>>>(u[l], u[l + 1], smooth, om1, sysi);
+            else
+                k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
+                    u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
         }
         SubArgs sa;
         sa.first = S;
@@ -1732,7 +1787,10 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         sa.sysi = sysi;
         k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
         for (int32_t l = S - 1; l >= 1; --l) {
-            k_prolong<3><<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
+            if (G.lv[l].smoothed)
+                k_prolong3_sa<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
+            else
+                k_prolong<3><<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
             k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
         }
     };

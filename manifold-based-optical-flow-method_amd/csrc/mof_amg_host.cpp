@@ -202,6 +202,124 @@ void smooth_prolongator(const Pattern &fine, const AmgParams &prm, const std::ve
     }
 }
 
+// P = (I - w D^-1 a) Q at a coarse level (bs = 3; a: 9 doubles per adjacency
+// block of F, row-major): as smooth_prolongator, with a dof of F that has no
+// prolongator column (dead) given a unit diagonal in D.
+void smooth_prolongator3(const AmgLevel &F, const std::vector<double> &a, double w, const std::vector<int32_t> &agg,
+                         const std::vector<float> &Q, std::vector<int32_t> &pptr, std::vector<int32_t> &pcol,
+                         std::vector<float> &P) {
+    const int32_t n = F.n;
+    pptr.assign(n + 1, 0);
+    pcol.clear();
+    P.clear();
+    std::vector<int32_t> rk;
+    std::vector<double> rv;
+    for (int32_t i = 0; i < n; ++i) {
+        rk.clear();
+        rv.clear();
+        auto add = [&](int32_t K, const double (&t)[9]) {
+            size_t e = 0;
+            while (e < rk.size() && rk[e] != K) ++e;
+            if (e == rk.size()) {
+                rk.push_back(K);
+                rv.insert(rv.end(), 9, 0.0);
+            }
+            for (int c = 0; c < 9; ++c) rv[9 * e + c] += t[c];
+        };
+        double own[9];
+        for (int c = 0; c < 9; ++c) own[c] = Q[9 * (size_t)i + c];
+        add(agg[i], own);
+        int32_t qd = -1;
+        for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q)
+            if (F.vcol[q] == i) qd = q;
+        double d[9];
+        bool ok = qd >= 0;
+        if (ok) {
+            for (int k = 0; k < 9; ++k) d[k] = a[9 * (size_t)qd + k];
+            for (int c = 0; c < 3; ++c)
+                if (!F.dead.empty() && F.dead[3 * (size_t)i + c]) d[4 * c] += 1.0;
+        }
+        double di[9];
+        if (ok) {  // 3x3 inverse by cofactors
+            const double c00 = d[4] * d[8] - d[5] * d[7], c01 = d[5] * d[6] - d[3] * d[8], c02 = d[3] * d[7] - d[4] * d[6];
+            const double det = d[0] * c00 + d[1] * c01 + d[2] * c02;
+            ok = det != 0.0 && std::isfinite(det);
+            if (ok) {
+                const double id = 1.0 / det;
+                di[0] = c00 * id;
+                di[1] = (d[2] * d[7] - d[1] * d[8]) * id;
+                di[2] = (d[1] * d[5] - d[2] * d[4]) * id;
+                di[3] = c01 * id;
+                di[4] = (d[0] * d[8] - d[2] * d[6]) * id;
+                di[5] = (d[2] * d[3] - d[0] * d[5]) * id;
+                di[6] = c02 * id;
+                di[7] = (d[1] * d[6] - d[0] * d[7]) * id;
+                di[8] = (d[0] * d[4] - d[1] * d[3]) * id;
+            }
+        }
+        if (ok) {
+            for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) {
+                const int32_t j = F.vcol[q];
+                const double *aq = &a[9 * (size_t)q];
+                double m[9];  // D^-1 a_ij
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        m[3 * r + c] = di[3 * r] * aq[c] + di[3 * r + 1] * aq[3 + c] + di[3 * r + 2] * aq[6 + c];
+                double t[9];
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        t[3 * r + c] = -w * (m[3 * r] * Q[9 * (size_t)j + c] + m[3 * r + 1] * Q[9 * (size_t)j + 3 + c] +
+                                             m[3 * r + 2] * Q[9 * (size_t)j + 6 + c]);
+                add(agg[j], t);
+            }
+        }
+        std::vector<size_t> ord(rk.size());
+        for (size_t e = 0; e < ord.size(); ++e) ord[e] = e;
+        std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return rk[x] < rk[y]; });
+        for (size_t e : ord) {
+            pcol.push_back(rk[e]);
+            for (int c = 0; c < 9; ++c) P.push_back((float)rv[9 * e + c]);
+        }
+        pptr[i + 1] = (int32_t)pcol.size();
+    }
+}
+
+// The Galerkin image C = P^T a P of a fine operator given per adjacency block
+// (bs x bs doubles, fine vptr / vcol order) on the coarse pattern
+// (C.vptr / vcol), 9 doubles per coarse adjacency block, fp64.
+std::vector<double> galerkin_image(const AmgLevel &F, int bs, const std::vector<double> &a, const AmgLevel &C) {
+    std::vector<double> out(9 * C.vcol.size(), 0.0);
+    for (int32_t i = 0; i < F.n; ++i)
+        for (int32_t q = F.vptr[i]; q < F.vptr[i + 1]; ++q) {
+            const int32_t j = F.vcol[q];
+            const double *aq = &a[(size_t)bs * bs * q];
+            for (int32_t ka = F.pptr[i]; ka < F.pptr[i + 1]; ++ka) {
+                const int32_t I = F.pcol[ka];
+                const float *pi = &F.Q[(size_t)bs * 3 * ka];
+                for (int32_t kb = F.pptr[j]; kb < F.pptr[j + 1]; ++kb) {
+                    const float *pj = &F.Q[(size_t)bs * 3 * kb];
+                    const int32_t p = (int32_t)(std::lower_bound(C.vcol.begin() + C.vptr[I], C.vcol.begin() + C.vptr[I + 1],
+                                                                 F.pcol[kb]) -
+                                                C.vcol.begin());
+                    double T[4][3];  // a_ij P_j (bs x 3)
+                    for (int r = 0; r < bs; ++r)
+                        for (int c = 0; c < 3; ++c) {
+                            double s = 0.0;
+                            for (int k = 0; k < bs; ++k) s += aq[bs * r + k] * (double)pj[3 * k + c];
+                            T[r][c] = s;
+                        }
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) {
+                            double s = 0.0;
+                            for (int k = 0; k < bs; ++k) s += (double)pi[3 * k + r] * T[k][c];
+                            out[9 * (size_t)p + 3 * r + c] += s;
+                        }
+                }
+            }
+        }
+    return out;
+}
+
 }  // namespace
 
 bool amg_auto_smooth(const Pattern &fine) {
@@ -330,9 +448,13 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         // prolongator rows: the tentative Q (one block per node), or smoothed
         const bool smooth = H.levels.size() == 1 && prm.nown < 0 && prm.a2 &&
                             (prm.smooth > 0 || (prm.smooth < 0 && amg_auto_smooth(fine)));
-        if (smooth) {
+        const bool smooth1 = H.levels.size() == 2 && prm.smooth1 > 0 && !F.a2img.empty() && F.n > kSubNodes;
+        if (smooth || smooth1) {
             std::vector<float> P;
-            smooth_prolongator(fine, prm, agg, F.Q, F.pptr, F.pcol, P);
+            if (smooth)
+                smooth_prolongator(fine, prm, agg, F.Q, F.pptr, F.pcol, P);
+            else
+                smooth_prolongator3(F, F.a2img, prm.smooth_omega, agg, F.Q, F.pptr, F.pcol, P);
             F.Q.swap(P);  // P blocks, indexed by the gather lists and the prolongation
             F.smoothed = true;
             for (int32_t i = 0; i < F.n; ++i) F.apos[i] = i;  // restriction gathers by node
@@ -380,6 +502,14 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
             }
         }
         sell_layout(C);
+        // level 1's image of the mesh's a2 (its smoothing, smooth1)
+        if (H.levels.size() == 1 && prm.nown < 0 && prm.a2 && prm.smooth1 > 0 && C.n > kSubNodes) {
+            std::vector<double> ab(4 * fine.vcol.size(), 0.0);  // a2 per adjacency block
+            for (size_t pos = 0; pos < fine.sell_blk.size(); ++pos)
+                if (fine.sell_blk[pos] >= 0)
+                    for (int k = 0; k < 4; ++k) ab[4 * (size_t)fine.sell_blk[pos] + k] = prm.a2[4 * pos + k];
+            C.a2img = galerkin_image(F, 2, ab, C);
+        }
         // Galerkin gather lists: coarse block -> terms P_iK^T A_ij P_jL, in fine
         // block order (then P block order)
         const int32_t cnb = (int32_t)C.vcol.size();

@@ -36,16 +36,16 @@ def test_roofline_reproduces_from_trace():
 
 
 def test_roofline_reproduces_from_trace_b1024():
-    """The default batch (1024, round 4's final build): the same reproduction
-    on its own trace and PMC passes (profiles/r04b_*)."""
-    out = json.loads(_run("profiles/roofline_check.py", "profiles/r04b_bench_c3_b1024_under_rocprof.json",
-                          "profiles/r04b_c3_mixed_amg_b1024_kernel_trace.csv", "C3/mixed/amg/B1024"))
+    """The default batch (1024, round 5's build): the line's SpMV roofline
+    reproduced from its own rocprof trace and PMC passes (profiles/r05_*)."""
+    out = json.loads(_run("profiles/roofline_check.py", "profiles/r05_bench_c3_b1024_under_rocprof.json",
+                          "profiles/r05_c3_mixed_amg_b1024_kernel_trace.csv", "C3/mixed/amg/B1024"))
     assert abs(out["rel_diff"]) < 0.01, out
     assert out["rocprof_frac"] >= 0.6
-    line = json.loads(open(os.path.join(P, "r04b_bench_c3_b1024_under_rocprof.json")).readline())
+    line = json.loads(open(os.path.join(P, "r05_bench_c3_b1024_under_rocprof.json")).readline())
     assert line["config"]["batch"] == 1024
     assert out["rocprof_launches"] == line["roofline"]["launches"] == 95
-    assert 3465.0 < out["rocprof_us_per_launch"] < 3485.0
+    assert 3575.0 < out["rocprof_us_per_launch"] < 3595.0
     rl = line["roofline"]
     own = rl["kernel_bytes_per_system"] * 1024 + rl["kernel_shared_bytes_per_launch"]
     assert abs(out["pmc_hbm_bytes_median_launch"] / own - 1.0) < 0.10
@@ -53,8 +53,8 @@ def test_roofline_reproduces_from_trace_b1024():
 
 def test_pmc_summary_reproduces_committed_entry_b1024(tmp_path):
     dst = tmp_path / "pmc.json"
-    _run("profiles/pmc_summary.py", "profiles/r04b_pmc_fetch_c3_mixed_amg_b1024.csv",
-         "profiles/r04b_pmc_write_c3_mixed_amg_b1024.csv", str(dst), "C3/mixed/amg/B1024", "4096")
+    _run("profiles/pmc_summary.py", "profiles/r05_pmc_fetch_c3_mixed_amg_b1024.csv",
+         "profiles/r05_pmc_write_c3_mixed_amg_b1024.csv", str(dst), "C3/mixed/amg/B1024", "4096")
     mine = json.load(open(dst))["C3/mixed/amg/B1024"]
     ref = json.load(open(os.path.join(P, "pmc_traffic.json")))["C3/mixed/amg/B1024"]
     assert mine["kernels"].keys() == ref["kernels"].keys()
@@ -76,7 +76,7 @@ def test_pmc_summary_reproduces_committed_entry(tmp_path):
 
 
 def test_headline_line_contract():
-    line = json.loads(open(os.path.join(P, "r04_bench_C3_default.json")).readline())
+    line = json.loads(open(os.path.join(P, "r05_bench_C3_default.json")).readline())
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline",
                 "cpu_baseline", "parity", "host_io"):
         assert key in line

@@ -24,7 +24,11 @@ mixed solve -- for aggregation-multigrid variants:
   sa=X        smoothed prolongator P = (I - X D^-1 A) P_tent at level 0,
               with the system's own A (per timestep)
   sa2=X       the same with lambda*a2 only (a per-mesh, timestep-free P)
+  sa1=X       smoothed P at the coarse levels (>= 1), with the level's own A
+  sa1a2=X     the same with the coarse levels' Galerkin image of lambda*a2 (per mesh)
+  sa1only=1   sa1 / sa1a2 at level 1 only (the transition 1 -> 2)
   w2          two coarse-grid visits per level-1 cycle (W-cycle at level 1)
+  nu1=K       K pre- and K post-smoothing sweeps at the coarse levels (V(K,K))
   q1=F        the sweeps at levels >= 1 on a stored copy of the operator: 1 bf16,
               2 int8 + one scale per block, 3 fp8 e4m3 + one scale per block,
               4 int8 + one scale per row
@@ -277,6 +281,13 @@ def build(A, a2m, e, opts):
             L.coarse = np.linalg.inv(Acur.toarray())
             break
         P, Bc = tentative(agg, na, Bnull, bs)
+        if lvl >= 1 and ("sa1" in opts or "sa1a2" in opts) and (lvl == 1 or "sa1only" not in opts):
+            # sa1: with the level's own A (per timestep); sa1a2: with the
+            # Galerkin image of lambda*a2 (per mesh)
+            Asm = Acur if "sa1" in opts else a2cur
+            _, Dinv_s = block_diag_inv(Asm, bs)
+            Dbsr = sp.block_diag([Dinv_s[i] for i in range(n)], format="csr")
+            P = (P - opts.get("sa1", opts.get("sa1a2")) * (Dbsr @ (Asm @ P))).tocsr()
         if lvl == 0 and ("sa" in opts or "sa2" in opts):
             Asm = Acur if "sa" in opts else a2m
             w = opts.get("sa", opts.get("sa2"))
@@ -380,13 +391,17 @@ def vcycle(levels, l, b, opts):
         if not hasattr(L, "Aq"):
             L.Aq = quantize(L.A, L.bs, int(qf))
         Aw = L.Aq
+    nu = int(opts.get("nu1", 1)) if l >= 1 else 1
     x = L.om * bsr_apply(L.Dinv, b, L.bs)
+    for _ in range(nu - 1):
+        x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
     cyc = 2 if (opts.get("w2") and l == 1) else 1
     for _ in range(cyc):
         r = b - Aw @ x
         y = vcycle(levels, l + 1, L.P.T @ r, opts)
         x = x + L.P @ y
-        x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
+        for _ in range(nu):
+            x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
     return x
 
 
