@@ -179,13 +179,6 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     // profiles/r04_ab/call10/), and on a small one (S1s, 3,249 vertices,
     // 30137 -> 28329) a third step costs less than the extra iterations
     if (amg && o.inner_rtol <= 0 && !mof::amg_fine(m).regular && m->N >= 16384) sp.inner_rtol = 1e-5;
-    // a folded closed surface (the W-cycle's regular meshes): the inner
-    // solves to 7e-5, so that the second refinement step meets the error
-    // control's bar without a third step for a quarter of the systems --
-    // round 5, F3 (profiles/r05_ab/inner/): 1945 -> 2014 timesteps/s, 30.1
-    // -> 31.0 PCG its in 2 instead of 3 steps; S1 / S1s (open) are flat
-    // over 1e-4 .. 3e-6, and C3 (no W-cycle) meets it at 1e-4
-    if (amg && o.inner_rtol <= 0 && mof::amg_fine(m).regular && mof::amg_fine(m).wcycle) sp.inner_rtol = 7e-5;
     tp[3] = now_ms();
     // host pointers: one upload of the nb+1 rows when I2 is I (S3
     // passes I_k twice), else nb rows of each

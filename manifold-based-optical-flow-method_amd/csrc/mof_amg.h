@@ -31,13 +31,15 @@ struct AmgParams {
     float smooth_omega = 0.66f;
     // smoothed aggregation at level 1 (the transition 1 -> 2), with the
     // Galerkin image P0^T a2 P0 of the mesh's a2 (per mesh, fp64 on the
-    // host): P1 = (I - w D1^-1 a2_1) P1_tent. 1 on, 0 off; applied when level
-    // 1 has more than kSubNodes nodes (the fused tiny levels keep the
-    // tentative transfers). CPU prototype (tools/amg_proto.py sa1a2=0.66
-    // sa1only=1, PCG its to 1e-4): the two-grid bound with an exact level-1
-    // solve is 8 its on F3 and 7 on C3, the V-cycle 18 / 8 -- the recursion
-    // below level 1 was F3's weakness; with P1 smoothed 12 / 7.
-    int32_t smooth1 = 1;
+    // host): P1 = (I - w D1^-1 a2_1) P1_tent. 1 on, 0 off (amg_build's
+    // auto choice: folded closed surfaces); applied when level 1 has more
+    // than kSubNodes nodes (the fused tiny levels keep the tentative
+    // transfers). CPU prototype (tools/amg_proto.py sa1a2=0.66 sa1only=1,
+    // PCG its to 1e-4): the two-grid bound with an exact level-1 solve is 8
+    // its on F3 and 7 on C3, the V-cycle 18 / 8 -- the recursion below level
+    // 1 was F3's weakness; with P1 smoothed 12 / 7 (C3 with the GPU's
+    // storage formats: 8 / 8).
+    int32_t smooth1 = 0;
     const double *a2 = nullptr;  // [sell_nb][4] level-0 a2 in the fine SELL layout (smoothing)
     // the fine level's mirror table when its operators are read symmetrically
     // (sell_mirror): level-0 gather entries of lower blocks then point at the
@@ -91,7 +93,12 @@ struct AmgHierarchy {
     // these over transitions with >= 64 aggregates (amg_build's W-cycle choice)
     std::vector<double> curl;
     double max_curl = 0.0;
+    bool folded = false;  // amg_build's auto choice rebuilt it with level 1 smoothed
 };
+
+// the fold criterion on AmgHierarchy::max_curl (amg_build): F3 0.46-0.51, the
+// jittered spheres <= 0.25 at every resolution, R3 0.09, S1 0.03
+constexpr double kFoldCurl = 0.35;
 
 void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,
                AmgHierarchy &H);

@@ -1438,7 +1438,10 @@ bool amg_build(mof_mesh *m) {
     if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
     if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
     if (const char *v = std::getenv("MOF_AMG_SMOOTH")) prm.smooth = std::atoi(v);  // 1 / 0 force, unset auto
-    if (const char *v = std::getenv("MOF_AMG_SMOOTH1")) prm.smooth1 = std::atoi(v);  // level 1: 1 / 0
+    // level 1's smoothed prolongator: -1 auto (below: folded closed
+    // surfaces), MOF_AMG_SMOOTH1=1 / 0 forces
+    prm.smooth1 = -1;
+    if (const char *v = std::getenv("MOF_AMG_SMOOTH1")) prm.smooth1 = std::atoi(v);
     if (m->n_own < m->N) prm.nown = m->n_own;
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
@@ -1465,7 +1468,7 @@ bool amg_build(mof_mesh *m) {
         MOF_HIP(hipStreamSynchronize(s));
         // the mesh's a2 (unscaled, fine SELL layout) for the smoothed prolongator
         std::vector<double> a2;
-        if (prm.nown < 0 && ((prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) || prm.smooth1 > 0)) {
+        if (prm.nown < 0 && ((prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat))) || prm.smooth1 != 0)) {
             a2.resize(4 * (size_t)m->pat.sell_nb());
             MOF_HIP(hipMemcpyAsync(a2.data(), m->a2.p, a2.size() * sizeof(double), hipMemcpyDeviceToHost, s));
             MOF_HIP(hipStreamSynchronize(s));
@@ -1478,7 +1481,29 @@ bool amg_build(mof_mesh *m) {
             prm.mirror = mir.data();
         }
         auto built = std::make_shared<AmgHierarchy>();
-        build_amg(m->pat, e.data(), prm, *built);
+        AmgParams p1 = prm;
+        p1.smooth1 = prm.smooth1 > 0 ? 1 : 0;
+        build_amg(m->pat, e.data(), p1, *built);
+        // auto: a closed surface whose coarse aggregates turn strongly (the
+        // median sigma_3 / sigma_1 of their near-null blocks >= kFoldCurl at
+        // some level: folds at the coarse levels' scale) is rebuilt with
+        // level 1's prolongator smoothed. Round 5, same box
+        // (profiles/r05_ab/sa1/): F3 (curl 0.46-0.51) 2003 -> 2292
+        // timesteps/s, 31.0 -> 26.2 PCG its, against the level-1 W-cycle's
+        // 2003 (23.0 its with both: 2131); C3 (curl <= 0.25) gains no
+        // iteration (17.0) and loses 12 % to the level-1 product; on the
+        // open S1 it breaks solves down (19 of 3072 recovered: the twice
+        // smoothed product cancels too much in fp32)
+        if (prm.smooth1 < 0 && !open_surface && prm.nown < 0 && prm.a2 && !built->levels.empty() &&
+            !built->levels[0].smoothed && built->max_curl >= kFoldCurl) {
+            const double curl = built->max_curl;
+            p1.smooth1 = 1;
+            auto again = std::make_shared<AmgHierarchy>();
+            build_amg(m->pat, e.data(), p1, *again);
+            again->max_curl = curl;
+            again->folded = true;
+            built = again;
+        }
         Hp = built;
         if (sh) {
             std::lock_guard<std::mutex> lk(sh->mu);
@@ -1511,16 +1536,12 @@ bool amg_build(mof_mesh *m) {
     // diverges there with the tentative P)
     if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = G.regular ? 1.1f : 1.05f;
     if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
-    // level 1 visits the levels below twice (W) where the coarse levels are
-    // weakest: on open surfaces, and on surfaces whose aggregates turn
-    // strongly at some coarse level (median sigma_3 / sigma_1 of an
-    // aggregate's near-null block >= kWCurl: folds at the coarse levels'
-    // scale). Round 5, same box (profiles/r05_ab/wcycle/): F3 (folded,
-    // curl 0.46 at level 2) 1727 -> 1934 timesteps/s (40.5 -> 30.1 PCG its),
-    // S1 (open) 858 -> 905 (59.5 -> 47.2); the spheres lose (C3, curl <= 0.24:
-    // 3652 -> 3370, 17.0 -> 15.9 its; R3 748 -> 657). MOF_AMG_W=0/1 forces.
-    constexpr double kWCurl = 0.35;
-    G.wcycle = m->n_own == m->N && (open_surface || H.max_curl >= kWCurl);
+    // level 1 visits the levels below twice (W) on open surfaces. Round 5,
+    // same box (profiles/r05_ab/wcycle/): S1 (open) 858 -> 905 timesteps/s
+    // (59.5 -> 47.2 PCG its); F3 (folded) 1727 -> 1934 (40.5 -> 30.1), where
+    // level 1's smoothed prolongator does better (above); the spheres lose
+    // (C3 3652 -> 3370, 17.0 -> 15.9 its; R3 748 -> 657). MOF_AMG_W=0/1 forces.
+    G.wcycle = m->n_own == m->N && open_surface;
     if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
@@ -1606,7 +1627,7 @@ bool amg_build(mof_mesh *m) {
             std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld%s curl %.3f%s\n", l,
                          H.levels[l].n, H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb(),
                          H.levels[l].smoothed ? " (smoothed P)" : "", l < H.curl.size() ? H.curl[l] : 0.0,
-                         l == 0 && G.wcycle ? " (W-cycle at level 1)" : "");
+                         l == 0 && G.wcycle ? " (W-cycle at level 1)" : (l == 0 && H.folded ? " (folded)" : ""));
     }
     MOF_HIP(hipStreamSynchronize(s));
     return true;

@@ -53,8 +53,9 @@ def test_hierarchy_deterministic_and_tiny():
     assert sizes == [len(p1)]
 
 
-def test_wcycle_criterion_separates_folded_from_spheres():
-    """The multigrid's W-cycle choice (amg_build, kWCurl = 0.35): the median
+def test_fold_criterion_separates_folded_from_spheres():
+    """The multigrid's fold choice (amg_build, kFoldCurl = 0.35: level 1's
+    prolongator smoothed on closed folded surfaces): the median
     turn of the tangent planes inside the coarse aggregates (sigma_3 /
     sigma_1 of their near-null blocks) is large on a folded surface (the
     F3 class, synth.folded_sphere) and stays small on jittered and random
