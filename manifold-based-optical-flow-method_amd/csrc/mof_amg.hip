@@ -947,6 +947,10 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 constexpr int kNSR = 8;    // systems per workgroup in the smoothed-P restriction
 constexpr int kNSP = 16;   // systems per thread in the smoothed-P prolongation
 constexpr int kRGS = 512;  // list entries per restriction group (smoothed P)
+// BSF = 3: level 1's smoothed prolongator (AmgParams::smooth1), r as float4
+// in node order; round 5 (F3): 938 us per 1024-system launch with one
+// (coarse node, system) per thread walking its list
+template <int BSF = 2>
 __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_t *__restrict__ grp, int32_t ngrp,
                                                       int32_t B, int32_t smooth, float omega,
                                                       const int32_t *__restrict__ sysi) {
@@ -967,17 +971,21 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
     const bool big = e1 - e0 > kRGS;  // one coarse node with an oversized list: summed from memory
     auto contrib = [&](int32_t e, float (&c3)[kNSR][3]) {
         const int32_t i = F.rent[2 * (int64_t)e];
-        const float *p = F.Q + (int64_t)F.rent[2 * (int64_t)e + 1] * 6;
-        float pm[6];
+        const float *p = F.Q + (int64_t)F.rent[2 * (int64_t)e + 1] * (BSF * 3);
+        float pm[BSF * 3];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) pm[k] = p[k];
-        float ri[kNSR][2];
+        for (int k = 0; k < BSF * 3; ++k) pm[k] = p[k];
+        float ri[kNSR][BSF];
 #pragma unroll
-        for (int t = 0; t < kNSR; ++t) ldr<2>(F.r, min(b0 + t, B - 1), F.n, i, ri[t]);
+        for (int t = 0; t < kNSR; ++t) ldr<BSF>(F.r, min(b0 + t, B - 1), F.n, i, ri[t]);
 #pragma unroll
         for (int t = 0; t < kNSR; ++t)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) c3[t][c] = pm[c] * ri[t][0] + pm[3 + c] * ri[t][1];
+            for (int c = 0; c < 3; ++c) {
+                float v = pm[c] * ri[t][0] + pm[3 + c] * ri[t][1];
+                if constexpr (BSF == 3) v += pm[6 + c] * ri[t][2];
+                c3[t][c] = v;
+            }
     };
     // two entries per thread and pass, both entries' loads in flight together
     for (int32_t e = e0 + threadIdx.x; e < e1 && !big; e += 2 * kWG) {
@@ -1079,55 +1087,42 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     }
 }
 
-// Level 1 with a smoothed prolongator (AmgParams::smooth1): the coarse
-// node's restriction list {fine node, P block} summed in list order, one
-// (coarse node, system) per thread -- level 1 is small (C3: 21,701 nodes;
-// the lists average 20 entries); with smooth also x_C = w D_C^-1 b_C.
-__global__ __launch_bounds__(kWG) void k_restrict3_sa(Lvl F, Lvl C, int32_t smooth, float omega,
-                                                      const int32_t *__restrict__ sysi) {
-#pragma clang fp contract(off)
-    const int32_t I = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
-    if (I >= C.n || retired(sysi, b)) return;
-    const int64_t fo = (int64_t)b * F.n * 4;
-    float acc[3] = {0.f, 0.f, 0.f};
-    for (int32_t e = F.rptr[I]; e < F.rptr[I + 1]; ++e) {
-        const int32_t i = F.rent[2 * (int64_t)e];
-        const float *p = F.Q + (int64_t)F.rent[2 * (int64_t)e + 1] * 9;
-        float r[3];
-        ldv<3>(F.r + fo, i, r);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) acc[c] += p[c] * r[0] + p[3 + c] * r[1] + p[6 + c] * r[2];
-    }
-    const int64_t vo = (int64_t)b * C.n * 4;
-    stv<3>(C.b + vo, I, acc);
-    if (smooth) {
-        float d[3][3], x[3];
-        ld_dh(C, b, I, d);
-        matvec<3>(d, acc, x);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) x[c] *= omega;
-        stv<3>(C.x + vo, I, x);
-    }
-}
-
 // x_i += sum over the fine node's P blocks of P_ik y_C[pcol k] (level 1,
-// smoothed prolongator), in place
-__global__ __launch_bounds__(kWG) void k_prolong3_sa(Lvl F, Lvl C, const int32_t *__restrict__ sysi) {
+// smoothed prolongator), in place; kNS3 systems per thread share the row's P
+// blocks and columns (round 5, F3: 559 us per 1024-system launch with one
+// system per thread)
+constexpr int kNS3 = 8;
+__global__ __launch_bounds__(kWG) void k_prolong3_sa(Lvl F, Lvl C, int32_t nblk, int32_t B,
+                                                     const int32_t *__restrict__ sysi) {
 #pragma clang fp contract(off)
-    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
-    if (i >= F.n || retired(sysi, b)) return;
-    float *xb = F.x + (int64_t)b * F.n * 4;
-    const float *yb = C.y + (int64_t)b * C.n * 4;
-    float xi[3];
-    ldv<3>(xb, i, xi);
+    int32_t rb, bq;
+    if (!xcd_map(nblk, (B + kNS3 - 1) / kNS3, rb, bq, kGrpProl)) return;
+    const int32_t i = rb * kWG + threadIdx.x;
+    if (i >= F.n) return;
+    const int32_t b0 = bq * kNS3;
+    float x[kNS3][3];
+#pragma unroll
+    for (int t = 0; t < kNS3; ++t) ldv<3>(F.x + (int64_t)min(b0 + t, B - 1) * F.n * 4, i, x[t]);
     for (int32_t k = F.pptr[i]; k < F.pptr[i + 1]; ++k) {
         const float *p = F.Q + (int64_t)k * 9;
-        float y[3];
-        ldv<3>(yb, F.pcol[k], y);
+        float pm[9];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) xi[r] += p[3 * r] * y[0] + p[3 * r + 1] * y[1] + p[3 * r + 2] * y[2];
+        for (int c = 0; c < 9; ++c) pm[c] = p[c];
+        const int32_t K = F.pcol[k];
+        float y[kNS3][3];
+#pragma unroll
+        for (int t = 0; t < kNS3; ++t) ldv<3>(C.y + (int64_t)min(b0 + t, B - 1) * C.n * 4, K, y[t]);
+#pragma unroll
+        for (int t = 0; t < kNS3; ++t)
+#pragma unroll
+            for (int r = 0; r < 3; ++r) x[t][r] += pm[3 * r] * y[t][0] + pm[3 * r + 1] * y[t][1] + pm[3 * r + 2] * y[t][2];
     }
-    stv<3>(xb, i, xi);
+#pragma unroll
+    for (int t = 0; t < kNS3; ++t) {
+        const int32_t b = b0 + t;
+        if (b >= B || retired(sysi, b)) continue;
+        stv<3>(F.x + (int64_t)b * F.n * 4, i, x[t]);
+    }
 }
 
 template <int BSF>
@@ -1794,7 +1789,8 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
             const int32_t smooth = l + 1 < L - 1;
             k_res3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], sysi);
             if (G.lv[l].smoothed)
-                k_restrict3_sa<<<grid2(u[l + 1].n, B), kWG, 0, s>>>(u[l], u[l + 1], smooth, om1, sysi);
+                k_restrict0_sa<3><<<dim3(xcd_grid(G.lv[l].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
+                    u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
             else
                 k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
                     u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
@@ -1808,8 +1804,11 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         sa.sysi = sysi;
         k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
         for (int32_t l = S - 1; l >= 1; --l) {
-            if (G.lv[l].smoothed)
-                k_prolong3_sa<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
+            if (G.lv[l].smoothed) {
+                const int32_t nb = (u[l].n + kWG - 1) / kWG;
+                k_prolong3_sa<<<dim3(xcd_grid(nb, (B + kNS3 - 1) / kNS3, kGrpProl)), kWG, 0, s>>>(u[l], u[l + 1], nb,
+                                                                                                   B, sysi);
+            }
             else
                 k_prolong<3><<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
             k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
@@ -1825,7 +1824,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                                  kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
                                               G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
             if (G.lv[0].smoothed) {
-                k_restrict0_sa<<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict0_sa<2><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             } else {
                 k_restrict<2, kRestrS><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kRestrS - 1) / kRestrS, kGrpRestr)), kWG, 0, s>>>(
