@@ -69,10 +69,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    # 1024 timesteps per step: +1-4 % over 512 by box (round 4,
-    # profiles/r04_ab/batch/: the setup kernels and the small multigrid
-    # levels hide more latency per launch), 1536 +3 % more at 225 GB of HBM
-    ap.add_argument("--batch", type=int, default=1024, help="timesteps per step")
+    # 1536 timesteps per step: +1-2 % over 1024 on one box (round 5,
+    # profiles/r05_ab/batch/: 3710 vs 3626-3675 timesteps/s at C3), which was
+    # +1-4 % over 512 (round 4: the setup kernels and the small multigrid
+    # levels hide more latency per launch); ~235 GB of HBM at C3 with the
+    # driver's 25 steps of signal rows, else the largest of 1024, 512, ...
+    # that fits
+    ap.add_argument("--batch", type=int, default=1536, help="timesteps per step")
     ap.add_argument("--config", default="C3", choices=sorted(CONFIG_NAMES))
     ap.add_argument("--precision", default=None, choices=["mixed", "f64"])
     ap.add_argument("--precond", default=None, choices=["jacobi", "amg"],
@@ -307,6 +310,8 @@ def main():
             return 720.0 * N * b + 8.0 * N * rows + 16.0 * N * b
 
         B0 = B
+        if need(B) > 0.85 * free_b and B > 1024:
+            B = 1024
         while B > 64 and need(B) > 0.85 * free_b:
             B //= 2
         if B != B0:
