@@ -1477,7 +1477,12 @@ bool amg_build(mof_mesh *m) {
         }
         auto built = std::make_shared<AmgHierarchy>();
         AmgParams p1 = prm;
-        p1.smooth1 = prm.smooth1 > 0 ? 1 : 0;
+        // level 1 smoothed at once where level 0 is (irregular or open
+        // surfaces): round 5, same box (profiles/r05_ab/sa1/): R3 742 ->
+        // 842 timesteps/s (53.6 -> 41.8 PCG its), S1 905 (with the level-1
+        // W-cycle) -> 995 (44.8 its; with both, 5 of 1536 solves broke down)
+        const bool l0_smooth = prm.nown < 0 && prm.a2 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat));
+        p1.smooth1 = prm.smooth1 > 0 || (prm.smooth1 < 0 && l0_smooth) ? 1 : 0;
         build_amg(m->pat, e.data(), p1, *built);
         // auto: a closed surface whose coarse aggregates turn strongly (the
         // median sigma_3 / sigma_1 of their near-null blocks >= kFoldCurl at
@@ -1489,7 +1494,7 @@ bool amg_build(mof_mesh *m) {
         // iteration (17.0) and loses 12 % to the level-1 product; on the
         // open S1 it breaks solves down (19 of 3072 recovered: the twice
         // smoothed product cancels too much in fp32)
-        if (prm.smooth1 < 0 && !open_surface && prm.nown < 0 && prm.a2 && !built->levels.empty() &&
+        if (prm.smooth1 < 0 && p1.smooth1 == 0 && prm.nown < 0 && prm.a2 && !built->levels.empty() &&
             !built->levels[0].smoothed && built->max_curl >= kFoldCurl) {
             const double curl = built->max_curl;
             p1.smooth1 = 1;
@@ -1531,12 +1536,13 @@ bool amg_build(mof_mesh *m) {
     // diverges there with the tentative P)
     if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = G.regular ? 1.1f : 1.05f;
     if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
-    // level 1 visits the levels below twice (W) on open surfaces. Round 5,
-    // same box (profiles/r05_ab/wcycle/): S1 (open) 858 -> 905 timesteps/s
-    // (59.5 -> 47.2 PCG its); F3 (folded) 1727 -> 1934 (40.5 -> 30.1), where
-    // level 1's smoothed prolongator does better (above); the spheres lose
-    // (C3 3652 -> 3370, 17.0 -> 15.9 its; R3 748 -> 657). MOF_AMG_W=0/1 forces.
-    G.wcycle = m->n_own == m->N && open_surface;
+    // level 1 visiting the levels below twice (W): measured, not the default.
+    // Round 5, same box (profiles/r05_ab/wcycle/): S1 (open) 858 -> 905
+    // timesteps/s (59.5 -> 47.2 PCG its), F3 (folded) 1727 -> 1934 (40.5 ->
+    // 30.1) -- level 1's smoothed prolongator does better on both (995,
+    // 2292) -- and the spheres lose (C3 3652 -> 3370, R3 748 -> 657).
+    // MOF_AMG_W=1 forces it.
+    G.wcycle = false;
     if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
