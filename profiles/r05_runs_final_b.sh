@@ -1,9 +1,10 @@
 #!/bin/bash
 # Round 5 final measurements, part B: the other configurations.
 set -o pipefail
-D=gpurun_out/r05final
+D=gpurun_out/r05final2
 mkdir -p $D
 export TMPDIR=/tmp
+timeout -k 10 400 python3 -u bench.py > $D/bench_C3_default.json 2> $D/bench_C3_default.err || exit 90
 timeout -k 10 200 python3 -u bench.py --config S1s > $D/bench_S1s.json 2> $D/bench_S1s.err || exit 91
 timeout -k 10 200 python3 -u bench.py --config C1 > $D/bench_C1.json 2> $D/bench_C1.err || exit 92
 timeout -k 10 240 python3 -u bench.py --config S1 --steps 5 --no-cpu-baseline > $D/bench_S1.json 2> $D/bench_S1.err || exit 93
