@@ -1201,7 +1201,9 @@ __global__ __launch_bounds__(kWG) void k_post3(Lvl L, float omega, const int32_t
 // The cycle below level S (all levels with <= kSubNodes nodes) in one launch:
 // one workgroup per system walks the tiny levels with barriers in between,
 // replacing ~4 launches per level.
-constexpr int kSubWG = 256;
+// 512 threads: a 400-node level (the 3,249-vertex S1s's level 1) takes one
+// row per thread in its sweeps instead of two
+constexpr int kSubWG = 512;
 // kSubNodes: mof_amg.h
 constexpr int kMaxLevels = 12;
 
@@ -1226,19 +1228,22 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
         __syncthreads();
     }
     // coarsest: y = A_c^-1 b (the inverse is symmetric: read by columns);
-    // b staged in LDS, the k range split over the two halves of the
-    // workgroup, 16 independent loads in flight per thread
+    // b staged in LDS, the k range split over the kH groups of kMaxCoarse
+    // threads, 16 independent loads in flight per thread, the groups'
+    // partial sums added in group order
     {
+        constexpr int kH = kSubWG / kMaxCoarse;
         __shared__ float bl[kMaxCoarse];
-        __shared__ float part[kMaxCoarse];
+        __shared__ float part[kH][kMaxCoarse];
         const Lvl &C = a.lv[a.last];
         const int32_t nc = 3 * C.n;
         const float *Mi = a.cinv + (int64_t)b * nc * nc;
         const float *bb = C.b + (int64_t)b * C.n * 4;
         for (int32_t q = tid; q < nc; q += kSubWG) bl[q] = bb[4 * (q / 3) + q % 3];
         __syncthreads();
-        const int32_t d = tid % kMaxCoarse, hf = tid / kMaxCoarse;  // kSubWG = 2 * kMaxCoarse
-        const int32_t k0 = hf * ((nc + 1) / 2), k1 = hf ? nc : (nc + 1) / 2;
+        const int32_t d = tid % kMaxCoarse, hf = tid / kMaxCoarse;
+        const int32_t chunk = (nc + kH - 1) / kH;
+        const int32_t k0 = min(nc, hf * chunk), k1 = min(nc, k0 + chunk);
         float sum = 0.f;
         if (d < nc) {
             constexpr int U = 16;
@@ -1250,9 +1255,14 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
                 for (int u = 0; u < U; ++u) sum += (k + u < k1) ? mv[u] * bl[min(k + u, k1 - 1)] : 0.f;
             }
         }
-        if (hf) part[d] = sum;
+        part[hf][d] = sum;
         __syncthreads();
-        if (!hf && d < nc) C.y[(int64_t)b * C.n * 4 + 4 * (d / 3) + d % 3] = sum + part[d];
+        if (!hf && d < nc) {
+            float t = part[0][d];
+#pragma unroll
+            for (int h = 1; h < kH; ++h) t += part[h][d];
+            C.y[(int64_t)b * C.n * 4 + 4 * (d / 3) + d % 3] = t;
+        }
         __syncthreads();
     }
     // up
