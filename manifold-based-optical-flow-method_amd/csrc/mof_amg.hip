@@ -495,65 +495,8 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ent(
     const int32_t b0 = bq * kGalENS;
     const int32_t p0 = ggrp[g], p1 = ggrp[g + 1];
     const int32_t e0 = gptr[p0], e1 = gptr[p1];
-    const int32_t np = p1 - p0;
-    if (e1 - e0 > kWG) {
-        // one position with more entries than the workgroup has threads (a
-        // smoothed level's diagonal block): thread t sums system t's terms
-        // straight from memory, the same terms in the same order as the
-        // staged path, so the same bits
-        const int32_t t = threadIdx.x, b = b0 + t, I = c_sell_row[p0];
-        if (t >= kGalENS || b >= B || I >= nC) return;
-        float Cm[3][3] = {};
-        for (int32_t q = e0; q < e1; ++q) {
-            const int32_t fp = gent[3 * (int64_t)q], ii = gent[3 * (int64_t)q + 1], jj = gent[3 * (int64_t)q + 2];
-            float qi[3][3], qj[3][3], a[3][3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    qi[k][c] = Q[((int64_t)ii * 3 + k) * 3 + c];
-                    qj[k][c] = Q[((int64_t)jj * 3 + k) * 3 + c];
-                }
-            ldm<3>(Af + (int64_t)b * f_sell_nb * kB3, max(fp, 0), a);
-            if (fp < 0) {
-#pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) a[r][k] = (fp == -1 && r == k) ? 1.f : 0.f;
-            }
-            float T[3][3];  // A Q_j
-#pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    float sum = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) sum += a[r][k] * qj[k][c];
-                    T[r][c] = sum;
-                }
-#pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    float sum = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) sum += qi[k][r] * T[k][c];
-                    Cm[r][c] += sum;
-                }
-        }
-        if (p0 == c_diag[I]) {
-#pragma unroll
-            for (int d = 0; d < 3; ++d)
-                if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
-            float D[3][3];
-            inv3(Cm, D);
-            st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
-        }
-        st3(Ac, (int64_t)b * c_sell_nb + p0, Cm);
-        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + p0, Cm);
-        return;
-    }
     const int32_t e = e0 + (int32_t)threadIdx.x;
+    const int32_t np = p1 - p0;
     int32_t tI = nC, tq0 = 0, tq1 = 0, tdg = -1;
     if ((int32_t)threadIdx.x < np * kGalENS) {
         const int32_t pos = p0 + (int32_t)threadIdx.x / kGalENS;
@@ -1675,20 +1618,13 @@ bool amg_build(mof_mesh *m) {
             if ((!L.smoothed || l >= 1) && ent_here && !(ge && *ge && std::atoi(ge) == 0)) {
                 const std::vector<int32_t> &gq = L.gptr;
                 const int32_t npos = (int32_t)gq.size() - 1;
-                // level >= 1: a position with more than kWG entries forms a
-                // group of its own (k_galerkin3_ent sums it from memory);
-                // level 0's kernel has no such path
                 bool ok = true;
-                for (int32_t p = 0; p < npos && ok && l == 0; ++p) ok = gq[p + 1] - gq[p] <= kWG;
+                for (int32_t p = 0; p < npos && ok; ++p) ok = gq[p + 1] - gq[p] <= kWG;
                 if (ok) {
                     std::vector<int32_t> gg{0};
-                    for (int32_t p = 0; p < npos; ++p) {
-                        const bool big = gq[p + 1] - gq[p] > kWG;
-                        if (p > gg.back() && (big || gq[p + 1] - gq[gg.back()] > kWG || p - gg.back() >= kWG))
-                            gg.push_back(p);
-                        if (big) gg.push_back(p + 1);
-                    }
-                    if (gg.back() != npos) gg.push_back(npos);
+                    for (int32_t p = 0; p < npos; ++p)
+                        if (gq[p + 1] - gq[gg.back()] > kWG || p - gg.back() >= kWG) gg.push_back(p);
+                    gg.push_back(npos);
                     D.nggrp = (int32_t)gg.size() - 1;
                     put_i(D.ggrp, gg);
                 }
