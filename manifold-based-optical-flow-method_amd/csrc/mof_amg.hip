@@ -1492,7 +1492,7 @@ bool amg_build(mof_mesh *m) {
         // 842 timesteps/s (53.6 -> 41.8 PCG its), S1 905 (with the level-1
         // W-cycle) -> 995 (44.8 its; with both, 5 of 1536 solves broke down)
         const bool l0_smooth = prm.nown < 0 && prm.a2 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat));
-        p1.smooth1 = prm.smooth1 > 0 || (prm.smooth1 < 0 && l0_smooth) ? 1 : 0;
+        p1.smooth1 = prm.smooth1 > 0 ? prm.smooth1 : (prm.smooth1 < 0 && l0_smooth ? 1 : 0);
         build_amg(m->pat, e.data(), p1, *built);
         // auto: a closed surface whose coarse aggregates turn strongly (the
         // median sigma_3 / sigma_1 of their near-null blocks >= kFoldCurl at

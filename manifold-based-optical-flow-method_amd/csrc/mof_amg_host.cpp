@@ -448,7 +448,10 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
         // prolongator rows: the tentative Q (one block per node), or smoothed
         const bool smooth = H.levels.size() == 1 && prm.nown < 0 && prm.a2 &&
                             (prm.smooth > 0 || (prm.smooth < 0 && amg_auto_smooth(fine)));
-        const bool smooth1 = H.levels.size() == 2 && prm.smooth1 > 0 && !F.a2img.empty() && F.n > kSubNodes;
+        // coarse levels: level 1 (smooth1 = 1), or every level above the fused
+        // tiny ones (smooth1 = 2), each from its own image of a2
+        const bool smooth1 = (H.levels.size() == 2 || (H.levels.size() > 2 && prm.smooth1 > 1)) && prm.smooth1 > 0 &&
+                             !F.a2img.empty() && F.n > kSubNodes;
         if (smooth || smooth1) {
             std::vector<float> P;
             if (smooth)
@@ -509,6 +512,8 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
                 if (fine.sell_blk[pos] >= 0)
                     for (int k = 0; k < 4; ++k) ab[4 * (size_t)fine.sell_blk[pos] + k] = prm.a2[4 * pos + k];
             C.a2img = galerkin_image(F, 2, ab, C);
+        } else if (H.levels.size() >= 2 && prm.smooth1 > 1 && !F.a2img.empty() && C.n > kSubNodes) {
+            C.a2img = galerkin_image(F, 3, F.a2img, C);
         }
         // Galerkin gather lists: coarse block -> terms P_iK^T A_ij P_jL, in fine
         // block order (then P block order)
