@@ -116,8 +116,6 @@ struct AmgDevLevel {
     DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
     DevArray<int32_t> ggrp;                         // level 0, tentative P: Galerkin groups (coarse
                                                     // position ranges of <= kWG gather entries)
-    DevArray<int32_t> gperm;                        // per-position Galerkin kernel: the next level's
-                                                    // positions by descending entry count (or empty)
     bool smoothed = false;                          // level 0: smoothed prolongator
     DevArray<int32_t> pptr, pcol, rptr, rent;
     int32_t ngrp = 0, nggrp = 0;

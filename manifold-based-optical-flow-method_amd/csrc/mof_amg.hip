@@ -399,25 +399,18 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
 // 4 entries per load batch), 935 with 2, 851 with 4 (132 VGPRs, 3 waves);
 // C3 +0.5 %, R3 (denser level 1) within noise (round 3).
 constexpr int kGal3NS = 4;
-// gperm (optional): the positions in descending order of their entry
-// counts, so that a wave's threads walk lists of about the same length (a
-// smoothed level's lists run from a few entries to several hundred: with
-// node order each wave waits for its longest); same per-position sums, same
-// bits.
 template <int NS>
 __global__ __launch_bounds__(kWG) void k_galerkin3_ns(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
-    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
-    const int32_t *__restrict__ gperm) {
+    uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
 #pragma clang fp contract(off)
     int32_t tile, bq;
     if (!xcd_map((int32_t)((c_sell_nb + kWG - 1) / kWG), (B + NS - 1) / NS, tile, bq, kGrpGal)) return;
-    const int64_t slot = (int64_t)tile * kWG + threadIdx.x;
-    if (slot >= c_sell_nb) return;
-    const int64_t pos = gperm ? gperm[slot] : slot;
+    const int64_t pos = (int64_t)tile * kWG + threadIdx.x;
+    if (pos >= c_sell_nb) return;
     const int32_t I = c_sell_row[pos];
     if (I >= nC) return;
     const int32_t b0 = bq * NS;
@@ -1627,14 +1620,6 @@ bool amg_build(mof_mesh *m) {
                 const int32_t npos = (int32_t)gq.size() - 1;
                 bool ok = true;
                 for (int32_t p = 0; p < npos && ok; ++p) ok = gq[p + 1] - gq[p] <= kWG;
-                if (!ok && l >= 1 && L.smoothed) {
-                    std::vector<int32_t> perm(npos);
-                    for (int32_t p = 0; p < npos; ++p) perm[p] = p;
-                    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) {
-                        return gq[a + 1] - gq[a] > gq[b + 1] - gq[b];
-                    });
-                    put_i(D.gperm, perm);
-                }
                 if (ok) {
                     std::vector<int32_t> gg{0};
                     for (int32_t p = 0; p < npos; ++p)
@@ -1762,7 +1747,7 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
             k_galerkin3_ns<kGal3NS>
                 <<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGal3NS - 1) / kGal3NS, kGrpGal)), kWG,
                    0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
-                           F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C), F.gperm.n ? F.gperm.p : nullptr);
+                           F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];
     k_coarse_inverse<<<dim3((unsigned)B), kInvWG, 0, s>>>(Lc.n, Lc.sell_off.p, Lc.sell_col.p, Lc.A.p,
