@@ -114,8 +114,11 @@ struct AmgDevLevel {
     DevArray<uint8_t> dead;                          // level >= 1
     DevArray<int32_t> agg, mptr, mlist, apos, gptr, gent;  // transition to level + 1
     DevArray<int32_t> rgrp;                         // restriction groups (aggregate ranges)
-    DevArray<int32_t> ggrp;                         // level 0, tentative P: Galerkin groups (coarse
-                                                    // position ranges of <= kWG gather entries)
+    DevArray<int32_t> ggrp;                         // Galerkin groups for the products by entry: coarse
+                                                    // position ranges [p0, p1) of <= kWG gather entries
+    DevArray<int32_t> gbig;                         // levels >= 1: positions past kGalBig entries, one
+                                                    // workgroup each (k_galerkin3_big)
+    int32_t nbig = 0;
     bool smoothed = false;                          // level 0: smoothed prolongator
     DevArray<int32_t> pptr, pcol, rptr, rent;
     int32_t ngrp = 0, nggrp = 0;
@@ -126,6 +129,8 @@ struct AmgDevLevel {
     DevArray<uint16_t> Dh22;     // [B][n] entry (2,2)
     DevArray<uint32_t> Ah;       // sweep copy (not the coarsest), st_a9: [B][sell_nb][2] int8 codes 0..7
     DevArray<uint16_t> Ah22;     // [B][sell_nb][2] code 8 | bf16 scale (MOF_COARSE_I8=0: [4] / [1] bf16)
+    DevArray<float> slab;        // level 1 of a smoothed level 0: one system slab's A as
+                                 // [sell_nb][64][12] (k_galerkin_sys<2> -> <3>)
     DevArray<float> b, x, r, y;  // [B][n][4] (level >= 1); level 0: x [B][n][2], r bf16 pairs [B][n]
                                  // r is stored in member order of the next level
 };
@@ -143,6 +148,9 @@ struct AmgDevice {
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)
+    // smoothed level 0: one slab of 64 systems' fp32 level-0 blocks as
+    // [sell_nb][64][4] (k_a_slab -> k_galerkin0_sys), reused slab by slab
+    DevArray<float> aslab;
     bool bf16_fresh = false;  // A0h written by the batch's assembly
 };
 

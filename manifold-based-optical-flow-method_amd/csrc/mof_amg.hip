@@ -317,7 +317,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
     const int32_t nq = (B + kGalENS - 1) / kGalENS;
     if (!xcd_map(ngrp, nq, g, bq, kGrpGal)) return;
     const int32_t b0 = bq * kGalENS;
-    const int32_t p0 = ggrp[g], p1 = ggrp[g + 1];
+    const int32_t p0 = ggrp[2 * g], p1 = ggrp[2 * g + 1];
     const int32_t e0 = gptr[p0], e1 = gptr[p1];
     const int32_t e = e0 + (int32_t)threadIdx.x;
     const int32_t np = p1 - p0;
@@ -389,6 +389,148 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
         }
         st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
         if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+    }
+}
+
+// Level 0 with the smoothed prolongator, by system slab: the gather lists
+// are wave-uniform and the 64 lanes of a wave are 64 systems of one coarse
+// position. The per-position kernel above (one position of 4 systems per
+// thread) gathers a 16-byte fine block per system from 4 lines 20 MB apart,
+// 64 positions' scattered blocks per load: S1 122 ms per 1536-system batch,
+// L2-line bound. Here a slab of kSlab systems' fp32 level-0 blocks is first
+// transposed to [fine position][system] (k_a_slab), so one fine block of
+// the whole wave is one 1 KB read, and the entry and its two P blocks are
+// scalar loads shared by the 64 systems. Every system runs the same
+// instructions in its own lane: the bits do not depend on the batch split.
+// S1, per 1536-system batch: level 0 122.5 -> 12.3 (k_a_slab) + 40.6 ms,
+// S1 1014 -> 1064 timesteps/s; with level 1 -> 2 from the slab copy level 0
+// writes beside its A (k_galerkin_sys<3>, instead of the chunked / by-entry
+// products, 55 ms): level 0 46.5 + level 1 29.6 ms, R3 906 -> 918
+// (profiles/r05_ab/gal_slab/).
+constexpr int kSlab = 64;
+constexpr int kSlabPos = 64;  // fine positions per k_a_slab workgroup
+__global__ __launch_bounds__(kWG) void k_a_slab(int64_t f_sell_nb, int32_t b0, int32_t nb,
+                                                const float4 *__restrict__ Af, float4 *__restrict__ AI) {
+    __shared__ float4 t[kSlabPos][kSlab + 1];
+    const int64_t q0 = (int64_t)blockIdx.x * kSlabPos;
+    const int32_t lane = (int32_t)threadIdx.x & 63, w = (int32_t)threadIdx.x >> 6;
+    // read: a wave takes one system's 64 consecutive blocks (1 KB)
+    for (int32_t s = w; s < kSlab; s += kWG / 64) {
+        const int64_t q = q0 + lane;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s < nb && q < f_sell_nb) v = Af[(int64_t)(b0 + s) * f_sell_nb + q];
+        t[lane][s] = v;
+    }
+    __syncthreads();
+    // write: a wave takes one fine position's 64 systems (1 KB)
+    for (int32_t k = w; k < kSlabPos; k += kWG / 64) {
+        const int64_t q = q0 + k;
+        if (q < f_sell_nb) AI[q * kSlab + lane] = t[k][lane];
+    }
+}
+
+constexpr int kGalSysPos = kWG / 64;  // coarse positions per workgroup, one per wave
+// Level l's Galerkin product over one system slab: BSF = 2 reads the level-0
+// slab (k_a_slab, float4 blocks, mirror entries), BSF = 3 the slab a level
+// l >= 1 product wrote beside its level's A (CS: [sell_nb][kSlab][3] float4,
+// the stored rows). Gather entries per load batch: 4 at level 0, 2 on the
+// coarse levels (their P blocks are 18 scalar registers each).
+template <int BSF>
+__global__ __launch_bounds__(kWG) void k_galerkin_sys(
+    int64_t c_sell_nb, int32_t nC, int32_t B, int32_t b0, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ gent, const float *__restrict__ Q, const float4 *__restrict__ FS,
+    float *__restrict__ Ac, uint4 *__restrict__ Dh, uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah,
+    uint16_t *__restrict__ Ah22, float4 *__restrict__ CS) {
+    constexpr int U = BSF == 2 ? 4 : 2;
+    constexpr int QS = 3 * BSF;  // floats per P block
+    int32_t tile, bq;
+    if (!xcd_map((int32_t)((c_sell_nb + kGalSysPos - 1) / kGalSysPos), 1, tile, bq, 1)) return;
+    const int64_t pos = (int64_t)tile * kGalSysPos + __builtin_amdgcn_readfirstlane((int32_t)threadIdx.x >> 6);
+    if (pos >= c_sell_nb) return;
+    const int32_t I = c_sell_row[pos];
+    if (I >= nC) return;
+    const int32_t lane = (int32_t)threadIdx.x & 63;
+    float Cm[3][3] = {};
+    const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
+    // U entries per load batch (the entries' scalar loads, then their fine
+    // blocks, in flight together); a batch's tail entries past g1 are
+    // clamped to the last one and skipped (wave-uniform)
+    for (int32_t t0 = g0; t0 < g1; t0 += U) {
+        int32_t fp[U];
+        float qi[U][QS], qj[U][QS], a[U][BSF][BSF];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = min(t0 + u, g1 - 1);
+            fp[u] = gent[3 * g];
+            const int32_t ii = gent[3 * g + 1], jj = gent[3 * g + 2];
+#pragma unroll
+            for (int k = 0; k < QS; ++k) {
+                qi[u][k] = Q[(int64_t)ii * QS + k];
+                qj[u][k] = Q[(int64_t)jj * QS + k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (fp[u] < 0) {  // a decomposed part's ghost block: identity / zero
+#pragma unroll
+                for (int r = 0; r < BSF; ++r)
+#pragma unroll
+                    for (int c = 0; c < BSF; ++c) a[u][r][c] = (fp[u] == -1 && r == c) ? 1.f : 0.f;
+            } else if constexpr (BSF == 2) {
+                const float4 v = FS[(int64_t)(fp[u] & kMirPos) * kSlab + lane];
+                const bool tr = fp[u] & kMirT;  // transposed upper block
+                a[u][0][0] = v.x; a[u][0][1] = tr ? v.z : v.y; a[u][1][0] = tr ? v.y : v.z; a[u][1][1] = v.w;
+            } else {
+                const float4 *p = FS + ((int64_t)fp[u] * kSlab + lane) * 3;
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const float4 v = p[r];
+                    a[u][r][0] = v.x; a[u][r][1] = v.y; a[u][r][2] = v.z;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (t0 + u >= g1) break;
+            // P blocks are BSF x 3, row-major: q[k * 3 + c]
+            float T[BSF][3];  // A Q_j
+#pragma unroll
+            for (int r = 0; r < BSF; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < BSF; ++k) sum += a[u][r][k] * qj[u][k * 3 + c];
+                    T[r][c] = sum;
+                }
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < BSF; ++k) sum += qi[u][k * 3 + r] * T[k][c];
+                    Cm[r][c] += sum;
+                }
+        }
+    }
+    const int32_t b = b0 + lane;
+    if (b >= B) return;
+    if (pos == c_diag[I]) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
+        float D[3][3];
+        inv3(Cm, D);
+        st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
+    }
+    st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
+    if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+    if (CS) {
+        float4 *p = CS + (pos * kSlab + lane) * 3;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) p[r] = make_float4(Cm[r][0], Cm[r][1], Cm[r][2], 0.f);
     }
 }
 
@@ -493,7 +635,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ent(
     const int32_t nq = (B + kGalENS - 1) / kGalENS;
     if (!xcd_map(ngrp, nq, g, bq, kGrpGal)) return;
     const int32_t b0 = bq * kGalENS;
-    const int32_t p0 = ggrp[g], p1 = ggrp[g + 1];
+    const int32_t p0 = ggrp[2 * g], p1 = ggrp[2 * g + 1];
     const int32_t e0 = gptr[p0], e1 = gptr[p1];
     const int32_t e = e0 + (int32_t)threadIdx.x;
     const int32_t np = p1 - p0;
@@ -572,6 +714,121 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ent(
         if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
     }
 }
+
+// Levels >= 1, the coarse positions with more than kGalBig gather entries
+// (a smoothed level's: S1 level 1 mean 105, p90 247, max 789 entries; 85 %
+// of its terms sit in positions past 128, where one thread per position
+// leaves a SELL wave 0.24 busy): one workgroup per (position, NSB systems)
+// walks the list in chunks of kWG entries -- every thread one entry's term
+// for the NSB systems, staged in LDS -- and 9 NSB threads, one per (system,
+// block entry), fold each chunk in list order. Each block entry is a sum of
+// its own terms, so the bits are k_galerkin3_ns's. S1 (1536 systems), level
+// 1 -> 2: 42.8 ms per launch per position -> 20.9 by chunk (and 4.6 ms for
+// the positions below the bound by entry); 4 systems per workgroup 23.1, 8
+// 25.8, bound 64 entries 24.9 + 3.3 (profiles/r05_ab/gal_slab/).
+constexpr int kGalBig = 128;
+template <int NSB>
+__global__ __launch_bounds__(kWG) void k_galerkin3_big(
+    int32_t nbig, const int32_t *__restrict__ gbig, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ gent, const float *__restrict__ Q, const float *__restrict__ Af, int64_t f_sell_nb,
+    int64_t c_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh, uint16_t *__restrict__ Dh22,
+    uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
+#pragma clang fp contract(off)
+    // rows padded by one word: the 9 NSB summing lanes read one column at
+    // a time, kWG + 1 words apart -- distinct banks
+    __shared__ float con[NSB][9][kWG + 1];
+    __shared__ float fin[NSB][9];
+    int32_t g, bq;
+    if (!xcd_map(nbig, (B + NSB - 1) / NSB, g, bq, kGrpGal)) return;
+    const int32_t b0 = bq * NSB;
+    const int32_t pos = gbig[g];
+    const int32_t e0 = gptr[pos], e1 = gptr[pos + 1];
+    const int32_t sk = (int32_t)threadIdx.x;  // summing lane: system sk / 9, block entry sk % 9
+    float acc = 0.f;
+    for (int32_t c0 = e0; c0 < e1; c0 += kWG) {
+        const int32_t e = c0 + (int32_t)threadIdx.x;
+        if (e < e1) {
+            const int32_t fp = gent[3 * (int64_t)e], ii = gent[3 * (int64_t)e + 1], jj = gent[3 * (int64_t)e + 2];
+            float qi[3][3], qj[3][3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    qi[k][c] = Q[((int64_t)ii * 3 + k) * 3 + c];
+                    qj[k][c] = Q[((int64_t)jj * 3 + k) * 3 + c];
+                }
+            float a[NSB][3][3];
+#pragma unroll
+            for (int t = 0; t < NSB; ++t) {
+                ldm<3>(Af + (int64_t)min(b0 + t, B - 1) * f_sell_nb * kB3, max(fp, 0), a[t]);
+                if (fp < 0) {
+#pragma unroll
+                    for (int r = 0; r < 3; ++r)
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) a[t][r][k] = (fp == -1 && r == k) ? 1.f : 0.f;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < NSB; ++t) {
+                float T[3][3];  // A Q_j
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        float sum = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) sum += a[t][r][k] * qj[k][c];
+                        T[r][c] = sum;
+                    }
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        float sum = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) sum += qi[k][r] * T[k][c];
+                        con[t][3 * r + c][threadIdx.x] = sum;
+                    }
+            }
+        }
+        __syncthreads();
+        if (sk < 9 * NSB) {
+            const float *row = con[sk / 9][sk % 9];
+            const int32_t m = min(kWG, e1 - c0);
+            int32_t q = 0;
+            for (; q + 8 <= m; q += 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = row[q + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += v[u];
+            }
+            for (; q < m; ++q) acc += row[q];
+        }
+        __syncthreads();
+    }
+    if (sk < 9 * NSB) fin[sk / 9][sk % 9] = acc;
+    __syncthreads();
+    if ((int32_t)threadIdx.x >= NSB) return;
+    const int32_t t = (int32_t)threadIdx.x, b = b0 + t;
+    if (b >= B) return;
+    const int32_t I = c_sell_row[pos];
+    float Cm[3][3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Cm[k / 3][k % 3] = fin[t][k];
+    if (pos == c_diag[I]) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
+        float D[3][3];
+        inv3(Cm, D);
+        st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
+    }
+    st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
+    if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+}
+constexpr int kGalBigNS = 2;
 
 constexpr int kMaxCoarse = 128;
 constexpr int kInvWG = 1024;
@@ -1615,18 +1872,41 @@ bool amg_build(mof_mesh *m) {
             const char *ge = std::getenv("MOF_GAL_ENT");
             const char *ge3 = std::getenv("MOF_GAL3_ENT");
             const bool ent_here = l == 0 || !(ge3 && *ge3 && std::atoi(ge3) == 0);
+            // Levels >= 1: positions past kGalBig entries (MOF_GAL_BIG: the
+            // threshold, 0 = none, i.e. a level with a position past kWG
+            // keeps the per-position product) go to k_galerkin3_big.
             if ((!L.smoothed || l >= 1) && ent_here && !(ge && *ge && std::atoi(ge) == 0)) {
+                const char *gb = std::getenv("MOF_GAL_BIG");
+                const int32_t big = l == 0 ? 0 : std::min<int32_t>(kWG, gb && *gb ? std::atoi(gb) : kGalBig);
                 const std::vector<int32_t> &gq = L.gptr;
                 const int32_t npos = (int32_t)gq.size() - 1;
                 bool ok = true;
-                for (int32_t p = 0; p < npos && ok; ++p) ok = gq[p + 1] - gq[p] <= kWG;
+                for (int32_t p = 0; p < npos && ok; ++p) ok = big > 0 || gq[p + 1] - gq[p] <= kWG;
                 if (ok) {
-                    std::vector<int32_t> gg{0};
-                    for (int32_t p = 0; p < npos; ++p)
-                        if (gq[p + 1] - gq[gg.back()] > kWG || p - gg.back() >= kWG) gg.push_back(p);
-                    gg.push_back(npos);
-                    D.nggrp = (int32_t)gg.size() - 1;
+                    // [p0, p1) pairs of consecutive positions within the bound;
+                    // a big position closes the open range
+                    std::vector<int32_t> gg, gbig;
+                    int32_t p0 = -1;
+                    for (int32_t p = 0; p < npos; ++p) {
+                        const bool isbig = big > 0 && gq[p + 1] - gq[p] > big;
+                        if (p0 >= 0 && (isbig || gq[p + 1] - gq[p0] > kWG || p - p0 >= kWG)) {
+                            gg.push_back(p0);
+                            gg.push_back(p);
+                            p0 = -1;
+                        }
+                        if (isbig)
+                            gbig.push_back(p);
+                        else if (p0 < 0)
+                            p0 = p;
+                    }
+                    if (p0 >= 0) {
+                        gg.push_back(p0);
+                        gg.push_back(npos);
+                    }
+                    D.nggrp = (int32_t)gg.size() / 2;
                     put_i(D.ggrp, gg);
+                    D.nbig = (int32_t)gbig.size();
+                    put_i(D.gbig, gbig);
                 }
             }
         }
@@ -1644,6 +1924,13 @@ bool amg_build(mof_mesh *m) {
     return true;
 }
 
+// the smoothed level-0 Galerkin product by system slab (k_a_slab, k_galerkin_sys);
+// MOF_GAL0_SYS=0 or MOF_SA_GAL_BF16: the per-position k_galerkin0_ns
+static bool gal0_sys() {
+    const char *e = std::getenv("MOF_GAL0_SYS");
+    return !(e && *e && std::atoi(e) == 0) && !std::getenv("MOF_SA_GAL_BF16");
+}
+
 void amg_ensure(mof_mesh *m, int32_t B) {
     AmgDevice &G = *m->amg;
     if (G.cap >= B) return;
@@ -1657,9 +1944,13 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
             G.A0h.alloc((size_t)(2 * m->pat.sell_nb() * B));  // 8 B per block
             G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
+            if (D.smoothed && gal0_sys() && G.aslab.n == 0) G.aslab.alloc((size_t)4 * kSlab * m->pat.sell_nb());
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
+            const char *g1 = std::getenv("MOF_GAL1_SYS");
+            if (l == 1 && G.aslab.n > 0 && G.lv.size() >= 3 && D.slab.n == 0 && !(g1 && *g1 && std::atoi(g1) == 0))
+                D.slab.alloc((size_t)kB3 * kSlab * D.sell_nb);
             if (l + 1 < G.lv.size()) {  // sweep copy, st_a9 (the coarsest stays fp32)
                 D.Ah.alloc(kAhWords * D.sell_nb * B);
                 D.Ah.zero(s);
@@ -1719,11 +2010,39 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
     // more than ~32k entry groups) takes the per-position kernel -- the same
     // terms in the same order, bit-identical (round 4: an unsliced by-entry
     // launch past the bound skipped workgroups)
-    auto ent_fits = [&](const AmgDevLevel &F) {
-        const int64_t G = sys_group((B + kGalENS - 1) / kGalENS, kGrpGal), nq = (B + kGalENS - 1) / kGalENS;
-        return F.nggrp > 0 && 8 * G * ((nq + G - 1) / G) * ((F.nggrp + 7) / 8) * kWG < ((int64_t)1 << 32);
+    auto fits = [&](int32_t nblk, int32_t ns) {
+        const int64_t nq = (B + ns - 1) / ns, G = sys_group((int32_t)nq, kGrpGal);
+        return 8 * G * ((nq + G - 1) / G) * ((nblk + 7) / 8) * kWG < ((int64_t)1 << 32);
     };
-    for (size_t l = 0; l + 1 < L; ++l) {
+    auto ent_fits = [&](const AmgDevLevel &F) {
+        return (F.nggrp > 0 || F.nbig > 0) && fits(F.nggrp, kGalENS) && fits(F.nbig, kGalBigNS);
+    };
+    // a smoothed level 0: its product, and level 1's when level 1 kept a
+    // slab copy, by system slab (k_a_slab -> k_galerkin_sys<2> -> <3>)
+    size_t l_first = 0;
+    if (G.lv[0].smoothed && G.aslab.n > 0) {
+        AmgDevLevel &F = G.lv[0], &C = G.lv[1];
+        const bool l1 = L >= 3 && C.slab.n > 0;
+        const int64_t fnb = m->pat.sell_nb();
+        auto sys_grid = [](int64_t nb) { return dim3(xcd_grid((int32_t)((nb + kGalSysPos - 1) / kGalSysPos), 1, 1)); };
+        for (int32_t b0 = 0; b0 < B; b0 += kSlab) {
+            k_a_slab<<<dim3((unsigned)((fnb + kSlabPos - 1) / kSlabPos)), kWG, 0, s>>>(
+                fnb, b0, std::min(kSlab, B - b0), reinterpret_cast<const float4 *>(w.A32.p),
+                reinterpret_cast<float4 *>(G.aslab.p));
+            k_galerkin_sys<2><<<sys_grid(C.sell_nb), kWG, 0, s>>>(
+                C.sell_nb, C.n, B, b0, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
+                reinterpret_cast<const float4 *>(G.aslab.p), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
+                l1 ? reinterpret_cast<float4 *>(C.slab.p) : nullptr);
+            if (l1) {
+                AmgDevLevel &C2 = G.lv[2];
+                k_galerkin_sys<3><<<sys_grid(C2.sell_nb), kWG, 0, s>>>(
+                    C2.sell_nb, C2.n, B, b0, C2.sell_row.p, C2.diag_pos.p, C2.dead.p, C.gptr.p, C.gent.p, C.Q.p,
+                    reinterpret_cast<const float4 *>(C.slab.p), C2.A.p, dh(C2), C2.Dh22.p, ah(C2), ah22(C2), nullptr);
+            }
+        }
+        l_first = l1 ? 2 : 1;
+    }
+    for (size_t l = l_first; l + 1 < L; ++l) {
         AmgDevLevel &F = G.lv[l], &C = G.lv[l + 1];
         const bool ent = ent_fits(F);
         if (l == 0 && ent)
@@ -1739,11 +2058,17 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                           F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
                                               ? nullptr
                                               : reinterpret_cast<const uint2 *>(G.A0h.p));
-        else if (ent)
-            k_galerkin3_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
-                F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
-                F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
-        else
+        else if (ent) {
+            if (F.nggrp > 0)
+                k_galerkin3_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
+                    F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
+                    F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
+            if (F.nbig > 0)
+                k_galerkin3_big<kGalBigNS>
+                    <<<dim3(xcd_grid(F.nbig, (B + kGalBigNS - 1) / kGalBigNS, kGrpGal)), kWG, 0, s>>>(
+                        F.nbig, F.gbig.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
+                        F.A.p, F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
+        } else
             k_galerkin3_ns<kGal3NS>
                 <<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGal3NS - 1) / kGal3NS, kGrpGal)), kWG,
                    0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,

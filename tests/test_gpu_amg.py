@@ -216,6 +216,39 @@ def test_smoothed_aggregation_irregular_mesh(monkeypatch):
             assert np.abs(out[smooth][0][k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), (smooth, k)
 
 
+def test_slab_galerkin_vs_per_position(monkeypatch):
+    """A smoothed level 0 (random hull, 20k vertices) takes its level-0 and
+    level-1 Galerkin products by system slab (k_a_slab -> k_galerkin_sys,
+    64 systems per wave): the same bits for batches that split the slabs
+    differently (70 = 64 + 6, 33 + 33 + 4), and against the per-position
+    products (MOF_GAL0_SYS=0; fused multiply-adds round differently) the
+    same iteration count within 5 % and V within 1e-6 of each other and of
+    the oracle."""
+    p, t, n, a = _hull(20000, seed=5)
+    T = 71
+    I = synth.travelling_wave(p, T)
+    tk = np.arange(float(T))
+    monkeypatch.delenv("MOF_GAL0_SYS", raising=False)
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=70)
+    V33, _ = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=33)
+    m.close()
+    assert st["failed"] == 0 and st["recovered"] == 0, st
+    assert np.array_equal(V, V33)
+    monkeypatch.setenv("MOF_GAL0_SYS", "0")
+    m = DeviceMesh(p, n, t, a)
+    Vn, sn = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=70)
+    m.close()
+    assert sn["failed"] == 0 and sn["recovered"] == 0, sn
+    assert abs(st["iterations"] - sn["iterations"]) <= 0.05 * sn["iterations"], (st["iterations"], sn["iterations"])
+    scale = max(1.0, np.abs(Vn).max())
+    assert np.abs(V - Vn).max() < VTOL * scale
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    for k in (0, 69):
+        Vo = oracle.worker(k, a2, gw, e, iw, t, list(tk), a, 0.01, I[k], I[k + 1])
+        assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
+
+
 @pytest.mark.parametrize("case", ["G1_ico642", "G2_cap641"])
 def test_galerkin_by_entry_bit_identical(case, monkeypatch):
     """The level-0 Galerkin product by gather entry (k_galerkin0_ent, the
@@ -240,21 +273,28 @@ def test_coarse_galerkin_by_entry_bit_identical(monkeypatch):
     """Levels >= 1 by gather entry (k_galerkin3_ent, round 4) against the
     per-position product (MOF_GAL3_ENT=0, k_galerkin3_ns): the same terms in
     the same order, the same bits, on a mesh with two coarse products
-    (10,242 -> ~1.3k -> ~170 nodes), ragged system groups."""
+    (10,242 -> ~1.3k -> ~170 nodes), ragged system groups. MOF_GAL_BIG=16
+    sends every position past 16 entries to k_galerkin3_big (chunked
+    lists, one summing lane per system and block entry): the same bits."""
     p, t = synth.icosphere(32, jitter=0.005)
     n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
     I = synth.travelling_wave(p, 12)
     tk = np.arange(12, dtype=np.float64)
     out = []
-    for ent in ("1", "0"):
+    for ent, big in (("1", None), ("1", "16"), ("0", None)):
         monkeypatch.setenv("MOF_GAL3_ENT", ent)
+        if big is None:
+            monkeypatch.delenv("MOF_GAL_BIG", raising=False)
+        else:
+            monkeypatch.setenv("MOF_GAL_BIG", big)
         m = DeviceMesh(p, n, t, a)
         V, st = m.solve_range(I, tk, 0, 11, 0.01, precision="mixed", precond="amg", batch=7)
         assert st["failed"] == 0 and st["recovered"] == 0
         out.append((V, st["iterations"]))
         m.close()
-    assert out[0][1] == out[1][1]
-    assert np.array_equal(out[0][0], out[1][0])
+    for o in out[1:]:
+        assert o[1] == out[0][1]
+        assert np.array_equal(o[0], out[0][0])
 
 
 def test_open_patch_batch_split_bit_identical():
