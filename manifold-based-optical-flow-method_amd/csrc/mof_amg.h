@@ -121,6 +121,7 @@ struct AmgDevLevel {
     int32_t nbig = 0;
     bool smoothed = false;                          // level 0: smoothed prolongator
     DevArray<int32_t> pptr, pcol, rptr, rent;
+    DevArray<int32_t> rperm;                        // smoothed P: restriction group entries by fine node
     int32_t ngrp = 0, nggrp = 0;
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap

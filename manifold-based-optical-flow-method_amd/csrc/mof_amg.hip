@@ -928,6 +928,7 @@ struct Lvl {
     const float *Q, *Qm;                 // tentative rows (node order / member order), or P blocks
     const int32_t *pptr, *pcol;          // smoothed P: row blocks of each fine node
     const int32_t *rptr, *rent;          // smoothed P: {fine node, P block} per coarse node
+    const int32_t *rperm;                // smoothed P: each restriction group's entries by fine node
 };
 
 // 3x3 bf16 block stored as 8 entries in 16 B + entry (2,2) in 2 B
@@ -1198,6 +1199,10 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 // 256-entry groups stay at 1347 us (profiles/r04_ab/sa_xfer/call38/); two
 // list entries per thread and pass with their loads in flight together
 // 1347 -> 1300 us (call42/).
+// Round 5: the entry pass in fine-node order within each group (rperm;
+// the per-node sums keep list order, same bits): S1 (1536 systems) 1653 ->
+// 1445 us per launch, the level-1 restriction 533 -> 439 us, S1 +0.9 %
+// (profiles/r05_ab/restr_sort/).
 // (The tentative k_restrict by (aggregate, system): 397 -> 448 us at C3,
 // and with two members per thread and pass: 360 vs 360 us (call43/); neither
 // kept.)
@@ -1244,21 +1249,25 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
                 c3[t][c] = v;
             }
     };
-    // two entries per thread and pass, both entries' loads in flight together
-    for (int32_t e = e0 + threadIdx.x; e < e1 && !big; e += 2 * kWG) {
-        const bool two = e + kWG < e1;
+    // two entries per thread and pass, both entries' loads in flight together;
+    // the entries visited in fine-node order (rperm: adjacent lanes gather
+    // adjacent r), each staged at its list slot
+    for (int32_t q = e0 + threadIdx.x; q < e1 && !big; q += 2 * kWG) {
+        const bool two = q + kWG < e1;
+        const int32_t ea = F.rperm ? F.rperm[q] : q;
+        const int32_t eb = two ? (F.rperm ? F.rperm[q + kWG] : q + kWG) : ea;
         float c3[2][kNSR][3];
-        contrib(e, c3[0]);
-        contrib(two ? e + kWG : e, c3[1]);
+        contrib(ea, c3[0]);
+        contrib(eb, c3[1]);
 #pragma unroll
         for (int t = 0; t < kNSR; ++t)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) con[t][c][e - e0] = c3[0][t][c];
+            for (int c = 0; c < 3; ++c) con[t][c][ea - e0] = c3[0][t][c];
         if (two)
 #pragma unroll
             for (int t = 0; t < kNSR; ++t)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) con[t][c][e + kWG - e0] = c3[1][t][c];
+                for (int c = 0; c < 3; ++c) con[t][c][eb - e0] = c3[1][t][c];
     }
     __syncthreads();
     // one thread per (coarse node, system), nodes adjacent across threads:
@@ -1864,6 +1873,19 @@ bool amg_build(mof_mesh *m) {
             grp.push_back(na);
             D.ngrp = (int32_t)grp.size() - 1;
             put_i(D.rgrp, grp);
+            // smoothed P: each group's list entries by fine node (stable), for
+            // k_restrict0_sa's gathers; MOF_RESTR_SORT=0: list order
+            const char *rs = std::getenv("MOF_RESTR_SORT");
+            if (L.smoothed && !(rs && *rs && std::atoi(rs) == 0)) {
+                std::vector<int32_t> perm(L.rent.size() / 2);
+                for (int32_t g = 0; g + 1 < (int32_t)grp.size(); ++g) {
+                    const int32_t e0 = L.rptr[grp[g]], e1 = L.rptr[grp[g + 1]];
+                    for (int32_t e = e0; e < e1; ++e) perm[e] = e;
+                    std::stable_sort(perm.begin() + e0, perm.begin() + e1,
+                                     [&](int32_t x, int32_t y) { return L.rent[2 * x] < L.rent[2 * y]; });
+                }
+                put_i(D.rperm, perm);
+            }
             // tentative P (every level but a smoothed level 0): coarse position
             // ranges of <= kWG gather entries and positions for the products by
             // entry, k_galerkin0_ent / k_galerkin3_ent (unless a single
@@ -2105,6 +2127,7 @@ Lvl level_view(const AmgDevLevel &D) {
     v.pcol = D.pcol.p;
     v.rptr = D.rptr.p;
     v.rent = D.rent.p;
+    v.rperm = D.rperm.n > 0 ? D.rperm.p : nullptr;
     return v;
 }
 

@@ -249,6 +249,29 @@ def test_slab_galerkin_vs_per_position(monkeypatch):
         assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
 
 
+def test_restriction_entry_order_bit_identical(monkeypatch):
+    """The smoothed-P restriction forms its list entries' terms in fine-node
+    order (rperm) but sums each coarse node's terms in list order: the same
+    bits as the list-order pass (MOF_RESTR_SORT=0)."""
+    p, t, n, a = _hull(20000, seed=7)
+    T = 9
+    I = synth.travelling_wave(p, T)
+    tk = np.arange(float(T))
+    out = []
+    for srt in (None, "0"):
+        if srt is None:
+            monkeypatch.delenv("MOF_RESTR_SORT", raising=False)
+        else:
+            monkeypatch.setenv("MOF_RESTR_SORT", srt)
+        m = DeviceMesh(p, n, t, a)
+        V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=8)
+        m.close()
+        assert st["failed"] == 0 and st["recovered"] == 0, st
+        out.append((V, st["iterations"]))
+    assert out[0][1] == out[1][1]
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 @pytest.mark.parametrize("case", ["G1_ico642", "G2_cap641"])
 def test_galerkin_by_entry_bit_identical(case, monkeypatch):
     """The level-0 Galerkin product by gather entry (k_galerkin0_ent, the
