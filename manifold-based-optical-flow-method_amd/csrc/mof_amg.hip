@@ -1820,6 +1820,8 @@ bool amg_build(mof_mesh *m) {
     // MOF_AMG_W=1 forces it.
     G.wcycle = false;
     if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
+    G.nu1 = 1;
+    if (const char *v = std::getenv("MOF_AMG_NU1")) G.nu1 = std::max(1, std::min(4, std::atoi(v)));
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
@@ -2148,9 +2150,19 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     // the cycle below level 0 from level 1's restricted b and pre-smoothed
     // x: down (residual, restriction + next pre-smooth), the fused tiny
     // levels, up (prolongation, post-smoothing into y)
-    auto coarse = [&](const Lvl (&u)[kMaxLevels]) {
+    // G.nu1 sweeps per side on the separate levels >= 1: the extra ones are
+    // k_post3 sweeps (y = x + w D^-1 (b - A x)) with x and y swapped after
+    // each, so the level's view always names its latest iterate x / result y
+    // (nu1 pre- and nu1 post-sweeps of the symmetric smoother: the cycle
+    // stays symmetric)
+    const int32_t nu1 = G.wcycle ? 1 : G.nu1;
+    auto coarse = [&](Lvl (&u)[kMaxLevels]) {
         for (int32_t l = 1; l < S; ++l) {
             const int32_t smooth = l + 1 < L - 1;
+            for (int32_t k = 1; k < nu1; ++k) {
+                k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+                std::swap(u[l].x, u[l].y);
+            }
             k_res3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], sysi);
             if (G.lv[l].smoothed)
                 k_restrict0_sa<3><<<dim3(xcd_grid(G.lv[l].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
@@ -2176,6 +2188,10 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
             else
                 k_prolong<3><<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
             k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+            for (int32_t k = 1; k < nu1; ++k) {
+                std::swap(u[l].x, u[l].y);
+                k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+            }
         }
     };
     // down at level 0: residual of the pre-smoothed x, restriction (+ level

@@ -391,7 +391,7 @@ def vcycle(levels, l, b, opts):
         if not hasattr(L, "Aq"):
             L.Aq = quantize(L.A, L.bs, int(qf))
         Aw = L.Aq
-    nu = int(opts.get("nu1", 1)) if l >= 1 else 1
+    nu = int(opts.get("nu1", 1)) if l >= 1 else int(opts.get("nu0", 1))  # sweeps per side
     x = L.om * bsr_apply(L.Dinv, b, L.bs)
     for _ in range(nu - 1):
         x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
