@@ -189,6 +189,36 @@ def test_dd_amg_fewer_iterations_deterministic():
 
 
 @pytest.mark.gpu
+def test_dd_amg_irregular_mesh_vs_smoothed_single_domain():
+    """A random hull (valence 3-14) over 3 RCB parts: the parts keep the
+    tentative prolongator (amg_build smooths only a whole mesh, nown < 0:
+    MOF_AMG_VERBOSE shows no "smoothed P" part level), the single domain
+    smooths levels 0 and 1 (slab Galerkin, chunked coarse product, sorted
+    restriction): two different preconditioners, V within 1e-6 of each
+    other and of the oracle; the decomposed solve has the same bits for
+    another batch size."""
+    p, t = synth.random_sphere(20000, 10.0, seed=11)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    T = 9
+    I = synth.travelling_wave(p, T)
+    tk = np.arange(float(T))
+    d = DecomposedMesh(p, n, t, a, 3)
+    V1, s1 = d.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=8)
+    V2, _ = d.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=5)
+    d.close()
+    assert s1["failed"] == s1["recovered"] == 0 and s1["max_rel_residual"] <= 1e-8
+    assert np.array_equal(V1, V2)
+    ref = DeviceMesh(p, n, t, a)
+    V0, s0 = ref.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg")
+    ref.close()
+    scale = max(1.0, np.abs(V0).max())
+    assert np.abs(V1 - V0).max() <= VTOL * scale
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    Vo = oracle.worker(4, a2, gw, e, iw, t, list(tk), a, 0.01, I[4], I[5])
+    assert np.abs(V1[4] - Vo).max() <= VTOL * scale
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
 @pytest.mark.parametrize("precond", ["jacobi", "amg"])
 def test_dd_full_size_c3(precond):
