@@ -475,6 +475,27 @@ __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
     red_pq_sys<V>(a, slot, blockIdx.x);
 }
 
+// One workgroup per system, between the update and the V-cycle: |r|^2 of the
+// update's partials (the same records and reduction as k_red_rzrr's, so the
+// same bits as the next SpMV's test) against the tolerance; a converged
+// system gets SI_CONV = it + 1 now, the value that SpMV would write, and the
+// V-cycle's kernels skip it -- its z was never used: the next SpMV only
+// applies the deferred x update (round 5: one V-cycle per system and inner
+// solve saved, and the batch's last iteration is an SpMV launch alone: C3
+// 3689 -> 3845 / 3876, S1 1080 -> 1121, F3 2485 -> 2582 timesteps/s, same
+// bits; profiles/r05_ab/conv_early/).
+template <typename V>
+__global__ __launch_bounds__(kWG) void k_pcg_conv_early(PcgArgs<V> a, int32_t it) {
+    __shared__ double lds[2 * (kWG / 64)];
+    const int32_t b = blockIdx.x;
+    int32_t *si = a.sysi + b * kSysStride;
+    if (!si[SI_ACTIVE] || si[SI_CONV] >= 0 || si[SI_FAILED]) return;
+    const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
+    double v[2];
+    reduce_sys<2, kWG>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, v, lds);
+    if (threadIdx.x == 0 && v[1] <= a.sysd[b * kSysStride + SD_TOL2]) si[SI_CONV] = it + 1;
+}
+
 // One workgroup per system: tolerance from |rhs|^2, reset the convergence word.
 // outer_rtol > 0 (refinement steps after the first): each system's inner
 // tolerance is what its own outer residual still needs, 0.3 rtol |f| / |r64|,
@@ -1192,6 +1213,9 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
+    // MOF_CONV_EARLY=0: converged systems run their last V-cycle
+    const char *ce = std::getenv("MOF_CONV_EARLY");
+    const bool early = amg && !(ce && *ce && std::atoi(ce) == 0);
     // z = M^-1 r for the external preconditioner, r.z into slot `slot`
     auto precond = [&](int32_t slot) {
         if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s, a.zh != 0);
@@ -1243,6 +1267,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             }
             k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it & 1);
             k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), (unsigned)B), kWG, 0, s>>>(a, it);
+            if (early) k_pcg_conv_early<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it);
             if (amg) precond((it + 1) & 1);
             k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, (it + 1) & 1);
         }
@@ -1267,6 +1292,15 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         if (sp.fail_at_max_iter) k_fail_running<<<dim3((unsigned)((B + 63) / 64)), 64, 0, s>>>(B, it, a.sysi);
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
+    } else if (early) {
+        // systems marked by the last queued iteration (SI_CONV == it) still
+        // owe the deferred x += alpha p of SpMV launch `it`: that launch alone
+        // (every other system is retired in it)
+        bool owe = false;
+        for (int32_t b = 0; b < B && !owe; ++b)
+            owe = was_active[b] && m->h_sysi[b * kSysStride + SI_CONV] == it;
+        if (owe) launch_spmv(a, false, gx, s, it, 0);
+        MOF_HIP(hipGetLastError());
     }
     int64_t total = 0;
     int32_t slowest = 0, slowest_conv = 0;
@@ -1281,9 +1315,11 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     }
     *max_iters = std::max(*max_iters, slowest);
     // the next batch's first chunk: +1 because convergence is seen by the
-    // launch after; only converged systems count (a failed or capped solve
-    // must not queue max_iter launches before the next look at the flags)
-    if (slowest_conv > 0) *hint = std::min(slowest_conv + 1, kMaxChunk);
+    // launch after (with the early mark, by the iteration itself: the owed
+    // SpMV launch above finishes it); only converged systems count (a failed
+    // or capped solve must not queue max_iter launches before the next look
+    // at the flags)
+    if (slowest_conv > 0) *hint = std::min(slowest_conv + (early ? 0 : 1), kMaxChunk);
     return total;
 }
 

@@ -338,3 +338,34 @@ def test_open_patch_batch_split_bit_identical():
     assert s1["failed"] == 0 and s41["failed"] == 0 and s41["recovered"] == 0
     assert np.array_equal(V1, V17) and np.array_equal(V1, V41)
     assert s1["iterations"] == s41["iterations"]
+
+
+@pytest.mark.parametrize("kind", ["golden", "hull"])
+def test_early_convergence_mark_bit_identical(kind, monkeypatch):
+    """Systems whose |r|^2 after the update already meets the tolerance are
+    marked converged before the V-cycle (k_pcg_conv_early) and skip it: the
+    z it would have made was never used, so V, the iteration counts and the
+    refinement are the same bits as with the last V-cycle run
+    (MOF_CONV_EARLY=0)."""
+    if kind == "golden":
+        g = load_golden("G1_ico642")
+        p, n, t, a = g["coordinates"], g["normals"], g["triangles"], g["areas"]
+        I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    else:
+        p, t, n, a = _hull(20000, seed=9)
+        I = synth.travelling_wave(p, 9)
+        tk, lam = np.arange(9.0), 0.01
+    T = len(I)
+    out = []
+    for ce in (None, "0"):
+        if ce is None:
+            monkeypatch.delenv("MOF_CONV_EARLY", raising=False)
+        else:
+            monkeypatch.setenv("MOF_CONV_EARLY", ce)
+        m = DeviceMesh(p, n, t, a)
+        V, st = m.solve_range(I, tk, 0, T - 1, lam, precision="mixed", precond="amg", batch=5)
+        m.close()
+        assert st["failed"] == 0 and st["recovered"] == 0, st
+        out.append((V, st["iterations"], st["max_rel_residual"]))
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+    assert np.array_equal(out[0][0], out[1][0])
