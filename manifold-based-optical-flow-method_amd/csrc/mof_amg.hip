@@ -929,6 +929,7 @@ struct Lvl {
     const int32_t *pptr, *pcol;          // smoothed P: row blocks of each fine node
     const int32_t *rptr, *rent;          // smoothed P: {fine node, P block} per coarse node
     const int32_t *rperm;                // smoothed P: each restriction group's entries by fine node
+    SysMap sm;                           // the systems the cycle's launches cover (amg_vcycle)
 };
 
 // 3x3 bf16 block stored as 8 entries in 16 B + entry (2,2) in 2 B
@@ -1097,7 +1098,7 @@ __device__ __forceinline__ void post3_node(const Lvl &L, int32_t b, int32_t i, f
 }
 
 __global__ __launch_bounds__(kWG) void k_res3(Lvl L, const int32_t *__restrict__ sysi) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = sm_b(L.sm, blockIdx.y);
     if (i >= L.n || retired(sysi, b)) return;
     res3_node(L, b, i);
 }
@@ -1123,24 +1124,25 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
 #pragma clang fp contract(off)
     __shared__ float con[NS][3][kRG];
     int32_t g, bq;
-    if (!xcd_map(ngrp, (B + NS - 1) / NS, g, bq, kGrpRestr)) return;
+    if (!xcd_map(ngrp, (F.sm.n + NS - 1) / NS, g, bq, kGrpRestr)) return;
     const int32_t b0 = bq * NS;
     bool any = false;
 #pragma unroll
-    for (int t = 0; t < NS; ++t) any |= b0 + t < B && !retired(sysi, b0 + t);
+    for (int t = 0; t < NS; ++t) any |= b0 + t < F.sm.n && !retired(sysi, sm_b(F.sm, b0 + t));
     if (!any) return;
     const int32_t I0 = grp[g], I1 = grp[g + 1];
     const int32_t q0 = F.mptr[I0], q1 = F.mptr[I1];
     if (q1 - q0 > kRG) {  // one oversized aggregate
         if (threadIdx.x == 0)
             for (int t = 0; t < NS; ++t)
-                if (b0 + t < B && !retired(sysi, b0 + t)) restrict_node<BSF>(F, C, b0 + t, I0, smooth != 0, omega);
+                if (b0 + t < F.sm.n && !retired(sysi, sm_b(F.sm, b0 + t)))
+                    restrict_node<BSF>(F, C, sm_b(F.sm, b0 + t), I0, smooth != 0, omega);
         return;
     }
     for (int32_t q = q0 + threadIdx.x; q < q1; q += kWG) {
         float ri[NS][BSF];
 #pragma unroll
-        for (int t = 0; t < NS; ++t) ldr<BSF>(F.r, min(b0 + t, B - 1), F.n, r_at<BSF>(F, q), ri[t]);
+        for (int t = 0; t < NS; ++t) ldr<BSF>(F.r, sm_b(F.sm, b0 + t), F.n, r_at<BSF>(F, q), ri[t]);
         const float *qm = F.Qm + (int64_t)q * BSF * 3;
         float qv[BSF * 3];
 #pragma unroll
@@ -1166,8 +1168,9 @@ __global__ __launch_bounds__(kWG) void k_restrict(Lvl F, Lvl C, const int32_t *_
                 for (int c = 0; c < 3; ++c) acc[t][c] += con[t][c][q - q0];
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
-            const int32_t b = b0 + t;
-            if (b >= B || retired(sysi, b)) continue;
+            if (b0 + t >= F.sm.n) continue;
+            const int32_t b = sm_b(F.sm, b0 + t);
+            if (retired(sysi, b)) continue;
             const int64_t vo = (int64_t)b * C.n * 4;
             stv<3>(C.b + vo, I, acc[t]);
             if (smooth) {
@@ -1221,12 +1224,12 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
 #pragma clang fp contract(off)
     __shared__ float con[kNSR][3][kRGS];
     int32_t g, bq;
-    const int32_t nq = (B + kNSR - 1) / kNSR;
+    const int32_t nq = (F.sm.n + kNSR - 1) / kNSR;
     if (!xcd_map(ngrp, nq, g, bq, kGrpRestr)) return;
     const int32_t b0 = bq * kNSR;
     bool any = false;
 #pragma unroll
-    for (int t = 0; t < kNSR; ++t) any |= b0 + t < B && !retired(sysi, b0 + t);
+    for (int t = 0; t < kNSR; ++t) any |= b0 + t < F.sm.n && !retired(sysi, sm_b(F.sm, b0 + t));
     if (!any) return;
     const int32_t I0 = grp[g], I1 = grp[g + 1];
     const int32_t e0 = F.rptr[I0], e1 = F.rptr[I1];
@@ -1239,7 +1242,7 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
         for (int k = 0; k < BSF * 3; ++k) pm[k] = p[k];
         float ri[kNSR][BSF];
 #pragma unroll
-        for (int t = 0; t < kNSR; ++t) ldr<BSF>(F.r, min(b0 + t, B - 1), F.n, i, ri[t]);
+        for (int t = 0; t < kNSR; ++t) ldr<BSF>(F.r, sm_b(F.sm, b0 + t), F.n, i, ri[t]);
 #pragma unroll
         for (int t = 0; t < kNSR; ++t)
 #pragma unroll
@@ -1275,8 +1278,10 @@ __global__ __launch_bounds__(kWG) void k_restrict0_sa(Lvl F, Lvl C, const int32_
     // entries in list order (the same per-system sums, bit for bit)
     const int32_t nI = I1 - I0;
     for (int32_t q = threadIdx.x; q < nI * kNSR; q += kWG) {
-        const int32_t t = q / nI, I = I0 + q - t * nI, b = b0 + t;
-        if (b >= B || retired(sysi, b)) continue;
+        const int32_t t = q / nI, I = I0 + q - t * nI;
+        if (b0 + t >= F.sm.n) continue;
+        const int32_t b = sm_b(F.sm, b0 + t);
+        if (retired(sysi, b)) continue;
         float acc[3] = {};
         for (int32_t e = F.rptr[I]; e < F.rptr[I + 1]; ++e) {
             float c3[3];
@@ -1314,7 +1319,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     // (a system's bits must not depend on its slot, i.e. on the batch split)
 #pragma clang fp contract(off)
     int32_t rb, bq;
-    const int32_t nq = (B + kNSP - 1) / kNSP;
+    const int32_t nq = (F.sm.n + kNSP - 1) / kNSP;
     if (!xcd_map(nblk, nq, rb, bq, kGrpProl)) return;
     const int32_t b0 = bq * kNSP;
     const int32_t i = rb * kWG + threadIdx.x;
@@ -1322,7 +1327,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     float x[kNSP][2];
 #pragma unroll
     for (int t = 0; t < kNSP; ++t) {
-        const float2 v = ld_x0(F.x, (int64_t)min(b0 + t, B - 1) * F.n + i);
+        const float2 v = ld_x0(F.x, (int64_t)sm_b(F.sm, b0 + t) * F.n + i);
         x[t][0] = v.x;
         x[t][1] = v.y;
     }
@@ -1335,7 +1340,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
         for (int c = 0; c < 6; ++c) qm[c] = q[c];
         float y[kNSP][3];
 #pragma unroll
-        for (int t = 0; t < kNSP; ++t) ldv<3>(C.y + (int64_t)min(b0 + t, B - 1) * C.n * 4, K, y[t]);
+        for (int t = 0; t < kNSP; ++t) ldv<3>(C.y + (int64_t)sm_b(F.sm, b0 + t) * C.n * 4, K, y[t]);
 #pragma unroll
         for (int t = 0; t < kNSP; ++t) {
             x[t][0] += qm[0] * y[t][0] + qm[1] * y[t][1] + qm[2] * y[t][2];
@@ -1344,8 +1349,9 @@ __global__ __launch_bounds__(kWG) void k_prolong0_sa(Lvl F, Lvl C, int32_t nblk,
     }
 #pragma unroll
     for (int t = 0; t < kNSP; ++t) {
-        const int32_t b = b0 + t;
-        if (b >= B || retired(sysi, b)) continue;
+        if (b0 + t >= F.sm.n) continue;
+        const int32_t b = sm_b(F.sm, b0 + t);
+        if (retired(sysi, b)) continue;
         if constexpr (XM == 2)  // full-precision x for the post-smoothing
             reinterpret_cast<float2 *>(F.y)[(int64_t)b * F.n + i] = make_float2(x[t][0], x[t][1]);
         else
@@ -1362,13 +1368,13 @@ __global__ __launch_bounds__(kWG) void k_prolong3_sa(Lvl F, Lvl C, int32_t nblk,
                                                      const int32_t *__restrict__ sysi) {
 #pragma clang fp contract(off)
     int32_t rb, bq;
-    if (!xcd_map(nblk, (B + kNS3 - 1) / kNS3, rb, bq, kGrpProl)) return;
+    if (!xcd_map(nblk, (F.sm.n + kNS3 - 1) / kNS3, rb, bq, kGrpProl)) return;
     const int32_t i = rb * kWG + threadIdx.x;
     if (i >= F.n) return;
     const int32_t b0 = bq * kNS3;
     float x[kNS3][3];
 #pragma unroll
-    for (int t = 0; t < kNS3; ++t) ldv<3>(F.x + (int64_t)min(b0 + t, B - 1) * F.n * 4, i, x[t]);
+    for (int t = 0; t < kNS3; ++t) ldv<3>(F.x + (int64_t)sm_b(F.sm, b0 + t) * F.n * 4, i, x[t]);
     for (int32_t k = F.pptr[i]; k < F.pptr[i + 1]; ++k) {
         const float *p = F.Q + (int64_t)k * 9;
         float pm[9];
@@ -1377,7 +1383,7 @@ __global__ __launch_bounds__(kWG) void k_prolong3_sa(Lvl F, Lvl C, int32_t nblk,
         const int32_t K = F.pcol[k];
         float y[kNS3][3];
 #pragma unroll
-        for (int t = 0; t < kNS3; ++t) ldv<3>(C.y + (int64_t)min(b0 + t, B - 1) * C.n * 4, K, y[t]);
+        for (int t = 0; t < kNS3; ++t) ldv<3>(C.y + (int64_t)sm_b(F.sm, b0 + t) * C.n * 4, K, y[t]);
 #pragma unroll
         for (int t = 0; t < kNS3; ++t)
 #pragma unroll
@@ -1385,15 +1391,16 @@ __global__ __launch_bounds__(kWG) void k_prolong3_sa(Lvl F, Lvl C, int32_t nblk,
     }
 #pragma unroll
     for (int t = 0; t < kNS3; ++t) {
-        const int32_t b = b0 + t;
-        if (b >= B || retired(sysi, b)) continue;
+        if (b0 + t >= F.sm.n) continue;
+        const int32_t b = sm_b(F.sm, b0 + t);
+        if (retired(sysi, b)) continue;
         stv<3>(F.x + (int64_t)b * F.n * 4, i, x[t]);
     }
 }
 
 template <int BSF>
 __global__ __launch_bounds__(kWG) void k_prolong(Lvl F, Lvl C, const int32_t *__restrict__ sysi) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = sm_b(F.sm, blockIdx.y);
     if (i >= F.n || retired(sysi, b)) return;
     prolong_node<BSF>(F, C, b, i);
 }
@@ -1414,7 +1421,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, in
     // no fp contraction: every system slot of the unrolled loops rounds alike
 #pragma clang fp contract(off)
     int32_t rb, bq;
-    if (!xcd_map(nblk, (B + kProlS - 1) / kProlS, rb, bq, kGrpProl)) return;
+    if (!xcd_map(nblk, (F.sm.n + kProlS - 1) / kProlS, rb, bq, kGrpProl)) return;
     const int32_t n = F.n;
     int32_t ii[kProlR], ag[kProlR];
     float q[kProlR][6];
@@ -1430,7 +1437,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, in
     float y[kProlS][kProlR][3];
 #pragma unroll
     for (int t = 0; t < kProlS; ++t) {
-        const int32_t b = min(bq * kProlS + t, B - 1);
+        const int32_t b = sm_b(F.sm, bq * kProlS + t);
         const float *yb = C.y + (int64_t)b * C.n * 4;
 #pragma unroll
         for (int r = 0; r < kProlR; ++r) {
@@ -1440,8 +1447,9 @@ __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, in
     }
 #pragma unroll
     for (int t = 0; t < kProlS; ++t) {
-        const int32_t b = bq * kProlS + t;
-        if (b >= B || retired(sysi, b)) continue;
+        if (bq * kProlS + t >= F.sm.n) continue;
+        const int32_t b = sm_b(F.sm, bq * kProlS + t);
+        if (retired(sysi, b)) continue;
         const int64_t vb = (int64_t)b * n;
 #pragma unroll
         for (int r = 0; r < kProlR; ++r) {
@@ -1459,7 +1467,7 @@ __global__ __launch_bounds__(kWG) void k_prolong0(Lvl F, Lvl C, int32_t nblk, in
 }
 
 __global__ __launch_bounds__(kWG) void k_post3(Lvl L, float omega, const int32_t *__restrict__ sysi) {
-    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = blockIdx.y;
+    const int32_t i = blockIdx.x * kWG + threadIdx.x, b = sm_b(L.sm, blockIdx.y);
     if (i >= L.n || retired(sysi, b)) return;
     post3_node(L, b, i, omega);
 }
@@ -1482,7 +1490,7 @@ struct SubArgs {
 };
 
 __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
-    const int32_t b = blockIdx.x;
+    const int32_t b = sm_b(a.lv[0].sm, blockIdx.x);
     if (retired(a.sysi, b)) return;
     const int32_t tid = threadIdx.x;
     // down: level first already holds b and the pre-smoothed x
@@ -1547,21 +1555,21 @@ __global__ __launch_bounds__(kSubWG) void k_subcycle(SubArgs a) {
 // -> 829 us per 512-system launch at NS = 2; 4 lowered the occupancy).
 constexpr int kRes0NS = 2, kRes0U = kSweepU;
 template <int NS>
-__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
+__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t nblk, int32_t B, SysMap sm, MatH mat,
                                                  const float *__restrict__ rv, const float *__restrict__ xv,
                                                  const int32_t *__restrict__ apos,
                                                  const int32_t *__restrict__ sysi, float *__restrict__ r1) {
 #pragma clang fp contract(off)
     int32_t rb, bq;
-    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpSmooth > NS ? kGrpSmooth / NS : 1)) return;
+    if (!xcd_map(nblk, (sm.n + NS - 1) / NS, rb, bq, kGrpSmooth > NS ? kGrpSmooth / NS : 1)) return;
     int32_t bs[NS];
     bool act[NS];
     bool any = false;
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
-        const int32_t b = bq * NS + t;
-        bs[t] = min(b, B - 1);
-        act[t] = b < B && !retired(sysi, b);
+        const int32_t l = bq * NS + t;
+        bs[t] = sm_b(sm, l);
+        act[t] = l < sm.n && !retired(sysi, bs[t]);
         any |= act[t];
     }
     if (!any) return;
@@ -1592,7 +1600,7 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_res0_ns(int32_t N, int32_t 
 // launch; 8 slots per batch 1030 us). D^-1 from the row's own diagonal block.
 constexpr int kPost0NS = 2, kPost0U = 4;
 template <int XM, bool ZH, int NS>
-__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t nblk, int32_t B, MatH mat,
+__global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t nblk, int32_t B, SysMap sm, MatH mat,
                                                   const float *__restrict__ rv,
                                                   const float *__restrict__ xv, float omega,
                                                   const int32_t *__restrict__ sysi,
@@ -1601,15 +1609,15 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t
 #pragma clang fp contract(off)
     __shared__ double lds[8 * NS];
     int32_t rb, bq;
-    if (!xcd_map(nblk, (B + NS - 1) / NS, rb, bq, kGrpSmooth > NS ? kGrpSmooth / NS : 1)) return;
+    if (!xcd_map(nblk, (sm.n + NS - 1) / NS, rb, bq, kGrpSmooth > NS ? kGrpSmooth / NS : 1)) return;
     int32_t bs[NS];
     bool act[NS];
     bool any = false;
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
-        const int32_t b = bq * NS + t;
-        bs[t] = min(b, B - 1);
-        act[t] = b < B && !retired(sysi, b);
+        const int32_t l = bq * NS + t;
+        bs[t] = sm_b(sm, l);
+        act[t] = l < sm.n && !retired(sysi, bs[t]);
         any |= act[t];
     }
     if (!any) return;
@@ -2134,7 +2142,7 @@ Lvl level_view(const AmgDevLevel &D) {
 }
 
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part_slot, int32_t nblk,
-                const RedArgs &rd, hipStream_t s, bool zh) {
+                const RedArgs &rd, hipStream_t s, bool zh, const int32_t *smap, int32_t nl) {
     AmgDevice &G = *m->amg;
     Workspace &w = m->ws;
     const int32_t L = (int32_t)G.lv.size();
@@ -2143,7 +2151,13 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     const float om1 = G.omega1;  // levels >= 1
     const MatH mat0 = level0_mat(m);
     Lvl v[kMaxLevels];
-    for (int32_t l = 0; l < L; ++l) v[l] = level_view(G.lv[l]);
+    // the launches cover nL systems: smap's (the PCG's tail iterations) or all B
+    const int32_t nL = smap ? nl : B;
+    const SysMap sm{smap, nL};
+    for (int32_t l = 0; l < L; ++l) {
+        v[l] = level_view(G.lv[l]);
+        v[l].sm = sm;
+    }
     // levels S.. run fused in k_subcycle
     int32_t S = 1;
     while (S < L - 1 && G.lv[S].n > kSubNodes) ++S;
@@ -2160,15 +2174,15 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         for (int32_t l = 1; l < S; ++l) {
             const int32_t smooth = l + 1 < L - 1;
             for (int32_t k = 1; k < nu1; ++k) {
-                k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+                k_post3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], om1, sysi);
                 std::swap(u[l].x, u[l].y);
             }
-            k_res3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], sysi);
+            k_res3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], sysi);
             if (G.lv[l].smoothed)
-                k_restrict0_sa<3><<<dim3(xcd_grid(G.lv[l].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict0_sa<3><<<dim3(xcd_grid(G.lv[l].ngrp, (nL + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
                     u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
             else
-                k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, B, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict<3><<<dim3(xcd_grid(G.lv[l].ngrp, nL, kGrpRestr)), kWG, 0, s>>>(
                     u[l], u[l + 1], G.lv[l].rgrp.p, G.lv[l].ngrp, B, smooth, om1, sysi);
         }
         SubArgs sa;
@@ -2178,19 +2192,19 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         sa.cinv = G.cinv.p;
         sa.omega = om1;
         sa.sysi = sysi;
-        k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
+        k_subcycle<<<dim3((unsigned)nL), kSubWG, 0, s>>>(sa);
         for (int32_t l = S - 1; l >= 1; --l) {
             if (G.lv[l].smoothed) {
                 const int32_t nb = (u[l].n + kWG - 1) / kWG;
-                k_prolong3_sa<<<dim3(xcd_grid(nb, (B + kNS3 - 1) / kNS3, kGrpProl)), kWG, 0, s>>>(u[l], u[l + 1], nb,
+                k_prolong3_sa<<<dim3(xcd_grid(nb, (nL + kNS3 - 1) / kNS3, kGrpProl)), kWG, 0, s>>>(u[l], u[l + 1], nb,
                                                                                                    B, sysi);
             }
             else
-                k_prolong<3><<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], u[l + 1], sysi);
-            k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+                k_prolong<3><<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], u[l + 1], sysi);
+            k_post3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], om1, sysi);
             for (int32_t k = 1; k < nu1; ++k) {
                 std::swap(u[l].x, u[l].y);
-                k_post3<<<grid2(u[l].n, B), kWG, 0, s>>>(u[l], om1, sysi);
+                k_post3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], om1, sysi);
             }
         }
     };
@@ -2199,15 +2213,15 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = 0; l < 1; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
-            k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (B + kRes0NS - 1) / kRes0NS,
+            k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (nL + kRes0NS - 1) / kRes0NS,
                                                kGrpSmooth > kRes0NS ? kGrpSmooth / kRes0NS : 1)),
-                                 kWG, 0, s>>>(v[0].n, nblk, B, mat0, r0, v[0].x,
+                                 kWG, 0, s>>>(v[0].n, nblk, B, sm, mat0, r0, v[0].x,
                                               G.lv[0].smoothed ? nullptr : v[0].apos, sysi, v[0].r);
             if (G.lv[0].smoothed) {
-                k_restrict0_sa<2><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict0_sa<2><<<dim3(xcd_grid(G.lv[0].ngrp, (nL + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             } else {
-                k_restrict<2, kRestrS><<<dim3(xcd_grid(G.lv[0].ngrp, (B + kRestrS - 1) / kRestrS, kGrpRestr)), kWG, 0, s>>>(
+                k_restrict<2, kRestrS><<<dim3(xcd_grid(G.lv[0].ngrp, (nL + kRestrS - 1) / kRestrS, kGrpRestr)), kWG, 0, s>>>(
                     v[0], v[1], G.lv[0].rgrp.p, G.lv[0].ngrp, B, smooth, om1, sysi);
             }
         }
@@ -2220,7 +2234,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         sa.cinv = G.cinv.p;
         sa.omega = om1;
         sa.sysi = sysi;
-        k_subcycle<<<dim3((unsigned)B), kSubWG, 0, s>>>(sa);
+        k_subcycle<<<dim3((unsigned)nL), kSubWG, 0, s>>>(sa);
     } else {
         coarse(v);
         if (G.wcycle) {
@@ -2235,25 +2249,25 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         if (l == 0) {
             const int32_t nb0 = (v[0].n + kWG - 1) / kWG;
             const int32_t nb0p = (v[0].n + kWG * kProlR - 1) / (kWG * kProlR);
-            const dim3 gsa(xcd_grid(nb0, (B + kNSP - 1) / kNSP, kGrpProl)), gp(xcd_grid(nb0p, (B + kProlS - 1) / kProlS, kGrpProl));
+            const dim3 gsa(xcd_grid(nb0, (nL + kNSP - 1) / kNSP, kGrpProl)), gp(xcd_grid(nb0p, (nL + kProlS - 1) / kProlS, kGrpProl));
             if (G.xm == 2) {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
-                    launch_post0<2, true>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
+                    launch_post0<2, true>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
                 else
-                    launch_post0<2, false>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
+                    launch_post0<2, false>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
             } else {
                 if (G.lv[0].smoothed)
                     k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
                 if (zh)
-                    launch_post0<1, true>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
+                    launch_post0<1, true>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
                 else
-                    launch_post0<1, false>(nblk, B, s, v[0].n, nblk, B, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
+                    launch_post0<1, false>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
             }
         }
     }

@@ -146,6 +146,7 @@ struct Workspace {
     DevArray<double> sc;               // pre-reduced PCG scalars: r.z, |r|^2 [2][B][2], p.q [2][B]
     DevArray<double> sysd;             // [B][8] per-system scalars
     DevArray<int32_t> sysi;            // [B][8] per-system flags
+    DevArray<int32_t> smap;            // [B] the systems a PCG tail chunk's launches cover (SysMap)
     DevArray<double> dt;               // [B]
     DevArray<double> Ibuf;             // [B][N] I0 rows + [B][N] I1 rows (host-staged)
     DevArray<double> Iint;             // the batch's I rows in internal vertex order ([B+1] or [2B] rows)
@@ -382,8 +383,10 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s);  // Galerkin + coar
 // z = V-cycle(r) on the fp32 inner vectors; writes partial r.z (component 0)
 // into the part_rzrr slot `part_slot`
 // zh: write z as a bf16 pair per vertex (uint32) instead of float2
+// smap / nl: the launches cover the nl systems smap lists (the PCG's tail
+// iterations), or all B when smap is null
 void amg_vcycle(mof_mesh *m, int32_t B, const float *r, float *z, double *part_slot, int32_t nblk,
-                const RedArgs &rd, hipStream_t s, bool zh);
+                const RedArgs &rd, hipStream_t s, bool zh, const int32_t *smap = nullptr, int32_t nl = 0);
 // level-0 smoother data the PCG update / init write the pre-smoothing with
 struct AmgFine {
     const void *A0h;  // bf16 level-0 operator [B][sell_nb] (its diagonal blocks give the smoother's D)

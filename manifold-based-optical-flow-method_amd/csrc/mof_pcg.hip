@@ -94,6 +94,7 @@ struct PcgArgs {
     int32_t zh;            // z stored as bf16 pairs: the multigrid cycle's output on a single
                            // domain with the tentative prolongator (the decomposed path's
                            // halo exchange moves float2 z)
+    SysMap sm;             // the systems the per-iteration launches cover (SysMap)
 };
 
 // The per-system scalars every workgroup of the next launch needs, reduced
@@ -460,7 +461,7 @@ __device__ __forceinline__ void red_rzrr_sys(const PcgArgs<V> &a, int32_t slot, 
 }
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_red_rzrr(PcgArgs<V> a, int32_t slot) {
-    red_rzrr_sys<V>(a, slot, blockIdx.x);
+    red_rzrr_sys<V>(a, slot, sm_b(a.sm, blockIdx.x));
 }
 template <typename V, int NT = kWG>
 __device__ __forceinline__ void red_pq_sys(const PcgArgs<V> &a, int32_t slot, int32_t b) {
@@ -472,7 +473,7 @@ __device__ __forceinline__ void red_pq_sys(const PcgArgs<V> &a, int32_t slot, in
 }
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
-    red_pq_sys<V>(a, slot, blockIdx.x);
+    red_pq_sys<V>(a, slot, sm_b(a.sm, blockIdx.x));
 }
 
 // One workgroup per system, between the update and the V-cycle: |r|^2 of the
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(kWG) void k_red_pq(PcgArgs<V> a, int32_t slot) {
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_conv_early(PcgArgs<V> a, int32_t it) {
     __shared__ double lds[2 * (kWG / 64)];
-    const int32_t b = blockIdx.x;
+    const int32_t b = sm_b(a.sm, blockIdx.x);
     int32_t *si = a.sysi + b * kSysStride;
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0 || si[SI_FAILED]) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
@@ -641,9 +642,9 @@ __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, i
 }
 template <typename V, bool FIRST, bool ZH = false>
 __device__ __forceinline__ void pcg_spmv_body(const PcgArgs<V> &a, int32_t it, int32_t flags) {
-    int32_t rb, b;
-    if (!xcd_map(a.nblk, a.B, rb, b, kGrpSpmv)) return;
-    pcg_spmv_rows<V, FIRST, ZH>(a, it, flags, rb, b);
+    int32_t rb, bl;
+    if (!xcd_map(a.nblk, a.sm.n, rb, bl, kGrpSpmv)) return;
+    pcg_spmv_rows<V, FIRST, ZH>(a, it, flags, rb, sm_b(a.sm, bl));
 }
 
 // Measured and not kept (round 2, profiles/r02_ab/spmvns_*): two systems
@@ -677,7 +678,7 @@ constexpr int spmv_wg() { return kWG; }
 // grid of an SpMV launch over (row block, system) in the XCD order its body maps
 template <typename V>
 dim3 spmv_grid(const PcgArgs<V> &a) {
-    return dim3(xcd_grid(a.nblk, a.B, kGrpSpmv));
+    return dim3(xcd_grid(a.nblk, a.sm.n, kGrpSpmv));
 }
 template <typename V>
 void launch_spmv(const PcgArgs<V> &a, bool first, dim3, hipStream_t s, int32_t it, int32_t flags) {
@@ -806,7 +807,7 @@ __device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it,
 }
 template <typename V>
 __global__ __launch_bounds__(kWG) void k_pcg_update(PcgArgs<V> a, int32_t it) {
-    pcg_update_rows<V>(a, it, blockIdx.x, blockIdx.y);
+    pcg_update_rows<V>(a, it, blockIdx.x, sm_b(a.sm, blockIdx.y));
 }
 
 // x64 (+)= x_inner for systems active in the inner solve, and the block's
@@ -1121,6 +1122,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.N = m->N;
     a.nblk = w.nblk;
     a.B = B;
+    a.sm = sys_all(B);
     a.mat = mat;
     a.dinv = dinv;
     a.x = reinterpret_cast<V *>(w.vx.p);
@@ -1158,6 +1160,17 @@ void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
 
 // Longest first chunk of launches queued before the host looks at the flags.
 constexpr int32_t kMaxChunk = 256;
+// a chunk whose running systems are at most this fraction of the batch
+// launches over them alone (pcg, SysMap). One box, round 5
+// (profiles/r05_ab/compact/): S1 1134 -> 1162 timesteps/s (its third and
+// fourth refinement steps run a few systems each), R3 / C3 / F3 unchanged
+// within noise; 0.5, or no first-chunk split, the same
+constexpr double kCompactFrac = 0.9;
+// pcg's hints: hint[0] the previous batch's slowest convergence, hint[kBulkHint]
+// the iteration by which kBulkFrac of its systems had converged -- the first
+// chunk stops there, so the tail (the slow few) runs compacted
+constexpr int32_t kBulkHint = 48;
+constexpr double kBulkFrac = 0.9;
 
 // Systems of a chunk [it0, it0 + n) each timed SpMV launch processed: system
 // b works in launch it while it < last_b (SI_CONV = the launch that saw it
@@ -1218,15 +1231,11 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     const bool early = amg && !(ce && *ce && std::atoi(ce) == 0);
     // z = M^-1 r for the external preconditioner, r.z into slot `slot`
     auto precond = [&](int32_t slot) {
-        if constexpr (sizeof(V) == 4) amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s, a.zh != 0);
+        if constexpr (sizeof(V) == 4)
+            amg_vcycle(m, B, a.r, a.z, a.part_rzrr + slot * ps, a.nblk, a.red, s, a.zh != 0, a.sm.map, a.sm.n);
     };
     dim3 g((unsigned)m->ws.nblk, (unsigned)B);
     const dim3 gx(xcd_grid(m->ws.nblk, B, kGrpSpmv));
-    k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
-    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol, etol);
-    if (amg) precond(0);
-    k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, 0);
-    MOF_HIP(hipGetLastError());
     // systems active at the start of this solve: the host mirror is current
     // (reset by solve_batch, refreshed by every outer check)
     std::vector<int32_t> was_active(B), running_at(B);
@@ -1236,12 +1245,38 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         solve_systems += was_active[b];
     }
     running_at = was_active;
+    // launches over the running systems only when they are at most
+    // kCompactFrac of the batch (SysMap): a later refinement step's few
+    // systems from the start, a long tail from its chunk boundary;
+    // MOF_COMPACT=0: all B
+    const char *ec = std::getenv("MOF_COMPACT");
+    const bool compact = !(ec && *ec && std::atoi(ec) == 0);
+    std::vector<int32_t> h_map(B);  // read by the async upload until the next fetch_flags
+    if (compact && solve_systems <= kCompactFrac * B) {
+        int32_t n = 0;
+        for (int32_t b = 0; b < B; ++b)
+            if (was_active[b]) h_map[n++] = b;
+        if (n > 0) {
+            MOF_HIP(hipMemcpyAsync(m->ws.smap.p, h_map.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+            a.sm = SysMap{m->ws.smap.p, n};
+        }
+    }
+    k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
+    k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol, etol);
+    if (amg) precond(0);
+    k_red_rzrr<V><<<dim3((unsigned)a.sm.n), kWG, 0, s>>>(a, 0);
+    MOF_HIP(hipGetLastError());
     // The first chunk runs as many iterations as the same solve of the
     // previous batch needed (timesteps of one run converge alike), so the
     // host usually synchronises once per inner solve; converged systems
     // retire on the device, so overshooting costs only early-exit launches.
+    // With a tail (the previous batch's slowest system 2+ iterations past
+    // the bulk of them, kBulkFrac) the first chunk stops at the bulk and the
+    // rest runs compacted, straight to the previous slowest.
     int32_t it = 0;
-    int32_t chunk = *hint > 0 ? std::min(*hint, kMaxChunk) : 8;
+    const int32_t bulk = compact ? hint[kBulkHint] : 0;
+    const bool split = bulk > 0 && *hint >= bulk + 2;
+    int32_t chunk = split ? std::min(bulk, kMaxChunk) : (*hint > 0 ? std::min(*hint, kMaxChunk) : 8);
     bool done = false;
     std::vector<hipEvent_t> &ev = m->spmv_events;
     std::vector<float> ms;
@@ -1265,11 +1300,12 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             } else {
                 launch_spmv(a, it == 0, gx, s, it, 0);
             }
-            k_red_pq<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it & 1);
-            k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), (unsigned)B), kWG, 0, s>>>(a, it);
-            if (early) k_pcg_conv_early<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, it);
+            const unsigned nl = (unsigned)a.sm.n;
+            k_red_pq<V><<<dim3(nl), kWG, 0, s>>>(a, it & 1);
+            k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), nl), kWG, 0, s>>>(a, it);
+            if (early) k_pcg_conv_early<V><<<dim3(nl), kWG, 0, s>>>(a, it);
             if (amg) precond((it + 1) & 1);
-            k_red_rzrr<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, (it + 1) & 1);
+            k_red_rzrr<V><<<dim3(nl), kWG, 0, s>>>(a, (it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);
@@ -1279,12 +1315,23 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             charge_chunk(m, B, running_at, it0, n, sp.precision, solve_systems, ms, timing);
         }
         done = true;
+        int32_t owe_or_run = 0;
         for (int32_t b = 0; b < B; ++b) {
             const int32_t *si = m->h_sysi + b * kSysStride;
             running_at[b] = si[SI_ACTIVE] && !si[SI_FAILED] && si[SI_CONV] < 0;
             if (running_at[b]) done = false;
+            // the next chunk's launches: the running systems and those owed
+            // the deferred x update of SpMV launch `it` (marked early by the
+            // chunk's last iteration)
+            if (was_active[b] && !si[SI_FAILED] && (si[SI_CONV] < 0 || si[SI_CONV] >= it)) h_map[owe_or_run++] = b;
         }
-        chunk = 8;
+        chunk = split && it == std::min(bulk, kMaxChunk) && *hint > it ? std::min(*hint - it, kMaxChunk) : 8;
+        // a tail chunk (at most kCompactFrac of the batch still running)
+        // launches over those systems only; same bits (SysMap)
+        if (!done && compact && owe_or_run <= kCompactFrac * B) {
+            MOF_HIP(hipMemcpyAsync(m->ws.smap.p, h_map.data(), sizeof(int32_t) * owe_or_run, hipMemcpyHostToDevice, s));
+            a.sm = SysMap{m->ws.smap.p, owe_or_run};
+        }
     }
     if (!done) {
         // one more check launch so SI_CONV records systems converged at max_iter
@@ -1304,6 +1351,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     }
     int64_t total = 0;
     int32_t slowest = 0, slowest_conv = 0;
+    std::vector<int32_t> convs;
     for (int32_t b = 0; b < B; ++b) {
         if (!was_active[b]) continue;
         const int32_t *si = m->h_sysi + b * kSysStride;
@@ -1311,7 +1359,15 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         const int32_t its = c >= 0 ? c : (si[SI_FAILED] && si[SI_FAIL_WHY] != FW_MAXITER ? si[SI_FAIL_IT] + 1 : it);
         total += its;
         slowest = std::max(slowest, its);
-        if (c >= 0) slowest_conv = std::max(slowest_conv, c);
+        if (c >= 0) {
+            slowest_conv = std::max(slowest_conv, c);
+            convs.push_back(c);
+        }
+    }
+    if (!convs.empty()) {
+        const size_t k = std::min(convs.size() - 1, (size_t)(kBulkFrac * (double)convs.size()));
+        std::nth_element(convs.begin(), convs.begin() + k, convs.end());
+        hint[kBulkHint] = convs[k];
     }
     *max_iters = std::max(*max_iters, slowest);
     // the next batch's first chunk: +1 because convergence is seen by the
@@ -1512,6 +1568,7 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
     w.part_dx.alloc((size_t)2 * ((N + kWG - 1) / kWG) * B);
     w.sysd.alloc((size_t)kSysStride * B);
     w.sysi.alloc((size_t)kSysStride * B);
+    w.smap.alloc((size_t)B);
     w.dt.alloc(B);
     w.Ibuf.alloc(2 * N * B);
     w.Iint.alloc(2 * N * B);
@@ -1624,7 +1681,7 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
         }
         MOF_HIP(hipMemcpyAsync(w.sysi.p, m->h_sysi, sizeof(int32_t) * kSysStride * B, hipMemcpyHostToDevice, s));
     }
-    if (m->iter_hint.size() < 3 * 16) m->iter_hint.assign(3 * 16, 0);
+    if (m->iter_hint.size() < 2 * kBulkHint) m->iter_hint.assign(2 * kBulkHint, 0);  // + pcg's bulk hints
     const bool amg = sp.amg && sp.precision == MOF_PREC_MIXED && amg_build(m);
     if (amg) {
         amg_ensure(m, B);

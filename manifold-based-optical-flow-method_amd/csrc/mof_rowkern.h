@@ -377,6 +377,21 @@ inline int32_t xcd_batch_cap(int64_t nblk, int32_t grp_sz) {
 }
 
 
+// A launch over n logical systems: logical l is system map[l] (map null: l
+// itself). A batch's tail iterations launch only the systems still running
+// (pcg: at most a quarter of the batch left), so the grid is not mostly
+// early-exiting workgroups; a system's arithmetic is the same whichever slot
+// of a launch it runs in (no fp contraction in the multi-system kernels).
+struct SysMap {
+    const int32_t *map;
+    int32_t n;
+};
+inline SysMap sys_all(int32_t B) { return SysMap{nullptr, B}; }
+__device__ __forceinline__ int32_t sm_b(const SysMap &s, int32_t l) {
+    l = min(l, s.n - 1);
+    return s.map ? s.map[l] : l;
+}
+
 struct MatH {
     int64_t sell_nb;
     const int32_t *sell_off, *sell_col;

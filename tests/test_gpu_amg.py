@@ -346,7 +346,8 @@ def test_early_convergence_mark_bit_identical(kind, monkeypatch):
     marked converged before the V-cycle (k_pcg_conv_early) and skip it: the
     z it would have made was never used, so V, the iteration counts and the
     refinement are the same bits as with the last V-cycle run
-    (MOF_CONV_EARLY=0)."""
+    (MOF_CONV_EARLY=0). Tail chunks launch over the running systems only
+    (SysMap): the same bits as launches over the whole batch (MOF_COMPACT=0)."""
     if kind == "golden":
         g = load_golden("G1_ico642")
         p, n, t, a = g["coordinates"], g["normals"], g["triangles"], g["areas"]
@@ -357,15 +358,17 @@ def test_early_convergence_mark_bit_identical(kind, monkeypatch):
         tk, lam = np.arange(9.0), 0.01
     T = len(I)
     out = []
-    for ce in (None, "0"):
-        if ce is None:
-            monkeypatch.delenv("MOF_CONV_EARLY", raising=False)
-        else:
-            monkeypatch.setenv("MOF_CONV_EARLY", ce)
+    for env in ({}, {"MOF_CONV_EARLY": "0"}, {"MOF_COMPACT": "0"}):
+        for k in ("MOF_CONV_EARLY", "MOF_COMPACT"):
+            if k in env:
+                monkeypatch.setenv(k, env[k])
+            else:
+                monkeypatch.delenv(k, raising=False)
         m = DeviceMesh(p, n, t, a)
         V, st = m.solve_range(I, tk, 0, T - 1, lam, precision="mixed", precond="amg", batch=5)
         m.close()
         assert st["failed"] == 0 and st["recovered"] == 0, st
         out.append((V, st["iterations"], st["max_rel_residual"]))
-    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
-    assert np.array_equal(out[0][0], out[1][0])
+    for o in out[1:]:
+        assert o[1] == out[0][1] and o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0])
