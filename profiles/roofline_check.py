@@ -15,6 +15,12 @@ those two `k_gather_I` starts are the timed ones (the host-IO leg and the
 parity solves after the clock are excluded); from a kernel summary, all
 SpMV launches (both template instances) -- and prints both fractions of the
 8 TB/s peak, and the full-launch durations side by side.
+Since round 5's early convergence mark, a refinement step whose systems were
+marked by its last queued iteration ends with one more SpMV launch that the
+bench does not time (the deferred x += alpha p only, every system retired
+from the SpMV work): in a trace those are the region's shortest SpMV
+launches beyond the line's `launches`, and they are left out (reported as
+`untimed_x_update_launches`).
 With a pmc_traffic.json key it also prints measured HBM bytes per launch
 (PMC, gfx950 FETCH_SIZE doubled) next to the algorithmic bytes.
 """
@@ -49,6 +55,8 @@ def main():
     full_us = None
     if rows and "Start_Timestamp" in rows[0]:
         d = timed_launches(rows, line, prefix)
+        extra = max(0, len(d) - int(rl.get("launches") or len(d)))
+        d = sorted(d)[extra:]
         n, us = len(d), sum(d) / len(d)
         full = sorted(d)[-rl["full_launches"]:] if rl.get("full_launches") else []
         full_us = sum(full) / len(full) if full else None
@@ -67,6 +75,8 @@ def main():
            "bytes_per_system": rl["bytes_per_system"],
            "bench_us_per_full_launch": rl.get("us_per_full_launch"),
            "rocprof_us_per_full_launch": round(full_us, 2) if full_us else None}
+    if rows and "Start_Timestamp" in rows[0]:
+        out["untimed_x_update_launches"] = extra
     if len(sys.argv) > 3:
         key = sys.argv[3]
         ent = json.load(open(sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"))[key]

@@ -51,6 +51,36 @@ def test_roofline_reproduces_from_trace_b1024():
     assert abs(out["pmc_hbm_bytes_median_launch"] / own - 1.0) < 0.10
 
 
+def test_roofline_reproduces_from_trace_b1536_final():
+    """The shipped default (batch 1536, round 5's final build): the SpMV
+    roofline reproduced from the line's own rocprof trace, the untimed
+    deferred-update launches (early convergence mark) left out, and the PMC
+    bytes within 10 % of the kernel's own."""
+    out = json.loads(_run("profiles/roofline_check.py", "profiles/r05_bench_c3_b1536_under_rocprof.json",
+                          "profiles/r05_c3_mixed_amg_b1536_kernel_trace.csv", "C3/mixed/amg/B1536"))
+    assert abs(out["rel_diff"]) < 0.01, out
+    line = json.loads(open(os.path.join(P, "r05_bench_c3_b1536_under_rocprof.json")).readline())
+    assert line["config"]["batch"] == 1536
+    assert out["rocprof_launches"] == line["roofline"]["launches"]
+    assert out["untimed_x_update_launches"] >= 0
+    assert out["rocprof_frac"] >= 0.65
+    rl = line["roofline"]
+    own = rl["kernel_bytes_per_system"] * 1536 + rl["kernel_shared_bytes_per_launch"]
+    assert abs(out["pmc_hbm_bytes_median_launch"] / own - 1.0) < 0.10
+
+
+def test_pmc_summary_reproduces_committed_entry_b1536(tmp_path):
+    dst = tmp_path / "pmc.json"
+    _run("profiles/pmc_summary.py", "profiles/r05_pmc_fetch_c3_mixed_amg_b1536.csv",
+         "profiles/r05_pmc_write_c3_mixed_amg_b1536.csv", str(dst), "C3/mixed/amg/B1536", "6144")
+    mine = json.load(open(dst))["C3/mixed/amg/B1536"]
+    ref = json.load(open(os.path.join(P, "pmc_traffic.json")))["C3/mixed/amg/B1536"]
+    assert mine["kernels"].keys() == ref["kernels"].keys()
+    for k, v in ref["kernels"].items():
+        assert mine["kernels"][k]["hbm_bytes_per_launch"] == pytest.approx(v["hbm_bytes_per_launch"])
+    assert mine["run"]["hbm_bytes_per_timestep"] == pytest.approx(ref["run"]["hbm_bytes_per_timestep"])
+
+
 def test_pmc_summary_reproduces_committed_entry_b1024(tmp_path):
     dst = tmp_path / "pmc.json"
     _run("profiles/pmc_summary.py", "profiles/r05_pmc_fetch_c3_mixed_amg_b1024.csv",
