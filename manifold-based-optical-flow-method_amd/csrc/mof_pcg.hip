@@ -95,6 +95,8 @@ struct PcgArgs {
                            // domain with the tentative prolongator (the decomposed path's
                            // halo exchange moves float2 z)
     SysMap sm;             // the systems the per-iteration launches cover (SysMap)
+    int32_t selfred;       // small meshes: the SpMV and the update reduce the partial records
+                           // they need themselves (no k_red_pq / k_red_rzrr launches)
 };
 
 // The per-system scalars every workgroup of the next launch needs, reduced
@@ -557,21 +559,35 @@ __device__ __forceinline__ void pcg_spmv_rows(const PcgArgs<V> &a, int32_t it, i
     using V2 = typename VT<V>::V2;
     const int64_t vb = (int64_t)b * a.N;
     double cur[2];
-    {
-        const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
-        cur[0] = c[0];
-        cur[1] = c[1];
-    }
     // The previous iteration's x += alpha p, deferred to here: this launch
     // reads p anyway (p = z + beta p), so the update kernel reads neither p
     // nor x. alpha is the update's own value (same partials, same order).
     V alpha_prev = 0;
     double old[2] = {1.0, 1.0};  // the previous iteration's r.z, |r|^2
-    if (!FIRST) {
-        const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
-        old[0] = o[0];
-        old[1] = o[1];
-        if (!force) alpha_prev = (V)(old[0] / *sc_pq(a.sc, a.B, (it + 1) & 1, b));
+    bool self = false;
+    if constexpr (NQ == 1) self = a.selfred != 0;
+    if (self) {
+        // the same reductions as k_red_rzrr / k_red_pq (reduce_sys), in every
+        // workgroup of the system: the same bits, two launches fewer
+        __shared__ double lds2[2 * (NT / 64)];
+        const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
+        reduce_sys<2, NT>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds2);
+        if (!FIRST) {
+            double pq1[1];
+            reduce_sys<2, NT>(a.part_rzrr + ((it + 1) & 1) * ps, a.red, a.B, b, old, lds2);
+            reduce_sys<1, NT>(a.part_pq + ((it + 1) & 1) * pqs, a.red, a.B, b, pq1, lds2);
+            if (!force) alpha_prev = (V)(old[0] / pq1[0]);
+        }
+    } else {
+        const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
+        cur[0] = c[0];
+        cur[1] = c[1];
+        if (!FIRST) {
+            const double *o = sc_rzrr(a.sc, a.B, (it + 1) & 1, b);
+            old[0] = o[0];
+            old[1] = o[1];
+            if (!force) alpha_prev = (V)(old[0] / *sc_pq(a.sc, a.B, (it + 1) & 1, b));
+        }
     }
     if (!force && cur[1] <= a.sysd[b * kSysStride + SD_TOL2]) {
         if (!FIRST) {
@@ -710,7 +726,13 @@ __device__ __forceinline__ void pcg_update_rows(const PcgArgs<V> &a, int32_t it,
     if (!si[SI_ACTIVE] || si[SI_CONV] >= 0) return;
     const int64_t ps = (int64_t)a.red.P * a.B * a.red.nmax * 2;
     double cur[2], pqv[1];
-    {
+    bool self = false;
+    if constexpr (NQ == 1) self = a.selfred != 0;
+    if (self) {  // small meshes: k_red_rzrr's and k_red_pq's reductions here (same bits)
+        __shared__ double lds2[2 * (kWG / 64)];
+        reduce_sys<2, kWG>(a.part_rzrr + (it & 1) * ps, a.red, a.B, b, cur, lds2);
+        reduce_sys<1, kWG>(a.part_pq + (it & 1) * ((int64_t)a.red.P * a.B * a.red.nmax), a.red, a.B, b, pqv, lds2);
+    } else {
         const double *c = sc_rzrr(a.sc, a.B, it & 1, b);
         cur[0] = c[0];
         cur[1] = c[1];
@@ -1123,6 +1145,7 @@ PcgArgs<V> make_args(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *din
     a.nblk = w.nblk;
     a.B = B;
     a.sm = sys_all(B);
+    a.selfred = 0;
     a.mat = mat;
     a.dinv = dinv;
     a.x = reinterpret_cast<V *>(w.vx.p);
@@ -1160,6 +1183,10 @@ void fetch_flags(mof_mesh *m, int32_t B, hipStream_t s) {
 
 // Longest first chunk of launches queued before the host looks at the flags.
 constexpr int32_t kMaxChunk = 256;
+// row blocks up to which the SpMV and the update reduce their scalars
+// themselves (PcgArgs::selfred): each workgroup then sums at most this many
+// records per value instead of reading one pre-reduced double
+constexpr int32_t kSelfRedBlk = 32;
 // a chunk whose running systems are at most this fraction of the batch
 // launches over them alone (pcg, SysMap). One box, round 5
 // (profiles/r05_ab/compact/): S1 1134 -> 1162 timesteps/s (its third and
@@ -1261,10 +1288,14 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
             a.sm = SysMap{m->ws.smap.p, n};
         }
     }
+    // a mesh of at most kSelfRedBlk row blocks: the SpMV and the update
+    // reduce their scalars themselves (MOF_SELFRED=0: the k_red_* launches)
+    const char *esr = std::getenv("MOF_SELFRED");
+    a.selfred = a.red.P == 1 && m->ws.nblk <= kSelfRedBlk && !(esr && *esr && std::atoi(esr) == 0) ? 1 : 0;
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol, etol);
     if (amg) precond(0);
-    k_red_rzrr<V><<<dim3((unsigned)a.sm.n), kWG, 0, s>>>(a, 0);
+    if (!a.selfred) k_red_rzrr<V><<<dim3((unsigned)a.sm.n), kWG, 0, s>>>(a, 0);
     MOF_HIP(hipGetLastError());
     // The first chunk runs as many iterations as the same solve of the
     // previous batch needed (timesteps of one run converge alike), so the
@@ -1301,11 +1332,11 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
                 launch_spmv(a, it == 0, gx, s, it, 0);
             }
             const unsigned nl = (unsigned)a.sm.n;
-            k_red_pq<V><<<dim3(nl), kWG, 0, s>>>(a, it & 1);
+            if (!a.selfred) k_red_pq<V><<<dim3(nl), kWG, 0, s>>>(a, it & 1);
             k_pcg_update<V><<<dim3(upd_blocks(m->ws.nblk), nl), kWG, 0, s>>>(a, it);
             if (early) k_pcg_conv_early<V><<<dim3(nl), kWG, 0, s>>>(a, it);
             if (amg) precond((it + 1) & 1);
-            k_red_rzrr<V><<<dim3(nl), kWG, 0, s>>>(a, (it + 1) & 1);
+            if (!a.selfred) k_red_rzrr<V><<<dim3(nl), kWG, 0, s>>>(a, (it + 1) & 1);
         }
         MOF_HIP(hipGetLastError());
         fetch_flags(m, B, s);

@@ -64,7 +64,7 @@ _KEY_NEUTRAL = frozenset((
     "MOF_CHECKPOINT_DIR", "MOF_CHECKPOINT_CHUNK", "MOF_SOLVE_VERBOSE", "MOF_AMG_VERBOSE", "MOF_HOSTIO_VERBOSE",
     "MOF_STAGE_MB", "MOF_STAGE_DIRECT_MB", "MOF_IO_THREADS", "MOF_FUSED_NQ", "MOF_FUSED_MAX_BLK", "MOF_RCCL_LIB",
     # same bits either way (GPU tests): launch shapes and work skipping only
-    "MOF_CONV_EARLY", "MOF_COMPACT", "MOF_RESTR_SORT", "MOF_GAL_BIG",
+    "MOF_CONV_EARLY", "MOF_COMPACT", "MOF_RESTR_SORT", "MOF_GAL_BIG", "MOF_SELFRED",
 ))
 
 

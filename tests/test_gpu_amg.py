@@ -347,7 +347,9 @@ def test_early_convergence_mark_bit_identical(kind, monkeypatch):
     z it would have made was never used, so V, the iteration counts and the
     refinement are the same bits as with the last V-cycle run
     (MOF_CONV_EARLY=0). Tail chunks launch over the running systems only
-    (SysMap): the same bits as launches over the whole batch (MOF_COMPACT=0)."""
+    (SysMap): the same bits as launches over the whole batch (MOF_COMPACT=0).
+    On the 642-vertex mesh the SpMV and the update reduce their own scalars
+    (PcgArgs::selfred): the same bits as the k_red_* launches (MOF_SELFRED=0)."""
     if kind == "golden":
         g = load_golden("G1_ico642")
         p, n, t, a = g["coordinates"], g["normals"], g["triangles"], g["areas"]
@@ -358,8 +360,8 @@ def test_early_convergence_mark_bit_identical(kind, monkeypatch):
         tk, lam = np.arange(9.0), 0.01
     T = len(I)
     out = []
-    for env in ({}, {"MOF_CONV_EARLY": "0"}, {"MOF_COMPACT": "0"}):
-        for k in ("MOF_CONV_EARLY", "MOF_COMPACT"):
+    for env in ({}, {"MOF_CONV_EARLY": "0"}, {"MOF_COMPACT": "0"}, {"MOF_SELFRED": "0"}):
+        for k in ("MOF_CONV_EARLY", "MOF_COMPACT", "MOF_SELFRED"):
             if k in env:
                 monkeypatch.setenv(k, env[k])
             else:
