@@ -300,7 +300,8 @@ def main():
     if not dry:
         # a batch whose workspace (~720 B per vertex and timestep with the
         # multigrid levels, the library's own estimate) and signal rows do
-        # not fit 85 % of this GPU's free HBM is halved -- and said so --
+        # not fit 85 % of this GPU's free HBM is reduced -- to the largest
+        # multiple of 256 that fits, then halved below 256 -- and said so,
         # rather than failing an allocation mid-run
         free_b, _ = torch.cuda.mem_get_info(local)
         steps_rows = (args.warmup + args.steps) if not strong else 0
@@ -310,8 +311,10 @@ def main():
             return 720.0 * N * b + 8.0 * N * rows + 16.0 * N * b
 
         B0 = B
-        if need(B) > 0.85 * free_b and B > 1024:
-            B = 1024
+        if need(B) > 0.85 * free_b and B > 256:
+            B = B // 256 * 256
+            while B > 256 and need(B) > 0.85 * free_b:
+                B -= 256
         while B > 64 and need(B) > 0.85 * free_b:
             B //= 2
         if B != B0:
