@@ -37,6 +37,9 @@ mixed solve -- for aggregation-multigrid variants:
               [-1, 1] as int8 with the one fixed scale 1/127, rescaled)
   amax=K      level-0 aggregates of at most K nodes (root + K-1 free
               neighbours; design study)
+  cheb=K      level 0 smoothed by degree-K Chebyshev in D^-1 A on both sides
+              (pre from x = 0); chebpost=K after the coarse correction only
+              (pre stays om D^-1 b); cr=X the interval [lmax / X, lmax]
   s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
               (from the copy's diagonal blocks) and the level-0 Galerkin
               product all on the stored copy in format F (1 = bf16, today)
@@ -392,6 +395,8 @@ def vcycle(levels, l, b, opts):
             L.Aq = quantize(L.A, L.bs, int(qf))
         Aw = L.Aq
     nu = int(opts.get("nu1", 1)) if l >= 1 else int(opts.get("nu0", 1))  # sweeps per side
+    if l == 0 and (opts.get("cheb") or opts.get("chebpost")):
+        return _cheb_vcycle(levels, L, Aw, b, opts)
     x = L.om * bsr_apply(L.Dinv, b, L.bs)
     for _ in range(nu - 1):
         x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
@@ -403,6 +408,47 @@ def vcycle(levels, l, b, opts):
         for _ in range(nu):
             x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
     return x
+
+
+def _cheb(L, Aw, b, x, deg, ratio):
+    """Degree-deg Chebyshev smoothing of Aw x = b in D^-1 Aw over
+    [lmax / ratio, lmax] (lmax: 1.1 x a 20-step power estimate, cached)."""
+    if not hasattr(L, "lmax"):
+        v = np.random.default_rng(0).standard_normal(Aw.shape[0])
+        for _ in range(20):
+            v = bsr_apply(L.Dinv, Aw @ v, L.bs)
+            lm = np.linalg.norm(v)
+            v /= lm
+        L.lmax = 1.1 * lm
+    hi, lo = L.lmax, L.lmax / ratio
+    theta, delta = 0.5 * (hi + lo), 0.5 * (hi - lo)
+    sigma = theta / delta
+    rho = 1.0 / sigma
+    r = bsr_apply(L.Dinv, b - Aw @ x if x is not None else b, L.bs)
+    x = np.zeros_like(b) if x is None else x
+    d = r / theta
+    for k in range(deg):
+        x = x + d
+        if k == deg - 1:
+            break
+        r = r - bsr_apply(L.Dinv, Aw @ d, L.bs)
+        rho1 = 1.0 / (2.0 * sigma - rho)
+        d = rho1 * rho * d + (2.0 * rho1 / delta) * r
+        rho = rho1
+    return x
+
+
+def _cheb_vcycle(levels, L, Aw, b, opts):
+    """Level 0 with Chebyshev smoothing: cheb=k both sides (pre from x = 0),
+    chebpost=k the post side only (pre stays om D^-1 b); cr = the ratio."""
+    ratio = float(opts.get("cr", 30.0))
+    kpre = int(opts.get("cheb", 0))
+    kpost = int(opts.get("chebpost", 0)) or kpre
+    x = _cheb(L, Aw, b, None, kpre, ratio) if kpre else L.om * bsr_apply(L.Dinv, b, L.bs)
+    r = b - Aw @ x
+    y = vcycle(levels, 1, L.P.T @ r, opts)
+    x = x + L.P @ y
+    return _cheb(L, Aw, b, x, kpost, ratio)
 
 
 def pcg(A, f, M, tol=1e-4, maxit=2000):
