@@ -40,6 +40,8 @@ mixed solve -- for aggregation-multigrid variants:
   cheb=K      level 0 smoothed by degree-K Chebyshev in D^-1 A on both sides
               (pre from x = 0); chebpost=K after the coarse correction only
               (pre stays om D^-1 b); cr=X the interval [lmax / X, lmax]
+  mcgs=1      level 0 smoothed by multicolour block Gauss-Seidel (forward
+              before, backward after; gsom=X damping)
   s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
               (from the copy's diagonal blocks) and the level-0 Galerkin
               product all on the stored copy in format F (1 = bf16, today)
@@ -397,6 +399,8 @@ def vcycle(levels, l, b, opts):
     nu = int(opts.get("nu1", 1)) if l >= 1 else int(opts.get("nu0", 1))  # sweeps per side
     if l == 0 and (opts.get("cheb") or opts.get("chebpost")):
         return _cheb_vcycle(levels, L, Aw, b, opts)
+    if l == 0 and opts.get("mcgs"):
+        return _mcgs_vcycle(levels, L, Aw, b, opts)
     x = L.om * bsr_apply(L.Dinv, b, L.bs)
     for _ in range(nu - 1):
         x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
@@ -449,6 +453,47 @@ def _cheb_vcycle(levels, L, Aw, b, opts):
     y = vcycle(levels, 1, L.P.T @ r, opts)
     x = x + L.P @ y
     return _cheb(L, Aw, b, x, kpost, ratio)
+
+
+def _colors(L):
+    """Greedy colouring of the level's block graph (node order)."""
+    if not hasattr(L, "color"):
+        G = block_graph(L.A, L.bs).tocsr()
+        n = G.shape[0]
+        col = -np.ones(n, dtype=np.int64)
+        for i in range(n):
+            used = set(col[G.indices[G.indptr[i]:G.indptr[i + 1]]].tolist())
+            c = 0
+            while c in used:
+                c += 1
+            col[i] = c
+        L.color = col
+        L.ncolor = int(col.max()) + 1
+    return L.color, L.ncolor
+
+
+def _mcgs(L, Aw, b, x, order, om):
+    """Block Gauss-Seidel by colour (the colours in `order`), damped by om."""
+    col, _ = _colors(L)
+    x = x.copy()
+    for c in order:
+        rows = np.flatnonzero(col == c)
+        dof = (rows[:, None] * L.bs + np.arange(L.bs)[None]).ravel()
+        r = (b[dof] - Aw[dof] @ x).reshape(-1, L.bs)
+        x[dof] += om * np.einsum("nij,nj->ni", L.Dinv[rows], r).ravel()
+    return x
+
+
+def _mcgs_vcycle(levels, L, Aw, b, opts):
+    """Level 0 with multicolour block Gauss-Seidel: mcgs=1 forward before,
+    backward after (symmetric); om damping from gsom= (default 1)."""
+    _, nc = _colors(L)
+    om = float(opts.get("gsom", 1.0))
+    x = _mcgs(L, Aw, b, np.zeros_like(b), range(nc), om)
+    r = b - Aw @ x
+    y = vcycle(levels, 1, L.P.T @ r, opts)
+    x = x + L.P @ y
+    return _mcgs(L, Aw, b, x, range(nc - 1, -1, -1), om)
 
 
 def pcg(A, f, M, tol=1e-4, maxit=2000):
