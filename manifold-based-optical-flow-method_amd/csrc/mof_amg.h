@@ -153,6 +153,11 @@ struct AmgDevice {
     // 2488 -> 2515 (the CPU prototype's 17 % fewer S1 its to 1e-4 did not
     // carry over to the refinement's inner solves): 1
     int32_t nu1 = 1;
+    // open surfaces: extra level-0 sweeps on the boundary rows and their
+    // neighbour ring (k_bsweep); bsw_n rows (0: none), bsw_pos[N] = the row's
+    // index in bsw_rows or -1
+    int32_t bsw_n = 0, bsw_sweeps = 0;
+    DevArray<int32_t> bsw_rows, bsw_pos;
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)

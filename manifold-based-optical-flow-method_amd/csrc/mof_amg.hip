@@ -1668,6 +1668,67 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t
     }
 }
 
+// Open surfaces: `sweeps` extra block-Jacobi sweeps (damping omega, b = r)
+// on the boundary rows and their neighbour ring only, after the fused
+// pre-smoothing and before the post-smoothing (the cycle stays symmetric).
+// At a Neumann boundary vertex the diagonal block lacks the missing
+// triangles, so one damped sweep leaves those rows least smoothed. One
+// workgroup per system; the subset's iterates live in LDS (two buffers: a
+// Jacobi sweep reads only the previous one), rows outside the subset are
+// read from x and do not change. F32X: x as fp32 pairs (the corrected
+// iterate with xm = 2), else the bf16 x0 format.
+constexpr int kBswWG = 1024, kBswMax = 4096;
+template <bool F32X>
+__global__ __launch_bounds__(kBswWG) void k_bsweep(int32_t N, int32_t nbr, const int32_t *__restrict__ rows,
+                                                   const int32_t *__restrict__ pos, SysMap sm, MatH mat,
+                                                   const float *__restrict__ rv, float *__restrict__ xv, float omega,
+                                                   int32_t sweeps, const int32_t *__restrict__ sysi) {
+#pragma clang fp contract(off)
+    __shared__ float2 xs[2][kBswMax];
+    if ((int32_t)blockIdx.x >= sm.n) return;
+    const int32_t b = sm_b(sm, blockIdx.x);
+    if (retired(sysi, b)) return;
+    const int64_t vb = (int64_t)b * N;
+    auto ldg = [&](int32_t j) -> float2 {
+        if constexpr (F32X)
+            return reinterpret_cast<const float2 *>(xv)[vb + j];
+        else
+            return ld_x0(xv, vb + j);
+    };
+    for (int32_t p = threadIdx.x; p < nbr; p += kBswWG) xs[0][p] = ldg(rows[p]);
+    __syncthreads();
+    int cur = 0;
+    for (int32_t k = 0; k < sweeps; ++k) {
+        for (int32_t p = threadIdx.x; p < nbr; p += kBswWG) {
+            const int32_t i = rows[p];
+            const int32_t bs[1] = {b};
+            float y[1][2];
+            uint2 dg[1];
+            auto xl = [&](int, int32_t j) -> float2 {
+                const int32_t q = pos[j];
+                return q >= 0 ? xs[cur][q] : ldg(j);
+            };
+            if (mat.sell_mir)
+                spmv_row_hx_ns<true, 1, kPost0U>(mat, bs, i, xl, y, dg);
+            else
+                spmv_row_hx_ns<false, 1, kPost0U>(mat, bs, i, xl, y, dg);
+            const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
+            const float2 ds = bf16_diag_solve(dg[0], ri.x - y[0][0], ri.y - y[0][1]);
+            const float2 xi = xs[cur][p];
+            xs[cur ^ 1][p] = make_float2(xi.x + omega * ds.x, xi.y + omega * ds.y);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    for (int32_t p = threadIdx.x; p < nbr; p += kBswWG) {
+        const float2 v = xs[cur][p];
+        if constexpr (F32X)
+            reinterpret_cast<float2 *>(xv)[vb + rows[p]] = v;
+        else
+            st_x0(xv, vb + rows[p], v.x, v.y);
+    }
+}
+
 template <int XM, bool ZH, typename... Args>
 void launch_post0(int32_t nblk, int32_t B, hipStream_t s, Args... args) {
     const dim3 g(xcd_grid(nblk, (B + kPost0NS - 1) / kPost0NS, kGrpSmooth > kPost0NS ? kGrpSmooth / kPost0NS : 1));
@@ -1841,6 +1902,46 @@ bool amg_build(mof_mesh *m) {
         d.alloc(h.size());
         if (!h.empty()) d.upload(h.data(), h.size(), s);
     };
+    // open surfaces: the boundary rows (fewer incident triangles than
+    // neighbours: the diagonal block's contribution list has one entry per
+    // incident triangle) and one ring of their neighbours, for k_bsweep.
+    // Auto: 2 sweeps per side where that ring is >= 1/20 of the rows. Round
+    // 5, one box (profiles/r05_ab/bsw/): S1s (ring 14 % of 3,249 rows) 28.6
+    // -> 19.8 PCG its/timestep, 25.8-26.3k -> 26.9-27.5k timesteps/s (two
+    // launches more per cycle on a launch-bound mesh); S1 (ring 2 %) 44.8 ->
+    // 42.9 its, 1151-1154 -> 1142-1147 (the CPU prototype's 10 -> 9 its to
+    // 1e-4, tools/amg_proto.py bsw=2). MOF_AMG_BSW = sweeps per side (0 off)
+    // forces it on any open surface.
+    G.bsw_n = 0;
+    G.bsw_sweeps = 0;
+    int32_t bsw = -1;
+    if (const char *v = std::getenv("MOF_AMG_BSW")) bsw = std::max(0, std::min(8, std::atoi(v)));
+    if (open_surface && bsw != 0) {
+        const Pattern &P = m->pat;
+        std::vector<uint8_t> mark(m->N, 0);
+        for (int32_t i = 0; i < m->N; ++i) {
+            const int32_t a = P.vptr[i], e2 = P.vptr[i + 1];
+            const int32_t d = (int32_t)(std::lower_bound(P.vcol.begin() + a, P.vcol.begin() + e2, i) - P.vcol.begin());
+            if (P.cptr[d + 1] - P.cptr[d] < e2 - a - 1) mark[i] = 1;
+        }
+        std::vector<uint8_t> ring(mark);
+        for (int32_t i = 0; i < m->N; ++i)
+            if (mark[i])
+                for (int32_t q = P.vptr[i]; q < P.vptr[i + 1]; ++q) ring[P.vcol[q]] = 1;
+        std::vector<int32_t> rows, pos(m->N, -1);
+        for (int32_t i = 0; i < m->N; ++i)
+            if (ring[i]) {
+                pos[i] = (int32_t)rows.size();
+                rows.push_back(i);
+            }
+        const bool want = bsw > 0 || 20 * (int64_t)rows.size() >= m->N;
+        if (want && !rows.empty() && rows.size() <= (size_t)kBswMax) {
+            put_i(G.bsw_rows, rows);
+            put_i(G.bsw_pos, pos);
+            G.bsw_n = (int32_t)rows.size();
+            G.bsw_sweeps = bsw > 0 ? bsw : 2;
+        }
+    }
     for (size_t l = 0; l < H.levels.size(); ++l) {
         const AmgLevel &L = H.levels[l];
         AmgDevLevel &D = G.lv[l];
@@ -2216,6 +2317,9 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = 0; l < 1; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
+            if (G.bsw_n > 0)
+                k_bsweep<false><<<dim3((unsigned)nL), kBswWG, 0, s>>>(v[0].n, G.bsw_n, G.bsw_rows.p, G.bsw_pos.p, sm,
+                                                                     mat0, r0, v[0].x, om, G.bsw_sweeps, sysi);
             k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (nL + kRes0NS - 1) / kRes0NS,
                                                kGrpSmooth > kRes0NS ? kGrpSmooth / kRes0NS : 1)),
                                  kWG, 0, s>>>(v[0].n, nblk, B, sm, mat0, r0, v[0].x,
@@ -2258,6 +2362,9 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
+                if (G.bsw_n > 0)
+                    k_bsweep<true><<<dim3((unsigned)nL), kBswWG, 0, s>>>(v[0].n, G.bsw_n, G.bsw_rows.p, G.bsw_pos.p,
+                                                                        sm, mat0, r0, v[0].y, om, G.bsw_sweeps, sysi);
                 if (zh)
                     launch_post0<2, true>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
                 else
@@ -2267,6 +2374,9 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                     k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
+                if (G.bsw_n > 0)
+                    k_bsweep<false><<<dim3((unsigned)nL), kBswWG, 0, s>>>(v[0].n, G.bsw_n, G.bsw_rows.p, G.bsw_pos.p,
+                                                                         sm, mat0, r0, v[0].x, om, G.bsw_sweeps, sysi);
                 if (zh)
                     launch_post0<1, true>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
                 else

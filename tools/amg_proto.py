@@ -55,6 +55,7 @@ import os
 import numpy as np
 import scipy.sparse as sp
 import scipy.linalg as sla
+import scipy.sparse.linalg as sla_sparse
 from scipy.sparse.csgraph import reverse_cuthill_mckee
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -388,6 +389,10 @@ def vcycle(levels, l, b, opts):
     L = levels[l]
     if hasattr(L, "coarse"):
         return L.coarse @ b
+    if l == int(opts.get("exact", -1)):  # an exact solve from this level down (two-grid bound)
+        if not hasattr(L, "lu"):
+            L.lu = sla_sparse.splu(L.A.tocsc())
+        return L.lu.solve(b)
     Aw = L.A
     qf = opts.get("q1") if l >= 1 else opts.get("q0")
     if hasattr(L, "Aq"):
@@ -401,6 +406,8 @@ def vcycle(levels, l, b, opts):
         return _cheb_vcycle(levels, L, Aw, b, opts)
     if l == 0 and opts.get("mcgs"):
         return _mcgs_vcycle(levels, L, Aw, b, opts)
+    if l == 0 and opts.get("bsw"):
+        return _bsw_vcycle(levels, L, Aw, b, opts)
     x = L.om * bsr_apply(L.Dinv, b, L.bs)
     for _ in range(nu - 1):
         x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
@@ -494,6 +501,40 @@ def _mcgs_vcycle(levels, L, Aw, b, opts):
     y = vcycle(levels, 1, L.P.T @ r, opts)
     x = x + L.P @ y
     return _mcgs(L, Aw, b, x, range(nc - 1, -1, -1), om)
+
+
+def _bsw(L, Aw, b, x, k, om, ring):
+    """k block-Jacobi sweeps (damping om) on the boundary rows and their
+    `ring`-neighbourhood only."""
+    if not hasattr(L, "bdof"):
+        rows = np.flatnonzero(system.boundary)
+        G = block_graph(L.A, L.bs).tocsr()
+        sel = np.zeros(G.shape[0], dtype=bool)
+        sel[rows] = True
+        for _ in range(ring):
+            sel = sel | (G @ sel.astype(np.float64) > 0)
+        L.brows = np.flatnonzero(sel)
+        L.bdof = (L.brows[:, None] * L.bs + np.arange(L.bs)[None]).ravel()
+        L.Ab = Aw[L.bdof].tocsr()
+    x = x.copy()
+    for _ in range(k):
+        r = (b[L.bdof] - L.Ab @ x).reshape(-1, L.bs)
+        x[L.bdof] += om * np.einsum("nij,nj->ni", L.Dinv[L.brows], r).ravel()
+    return x
+
+
+def _bsw_vcycle(levels, L, Aw, b, opts):
+    """Level 0 as the library's, plus bsw=K sweeps on the boundary rows
+    (bring=R neighbour rings, bom=X damping) after the pre- and before the
+    post-smoothing (symmetric)."""
+    k, ring, om = int(opts["bsw"]), int(opts.get("bring", 1)), float(opts.get("bom", 0.7))
+    x = L.om * bsr_apply(L.Dinv, b, L.bs)
+    x = _bsw(L, Aw, b, x, k, om, ring)
+    r = b - Aw @ x
+    y = vcycle(levels, 1, L.P.T @ r, opts)
+    x = x + L.P @ y
+    x = _bsw(L, Aw, b, x, k, om, ring)
+    return x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
 
 
 def pcg(A, f, M, tol=1e-4, maxit=2000):
