@@ -42,6 +42,11 @@ mixed solve -- for aggregation-multigrid variants:
               (pre stays om D^-1 b); cr=X the interval [lmax / X, lmax]
   mcgs=1      level 0 smoothed by multicolour block Gauss-Seidel (forward
               before, backward after; gsom=X damping)
+  bsw=K       K extra block-Jacobi sweeps on the boundary rows (open
+              surfaces) and bring=R rings of neighbours (bom=X damping), after
+              the pre- and before the post-smoothing (the library's k_bsweep)
+  exact=L     an exact (sparse LU) solve from level L down: the two-grid
+              bound at L = 1
   s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
               (from the copy's diagonal blocks) and the level-0 Galerkin
               product all on the stored copy in format F (1 = bf16, today)
