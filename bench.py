@@ -105,6 +105,10 @@ def parse():
     ap.add_argument("--etol", type=float, default=0.0,
                     help="the refinement's error control: estimated error <= etol max|V| (0: the library's "
                          "1e-7, < 0: the residual test alone)")
+    ap.add_argument("--legs", default="auto",
+                    help="comma-separated extra configurations timed after the main line on the same GPU, "
+                         "each with its iterations, parity and SpMV roofline (auto: F3,S1s -- the reference's "
+                         "mesh class -- for a 1-GPU C3 line; none: no legs)")
     ap.add_argument("--host-batches", type=int, default=4,
                     help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
                          "the device-resident region (0: none)")
@@ -165,34 +169,201 @@ def step_traffic(key, value):
             "source": "profiles/pmc_traffic.json[%s] (PMC run of %d timesteps)" % (key, run["timesteps"])}
 
 
-def parity_check(geom, t, a, lam, samples):
-    """Parity in the measured run: for each sampled timestep of the last timed
-    batch, the reference's system (oracle.step_system: the bit-exact
+def parity_checks(jobs):
+    """Parity in the measured run: for each sampled timestep of a line's last
+    timed batch, the reference's system (oracle.step_system: the bit-exact
     restatement of worker's assembly, compute_optical_flow.py:100-146) solved
     by the reference's own solver, scipy's spsolve (:147), against the V the
-    timed GPU solve returned. The samples run in host threads (the C oracle
-    and SuperLU release the GIL)."""
+    timed GPU solve returned. jobs: [(geometry, triangles, areas, lambda,
+    samples)], one per line (the main line and its legs); every sample of
+    every job runs in one pool of host threads (the C oracle and SuperLU
+    release the GIL). Returns one parity dict per job."""
     import oracle
     from concurrent.futures import ThreadPoolExecutor
     from scipy.sparse.linalg import spsolve
-    a2, gw, e, iw = geom
 
-    def one(smp):
-        k, I0, I1, dt, V = smp
+    def one(item):
+        (a2, gw, e, iw), t, a, lam, (k, I0, I1, dt, V) = item
         A, f = oracle.step_system(a2, gw, e, iw, t, a, lam, I0, I1, dt)
         Vo = spsolve(A.tocsc(), f)
         return k, float(np.abs(V - Vo).max()), float(np.abs(Vo).max()), \
             float(np.linalg.norm(f - A @ V) / np.linalg.norm(f))
 
+    items = [((geom, t, a, lam, smp), j) for j, (geom, t, a, lam, samples) in enumerate(jobs) for smp in samples]
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(max(1, len(samples))) as ex:
-        res = list(ex.map(one, samples))
-    return {"max_abs_err": max(r[1] for r in res), "timesteps": [r[0] for r in res],
-            "per_timestep_max_abs_err": [r[1] for r in res], "max_abs_V": max(r[2] for r in res),
-            "rel_residual_oracle_A": max(r[3] for r in res), "bar": 1e-6,
-            "reference": "oracle.step_system (bit-exact A_k, f_k of compute_optical_flow.py:100-146) + "
-                         "scipy spsolve (:147), on timesteps of the last timed batch",
-            "seconds": round(time.perf_counter() - t0, 1)}
+    with ThreadPoolExecutor(max(1, min(16, len(items)))) as ex:
+        res = list(ex.map(one, [it for it, _ in items]))
+    secs = round(time.perf_counter() - t0, 1)
+    out = []
+    for j in range(len(jobs)):
+        rj = [r for r, (_, jj) in zip(res, items) if jj == j]
+        out.append({"max_abs_err": max(r[1] for r in rj), "timesteps": [r[0] for r in rj],
+                    "per_timestep_max_abs_err": [r[1] for r in rj], "max_abs_V": max(r[2] for r in rj),
+                    "rel_residual_oracle_A": max(r[3] for r in rj), "bar": 1e-6,
+                    "reference": "oracle.step_system (bit-exact A_k, f_k of compute_optical_flow.py:100-146) + "
+                                 "scipy spsolve (:147), on timesteps of the last timed batch",
+                    "seconds": secs} if rj else None)
+    return out
+
+
+# extra lines after the main one (--legs): (batch, timed steps, warmup steps);
+# the small jobs time their whole job per step (SMALL_JOBS)
+LEGS = {"F3": (1536, 5, 1), "S1s": (97, 20, 2), "S1": (1536, 3, 1), "R3": (1536, 3, 1), "C2": (1536, 5, 1)}
+
+
+def run_leg(name, args, torch, local):
+    """One extra configuration on this GPU, device-resident like the main
+    line (mixed precision, multigrid): its timesteps/s, PCG iterations, SpMV
+    roofline and parity samples (checked by parity_checks with the main
+    line's). The mesh and its signal rows are freed before returning."""
+    from mofhip import DeviceMesh, synth
+    p, t, n, a = synth.mesh_for_config(name)
+    N = len(p)
+    dev = torch.device("cuda", local)
+    t0 = time.perf_counter()
+    mesh = DeviceMesh(p, n, t, a, device=local)
+    info = mesh.info()
+    build_s = time.perf_counter() - t0
+    B, steps, warmup = LEGS[name]
+    if name in SMALL_JOBS:
+        B = SMALL_JOBS[name]
+        calls = [(0, B)] * (warmup + steps)
+        rows = B + 1
+    else:
+        B = min(B, int(info.get("max_batch") or B))
+        calls = [(s_ * B, (s_ + 1) * B) for s_ in range(warmup + steps)]
+        rows = (warmup + steps) * B + 1
+    phase, kappa = synth.wave_phase(name, p)
+    phi = torch.from_numpy(np.ascontiguousarray(phase)).to(dev)
+    I_dev = torch.empty((rows, N), dtype=torch.float64, device=dev)
+    for r0 in range(0, rows, 256):
+        r1 = min(rows, r0 + 256)
+        kk = torch.arange(r0, r1, dtype=torch.float64, device=dev)
+        I_dev[r0:r1] = torch.sin(kappa * phi[None, :] - 0.3 * kk[:, None])
+    V_dev = torch.empty((B, 2 * N), dtype=torch.float64, device=dev)
+    tk = np.arange(rows, dtype=np.float64)
+    opts = dict(precision="mixed", batch=B, rtol=args.rtol, precond="amg", etol=args.etol)
+
+    def solve(a_, b_, timed):
+        return mesh.solve_range_device(I_dev.data_ptr(), I_dev.data_ptr(), rows, tk, a_, b_, args.lambda_,
+                                       V_dev.data_ptr(), device=local, time_spmv=timed, **opts)
+
+    for a_, b_ in calls[:warmup]:
+        solve(a_, b_, False)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    agg = {}
+    for a_, b_ in calls[warmup:]:
+        st = solve(a_, b_, True)
+        for k, v in st.items():
+            agg[k] = max(agg.get(k, 0), v) if k.startswith("max_") else agg.get(k, 0) + v
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    a_, b_ = calls[-1]
+    samples = []
+    for k in sorted({a_, b_ - 1}):
+        samples.append((k, I_dev[k].cpu().numpy(), I_dev[k + 1].cpu().numpy(), float(tk[k + 1] - tk[k]),
+                        V_dev[k - a_].cpu().numpy()))
+    del I_dev, V_dev, phi
+    mesh.close()
+    torch.cuda.empty_cache()
+    n_ts = agg["systems"]
+    leg = {"config": name, "workload": CONFIG_NAMES[name], "vertices": N, "batch": B,
+           "value": round(n_ts / elapsed, 3), "unit": "timesteps/s", "steps": steps, "warmup": warmup,
+           "timesteps_timed": n_ts, "ms_per_step": round(1e3 * elapsed / steps, 3),
+           "precision": "mixed", "precond": "amg",
+           "roofline": spmv_roofline(agg, info, N, "mixed", "amg", B, name),
+           "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / max(1, n_ts), 1),
+                      "failed": agg["failed"], "recovered": agg["recovered"],
+                      "max_rel_residual": agg["max_rel_residual"], "max_err_est": agg["max_err_est"],
+                      "mesh_build_s": round(build_s, 3)}}
+    return leg, (p, t, n, a), samples
+
+
+def size_batch(B, N, free_b, max_batch, rows_of):
+    """The batch this rank can run: a batch whose workspace (~720 B per
+    vertex and timestep with the multigrid levels, the library's own
+    estimate) and signal rows (rows_of(b) rows of N f64) do not fit 85 % of
+    the GPU's free HBM is reduced -- to the largest multiple of 256 that
+    fits, then halved below 256 -- and said so, rather than failing an
+    allocation mid-run; then clamped to the library's largest batch whose
+    launch grids fit 2^32 work-items (mof_mesh_info.max_batch). Returns
+    (batch, note or None)."""
+    def need(b):
+        return 720.0 * N * b + 8.0 * N * rows_of(b) + 16.0 * N * b
+
+    note = None
+    B0 = B
+    if need(B) > 0.85 * free_b and B > 256:
+        B = B // 256 * 256
+        while B > 256 and need(B) > 0.85 * free_b:
+            B -= 256
+    while B > 64 and need(B) > 0.85 * free_b:
+        B //= 2
+    if B != B0:
+        note = "batch %d reduced to %d: %.0f GB of HBM free" % (B0, B, free_b / 1e9)
+    if max_batch and B > max_batch:
+        B1, B = B, int(max_batch)
+        note = (note + "; " if note else "") + "batch %d reduced to %d: launch grids past 2^32 work-items" % (B1, B)
+    return B, note
+
+
+def spmv_roofline(agg, info, N, precision, precond, B, config):
+    """The SpMV roofline of a timed region (the dominant kernel, k_pcg_spmv)."""
+    # roofline of the dominant kernel (k_pcg_spmv), live over the timed region:
+    # every timed launch is charged with the systems it processed, in
+    # SURVEY.md 8(d)'s algorithmic bytes of a batched CSR SpMV
+    #   B nnz s_v + 4 nnz + 4 (R + 1) + B R (s_x + s_y)   (nnz = 4 nblocks, R = 2N)
+    achieved = agg["spmv_bytes"] / (agg["ms_spmv"] * 1e-3) / 1e9 if agg["ms_spmv"] > 0 else 0.0
+    kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
+    traffic, traffic_src = pmc_traffic("%s/%s/%s/B%d" % (config, precision, precond, B), kname)
+    sv = 4 if precision == "mixed" else 8
+    nnz, R = 4 * info["nblocks"], 2 * N
+    per_sys = nnz * sv + R * 2 * sv
+    shared = 4 * nnz + 4 * (R + 1)
+    nl = max(1, agg["spmv_launches"])
+    nfull = max(1, agg["spmv_full_launches"])
+    t_full = agg["ms_spmv_full"] / nfull * 1e-3 if agg["ms_spmv_full"] > 0 else 0.0
+    # launches that did work (the shared bytes are charged once each)
+    n_work = round((agg["spmv_bytes"] - agg["spmv_systems"] * per_sys) / shared) if agg["spmv_bytes"] else 0
+    # the kernel's own traffic: the fp32 operator's diagonal + upper blocks
+    # (lower ones read as transposes through the shared mirror table), z
+    # gathered, q, p and x read and written; shared column indices (+ mirror)
+    nread = info.get("blocks_read", info["nblocks"]) if precision == "mixed" else info["nblocks"]
+    k_sys = nread * 4 * sv + N * 2 * sv * 7
+    k_shared = info["nblocks"] * 4 * (2 if nread < info["nblocks"] else 1)
+    k_bytes = agg["spmv_systems"] * k_sys + n_work * k_shared
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": traffic_src, "kernel": kname,
+                "bytes_formula": "SURVEY.md 8(d): B*nnz*s_v + 4*nnz + 4*(R+1) + B*R*(s_x+s_y)",
+                "bytes_per_launch": round(agg["spmv_bytes"] / nl),
+                "bytes_per_system": per_sys, "shared_bytes_per_launch": shared,
+                "systems_per_launch": round(agg["spmv_systems"] / nl, 2),
+                "us_per_launch": round(1e3 * agg["ms_spmv"] / nl, 2),
+                "launches": agg["spmv_launches"],
+                "full_launches": agg["spmv_full_launches"],
+                "us_per_full_launch": round(1e6 * t_full, 2),
+                "full_launch_frac": round((B * per_sys + shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
+                if t_full > 0 else None,
+                "symmetric_reads": nread < info["nblocks"],
+                # context: what this fused kernel itself must move
+                "kernel_bytes_per_system": k_sys, "kernel_shared_bytes_per_launch": k_shared,
+                "kernel_frac": round(k_bytes / (agg["ms_spmv"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                if agg["ms_spmv"] > 0 else None,
+                "kernel_full_launch_frac": round((B * k_sys + k_shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
+                if t_full > 0 else None}
+
+    if agg["spmv_launches"] == 0 and agg["fused_launches"] > 0:
+        # the fused one-launch solve (small meshes) runs its SpMV inside one
+        # kernel per batch with no per-SpMV timing: no SpMV roofline is
+        # measured, and the line says so instead of reporting 0 GB/s
+        roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                    "traffic": None, "kernel": "k_solve_fused (the whole fp64 solve of a batch in one launch)",
+                    "us_per_launch": round(1e3 * agg["ms_fused"] / agg["fused_launches"], 2),
+                    "launches": agg["fused_launches"],
+                    "note": "no per-SpMV timing inside the fused launch: the SpMV roofline is not measured"}
+    return roofline
 
 
 def cpu_baseline(p, t, n, a, lam, frac, per_core=2, geom=None, full_timesteps=0, cores=0, config="C3"):
@@ -294,42 +465,35 @@ def main():
             torch.cuda.synchronize(dev)
 
     # --- this rank's timesteps --------------------------------------------
-    B = args.batch
     strong = args.fixed_timesteps > 0
-    batch_note = None
-    if not dry:
-        # a batch whose workspace (~720 B per vertex and timestep with the
-        # multigrid levels, the library's own estimate) and signal rows do
-        # not fit 85 % of this GPU's free HBM is reduced -- to the largest
-        # multiple of 256 that fits, then halved below 256 -- and said so,
-        # rather than failing an allocation mid-run
-        free_b, _ = torch.cuda.mem_get_info(local)
-        steps_rows = (args.warmup + args.steps) if not strong else 0
-
-        def need(b):
-            rows = (steps_rows * b if not strong else args.fixed_timesteps) + 1
-            return 720.0 * N * b + 8.0 * N * rows + 16.0 * N * b
-
-        B0 = B
-        if need(B) > 0.85 * free_b and B > 256:
-            B = B // 256 * 256
-            while B > 256 and need(B) > 0.85 * free_b:
-                B -= 256
-        while B > 64 and need(B) > 0.85 * free_b:
-            B //= 2
-        if B != B0:
-            batch_note = "batch %d reduced to %d: %.0f GB of HBM free" % (B0, B, free_b / 1e9)
-        # the library clamps every batch to the largest whose launch grids
-        # fit 2^32 work-items (mof_mesh_info.max_batch); say so here
-        if info.get("max_batch") and B > info["max_batch"]:
-            B1, B = B, int(info["max_batch"])
-            batch_note = (batch_note + "; " if batch_note else "") + \
-                "batch %d reduced to %d: launch grids past 2^32 work-items" % (B1, B)
-            print("[bench] " + batch_note, file=sys.stderr, flush=True)
     if strong:
         # the fixed job, split over the ranks; a step solves all of it
         k_off, k_end = rank_k_range(rank, world, 0, args.fixed_timesteps)
-        K_rank = k_end - k_off
+        K_strong = k_end - k_off
+    if dry:
+        # dry runs size the batch as a GPU run would, against this rank's
+        # simulated free HBM (MOF_BENCH_DRYRUN_FREE_GB: one value, or one
+        # per rank; default the MI355X's 288 GB) and no grid cap
+        fg = os.environ.get("MOF_BENCH_DRYRUN_FREE_GB", "288").split(",")
+        free_b, max_batch = float(fg[min(rank, len(fg) - 1)]) * 1e9, None
+    else:
+        free_b, _ = torch.cuda.mem_get_info(local)
+        max_batch = info.get("max_batch")
+    B, batch_note = size_batch(args.batch, N, free_b, max_batch,
+                               (lambda b: K_strong + 1) if strong else
+                               (lambda b: (args.warmup + args.steps) * b + 1))
+    # every rank runs the smallest rank's batch, so the line rank 0 prints
+    # (batch, timesteps per step) holds for every rank
+    cdev = torch.device("cpu") if (rehearse or dry) else torch.device("cuda", local)
+    B_rank = B
+    B = int(-max_over_ranks(-B, dist, cdev))
+    if B != B_rank:
+        batch_note = (batch_note + "; " if batch_note else "") + \
+            "batch %d reduced to %d: the smallest rank's batch" % (B_rank, B)
+    if batch_note and rank == 0:
+        print("[bench] " + batch_note, file=sys.stderr, flush=True)
+    if strong:
+        K_rank = K_strong
     else:
         K_rank = (args.warmup + args.steps) * B
         k_off, _ = rank_k_range(rank, world, 0, world * K_rank)
@@ -435,7 +599,6 @@ def main():
                 I0k, I1k = I_dev[k].cpu().numpy(), I_dev[k + 1].cpu().numpy()
             samples.append((k_off + k, I0k, I1k, float(tk[k + 1] - tk[k]), Vk))
     kept.clear()
-    cdev = torch.device("cpu") if (rehearse or dry) else dev
     elapsed = max_over_ranks(elapsed, dist, cdev)
     agg["failed"] = int(sum_over_ranks(agg["failed"], dist, cdev))
     agg["recovered"] = int(sum_over_ranks(agg["recovered"], dist, cdev))
@@ -445,64 +608,12 @@ def main():
     rank_ranges = None
     if dry and dist:
         got = [None] * world
-        dist.all_gather_object(got, [k_off, k_off + K_rank, agg["systems"]])
+        dist.all_gather_object(got, [k_off, k_off + K_rank, agg["systems"], B_rank, opts["batch"]])
         rank_ranges = got
     elif dry:
-        rank_ranges = [[k_off, k_off + K_rank, agg["systems"]]]
+        rank_ranges = [[k_off, k_off + K_rank, agg["systems"], B_rank, opts["batch"]]]
 
-    # roofline of the dominant kernel (k_pcg_spmv), live over the timed region:
-    # every timed launch is charged with the systems it processed, in
-    # SURVEY.md 8(d)'s algorithmic bytes of a batched CSR SpMV
-    #   B nnz s_v + 4 nnz + 4 (R + 1) + B R (s_x + s_y)   (nnz = 4 nblocks, R = 2N)
-    achieved = agg["spmv_bytes"] / (agg["ms_spmv"] * 1e-3) / 1e9 if agg["ms_spmv"] > 0 else 0.0
-    kname = "k_pcg_spmv<%s, false>" % ("float" if precision == "mixed" else "double")
-    traffic, traffic_src = pmc_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), kname)
-    sv = 4 if precision == "mixed" else 8
-    nnz, R = 4 * info["nblocks"], 2 * N
-    per_sys = nnz * sv + R * 2 * sv
-    shared = 4 * nnz + 4 * (R + 1)
-    nl = max(1, agg["spmv_launches"])
-    nfull = max(1, agg["spmv_full_launches"])
-    t_full = agg["ms_spmv_full"] / nfull * 1e-3 if agg["ms_spmv_full"] > 0 else 0.0
-    # launches that did work (the shared bytes are charged once each)
-    n_work = round((agg["spmv_bytes"] - agg["spmv_systems"] * per_sys) / shared) if agg["spmv_bytes"] else 0
-    # the kernel's own traffic: the fp32 operator's diagonal + upper blocks
-    # (lower ones read as transposes through the shared mirror table), z
-    # gathered, q, p and x read and written; shared column indices (+ mirror)
-    nread = info.get("blocks_read", info["nblocks"]) if precision == "mixed" else info["nblocks"]
-    k_sys = nread * 4 * sv + N * 2 * sv * 7
-    k_shared = info["nblocks"] * 4 * (2 if nread < info["nblocks"] else 1)
-    k_bytes = agg["spmv_systems"] * k_sys + n_work * k_shared
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": traffic_src, "kernel": kname,
-                "bytes_formula": "SURVEY.md 8(d): B*nnz*s_v + 4*nnz + 4*(R+1) + B*R*(s_x+s_y)",
-                "bytes_per_launch": round(agg["spmv_bytes"] / nl),
-                "bytes_per_system": per_sys, "shared_bytes_per_launch": shared,
-                "systems_per_launch": round(agg["spmv_systems"] / nl, 2),
-                "us_per_launch": round(1e3 * agg["ms_spmv"] / nl, 2),
-                "launches": agg["spmv_launches"],
-                "full_launches": agg["spmv_full_launches"],
-                "us_per_full_launch": round(1e6 * t_full, 2),
-                "full_launch_frac": round((B * per_sys + shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
-                if t_full > 0 else None,
-                "symmetric_reads": nread < info["nblocks"],
-                # context: what this fused kernel itself must move
-                "kernel_bytes_per_system": k_sys, "kernel_shared_bytes_per_launch": k_shared,
-                "kernel_frac": round(k_bytes / (agg["ms_spmv"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                if agg["ms_spmv"] > 0 else None,
-                "kernel_full_launch_frac": round((B * k_sys + k_shared) / t_full / 1e9 / HBM_PEAK_GBS, 4)
-                if t_full > 0 else None}
-
-    if agg["spmv_launches"] == 0 and agg["fused_launches"] > 0:
-        # the fused one-launch solve (small meshes) runs its SpMV inside one
-        # kernel per batch with no per-SpMV timing: no SpMV roofline is
-        # measured, and the line says so instead of reporting 0 GB/s
-        roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                    "traffic": None, "kernel": "k_solve_fused (the whole fp64 solve of a batch in one launch)",
-                    "us_per_launch": round(1e3 * agg["ms_fused"] / agg["fused_launches"], 2),
-                    "launches": agg["fused_launches"],
-                    "note": "no per-SpMV timing inside the fused launch: the SpMV roofline is not measured"}
+    roofline = spmv_roofline(agg, info, N, precision, precond, B, args.config)
 
     # host-to-host leg (SURVEY.md 8(d)'s metric: host I -> host V_k, the
     # reference's submit -> join, compute_optical_flow.py:160-182), measured in
@@ -528,11 +639,38 @@ def main():
                           "(SURVEY.md 8(d) metric; reference timer compute_optical_flow.py:160-182)"}
         del Vh, I_h
 
+    # extra configurations on this GPU (--legs; a 1-GPU C3 line by default:
+    # F3 and S1s, the reference's mesh class), after the main mesh is freed
+    legs, leg_jobs = [], []
+    leg_names = ([] if args.legs == "none" else
+                 (["F3", "S1s"] if args.config == "C3" else []) if args.legs == "auto" else
+                 [x for x in args.legs.split(",") if x])
+    if world > 1 or dry or host_io:
+        leg_names = []
+    if leg_names:
+        del I_dev, V_dev
+        mesh.close()
+        torch.cuda.empty_cache()
+        for name in leg_names:
+            if name not in LEGS:
+                raise SystemExit("bench.py: --legs knows %s" % ",".join(sorted(LEGS)))
+            leg, mesh_l, smp = run_leg(name, args, torch, local)
+            legs.append(leg)
+            leg_jobs.append((mesh_l, smp))
+
     cpu = geom = None
     if rank == 0 and not dry and (not args.no_cpu_baseline or samples):
         import oracle
         geom = oracle.geometry(p, n, t, a)
-    parity = parity_check(geom, t, a, args.lambda_, samples) if samples else None
+    jobs = [(geom, t, a, args.lambda_, samples)] if samples else []
+    if leg_jobs and args.parity_samples > 0:
+        import oracle
+        for (pl, tl, nl_, al), smp in leg_jobs:
+            jobs.append((oracle.geometry(pl, nl_, tl, al), tl, al, args.lambda_, smp))
+    par = parity_checks(jobs) if jobs else []
+    parity = par[0] if samples else None
+    for i, leg in enumerate(legs):
+        leg["parity"] = par[i + (1 if samples else 0)] if args.parity_samples > 0 else None
     if rank == 0 and not args.no_cpu_baseline and not dry:
         cpu = cpu_baseline(p, t, n, a, args.lambda_, args.cpu_sample_frac, args.cpu_timesteps_per_core, geom=geom,
                            full_timesteps=args.fixed_timesteps if args.config in SMALL_JOBS else 0,
@@ -562,6 +700,7 @@ def main():
             "step_traffic": step_traffic("%s/%s/%s/B%d" % (args.config, precision, precond, B), value),
             "host_io": host_leg,
             "parity": parity,
+            "legs": legs or None,
             "cpu_baseline": cpu,
             "solver": {"pcg_iterations_per_timestep": round(agg["iterations"] / n_local, 1),
                        "failed": agg["failed"], "recovered": agg["recovered"],
@@ -593,6 +732,15 @@ def main():
             line["defect"] = defect
         if parity is not None and parity["max_abs_err"] > parity["bar"] * max(1.0, parity["max_abs_V"]):
             line["defect"] = dict(defect or {}, parity=parity["max_abs_err"])
+        for leg in legs:  # the legs' solver defects and parity, as the main line's
+            lp, ls = leg.get("parity"), leg["solver"]
+            bad = {}
+            if ls["recovered"] or ls["failed"]:
+                bad.update(recovered=ls["recovered"], failed=ls["failed"])
+            if lp is not None and lp["max_abs_err"] > lp["bar"] * max(1.0, lp["max_abs_V"]):
+                bad["parity"] = lp["max_abs_err"]
+            if bad:
+                line["defect"] = dict(line.get("defect") or {}, **{leg["config"]: bad})
         if dry:
             line["dry_run"] = True
             line["rank_ranges"] = rank_ranges
@@ -600,7 +748,9 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-    if rank == 0 and "defect" in line and not (args.allow_recovery and "parity" not in line["defect"]):
+    parity_bad = rank == 0 and "defect" in line and (
+        "parity" in line["defect"] or any(isinstance(v, dict) and "parity" in v for v in line["defect"].values()))
+    if rank == 0 and "defect" in line and not (args.allow_recovery and not parity_bad):
         print("[bench] defect: %s" % json.dumps(line["defect"]), file=sys.stderr, flush=True)
         return 3
     return 0

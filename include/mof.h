@@ -67,9 +67,9 @@ extern "C" {
                                   once per mesh; meshes of <= 64 vertices
                                   keep block Jacobi). Smoother damping:
                                   0.85 on the fine level, 1.05 on the coarse
-                                  levels; the environment variables
-                                  MOF_AMG_OMEGA / MOF_AMG_OMEGA1, read when
-                                  the hierarchy is built, override them */
+                                  levels; the environment variable
+                                  MOF_AMG_OMEGA=w0[,w1], read when the
+                                  hierarchy is built, overrides them */
 #define MOF_NO_RECOVERY 16u    /* systems whose solve fails (breakdown,
                                   divergence, stagnation, max_iter) are
                                   NaN-filled at once. Default: they are
@@ -94,8 +94,7 @@ extern "C" {
                                   kernels' bodies run row block by row block;
                                   bit-identical V, flags and iteration
                                   counts). Default: on for meshes of at most
-                                  16 row blocks of 256 vertices
-                                  (MOF_FUSED_MAX_BLK), where the eager
+                                  16 row blocks of 256 vertices, where the eager
                                   launches are latency-bound */
 #define MOF_SOLVE_EAGER 256u   /* never the fused solve */
 

@@ -105,20 +105,18 @@ void sell_to_csr(const mof_mesh *m, const std::vector<double> &blk, int32_t drop
     *nnz_out = nnz;
 }
 
-int env_int(const char *name, int dflt) {
-    const char *v = std::getenv(name);
-    return (v && *v) ? std::atoi(v) : dflt;
-}
-
 // Pinned ring, copy stream and the two device slots of a host-pointer solve
 // (mof_hostio.h); kept on the handle across calls.
 // The ring's chunk follows the job: a quarter of the larger per-batch
-// transfer in whole MiB, at most MOF_STAGE_MB (32): pinning the 4 x 32 MiB
+// transfer in whole MiB, at most stage_cap() (32): pinning the 4 x 32 MiB
 // ring took tens of ms -- longer than a 3k-vertex, 97-timestep job's whole
 // solve. A later, larger job replaces the stage. direct: only the device
 // slots (the batches' copies run on the compute stream, solve_batches).
+// MOF_STAGE_MB (MiB, default 32): the ring's largest chunk
+size_t stage_cap() { return (size_t)std::max(1, mof::knob_int(mof::Knob::StageMB, 32)) << 20; }
+
 void host_io_prepare(mof_mesh *m, int64_t in_elems, int64_t out_elems, bool direct) {
-    const size_t mib = (size_t)1 << 20, cap = (size_t)std::max(1, env_int("MOF_STAGE_MB", 32)) * mib;
+    const size_t mib = (size_t)1 << 20, cap = stage_cap();
     const size_t larger = (size_t)std::max(in_elems, out_elems) * sizeof(double);
     const size_t want = std::min(cap, (larger / 4 + mib - 1) / mib * mib);
     if (!direct && m->stage && m->stage->chunk() < want) {
@@ -154,9 +152,9 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     mof::SolveParams sp = sp_in;
     const int32_t K = k1 - k0;
     const int32_t nbat = (K + B - 1) / B;
-    // MOF_HOSTIO_VERBOSE: helper-thread and wait times, and the call's setup
-    // steps, on stderr
-    const bool hostio_verbose = env_int("MOF_HOSTIO_VERBOSE", 0) != 0;
+    // MOF_VERBOSE: helper-thread and wait times, and the call's setup steps,
+    // on stderr
+    const bool hostio_verbose = mof::knob(mof::Knob::Verbose) != nullptr;
     double tp[5];
     tp[0] = now_ms();
     mof::ensure_workspace(m, B, sp.precision);
@@ -184,12 +182,13 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     // passes I_k twice), else nb rows of each
     const bool shared_I = (I2 == I);
     const int64_t in_rows = shared_I ? B + 1 : 2 * (int64_t)B;
-    // host transfers of at most MOF_STAGE_DIRECT_MB (16) per batch: straight
-    // pageable copies on the compute stream (the runtime stages them), no
-    // copy stream, helper thread or pinned ring -- creating those cost a
-    // small job 4-12 ms, more than its solve (S1s: 3.8 ms)
+    // host transfers of at most 16 MiB per batch (half the ring's chunk cap
+    // when MOF_STAGE_MB sets it lower): straight pageable copies on the
+    // compute stream (the runtime stages them), no copy stream, helper thread
+    // or pinned ring -- creating those cost a small job 4-12 ms, more than its
+    // solve (S1s: 3.8 ms)
     const bool direct = !dev_io && (size_t)std::max(in_rows, 2 * (int64_t)B) * N * sizeof(double) <=
-                                       ((size_t)std::max(0, env_int("MOF_STAGE_DIRECT_MB", 16)) << 20);
+                                       std::min<size_t>((size_t)16 << 20, stage_cap() / 2);
     if (!dev_io) host_io_prepare(m, in_rows * N, 2 * N * B, direct);
     tp[4] = now_ms();
     if (hostio_verbose)
@@ -369,8 +368,8 @@ void recover_systems(int32_t nb, const SolveParams &sp, int32_t user_max_iter, c
     int32_t nfirst = 0;
     for (int32_t b = 0; b < nb; ++b) nfirst += (first[b] = failed(b));
     if (!nfirst) return;
-    // MOF_SOLVE_VERBOSE: why and when the first solve's failed systems failed
-    if (std::getenv("MOF_SOLVE_VERBOSE")) {
+    // MOF_VERBOSE: why and when the first solve's failed systems failed
+    if (knob(Knob::Verbose)) {
         int32_t why[8] = {0}, itmin = 1 << 30, itmax = 0;
         for (int32_t b = 0; b < nb; ++b)
             if (first[b]) {
@@ -435,8 +434,7 @@ void mesh_set_own(mof_mesh *m, int32_t nown) {
     MOF_HIP(hipSetDevice(m->device));
     m->n_own = nown;
     // MOF_SYM_READS: 1 / 0 force the symmetric / plain reads, unset: per mesh
-    const char *env = std::getenv("MOF_SYM_READS");
-    const int sym = env && *env ? (std::atoi(env) != 0) : -1;
+    const int sym = knob(Knob::SymReads) ? (knob_int(Knob::SymReads, 0) != 0) : -1;
     // one host mirror table per (mesh, nown, mode), shared by the clones
     std::shared_ptr<const MirrorTable> mt;
     {
@@ -501,9 +499,7 @@ void mesh_prepare_host(mof_mesh *m, const double *xyz, const double *nrm, const 
             // Wider windows pad less (512 / 1024 / 2048 rows: ≈1.24 / 1.20 /
             // 1.18 M slots) but scatter the gathers: R3 687 / 676 / 670 vs
             // 696 timesteps/s (round 3, profiles/r03_ab/r3win*).
-            // MOF_WINDOW_SORT=0/1 forces either.
-            const char *ws = std::getenv("MOF_WINDOW_SORT");
-            const bool wsort = ws && *ws ? std::atoi(ws) != 0 : mof::amg_auto_smooth(adj);
+            const bool wsort = mof::amg_auto_smooth(adj);
             if (wsort) {
                 std::vector<int32_t> byrcm(N);  // byrcm[rcm position] = caller vertex
                 for (int32_t i = 0; i < N; ++i) byrcm[m->perm[i]] = i;
@@ -707,7 +703,7 @@ int mof_mesh_clone(const mof_mesh *src, int32_t device, mof_mesh **out) {
 int mof_mesh_destroy(mof_mesh *m) {
     if (!m) return MOF_OK;
     return guarded([&] {
-        if (m->prep.valid()) m->prep.wait();  // its error, if any, dies with the handle
+        mof::mesh_join_prep(m);  // its error, if any, dies with the handle
         {
             DeviceGuard dg(m->device);
             if (m->stream) (void)hipStreamSynchronize(m->stream);
@@ -738,13 +734,15 @@ int mof_mesh_destroy(mof_mesh *m) {
 int mof_mesh_prepare(mof_mesh *m, const mof_opts *opts) {
     return guarded([&] {
         MOF_REQUIRE(m, "mesh is NULL");
-        mof::mesh_join_prep(m);
         mof_opts o{};
         if (opts) {
             MOF_REQUIRE(opts->struct_size == 0 || opts->struct_size >= sizeof(mof_opts),
                         "mof_opts.struct_size too small");
             o = *opts;
         }
+        mof::mesh_join_prep(m);
+        std::lock_guard<std::mutex> lk(m->prep_mu);
+        m->prep_err = nullptr;  // a new setup supersedes the last one's error
         if (!(o.flags & MOF_PRECOND_AMG) || o.precision != MOF_PREC_MIXED || m->n_own != m->N) return;
         m->prep = std::async(std::launch::async, [m] {
             DeviceGuard dg(m->device);
@@ -756,7 +754,7 @@ int mof_mesh_prepare(mof_mesh *m, const mof_opts *opts) {
 int mof_mesh_sync(mof_mesh *m) {
     return guarded([&] {
         MOF_REQUIRE(m, "mesh is NULL");
-        mof::mesh_join_prep(m);
+        mof::mesh_join_prep(m, true);
     });
 }
 
@@ -863,7 +861,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
     int rc = guarded([&] {
         MOF_REQUIRE(m && I && t_k && V_out, "NULL argument");
         MOF_REQUIRE(T >= 1 && k0 >= 0 && k0 <= k1 && k1 <= T - 1, "need 0 <= k0 <= k1 <= T-1");
-        mof::mesh_join_prep(m);
+        mof::mesh_join_prep(m);  // its error: below, for the multigrid solve
         mof_opts o{};
         if (opts) {
             MOF_REQUIRE(opts->struct_size == 0 || opts->struct_size >= sizeof(mof_opts),
@@ -875,6 +873,7 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         sp.precision = o.precision;
         sp.amg = (o.flags & MOF_PRECOND_AMG) != 0;
         MOF_REQUIRE(!sp.amg || o.precision == MOF_PREC_MIXED, "MOF_PRECOND_AMG needs MOF_PREC_MIXED");
+        if (sp.amg) mof::mesh_join_prep(m, true);  // the multigrid setup's error, if any
         // the multigrid smoother is the 2x2 block Jacobi
         sp.block_jacobi = sp.amg || !(o.flags & MOF_NO_BLOCK_JACOBI);
         sp.time_spmv = (o.flags & MOF_TIME_SPMV) != 0;
@@ -886,9 +885,8 @@ int mof_solve_range(mof_mesh *m, const double *I, const double *I2, const double
         sp.etol = o.etol > 0 ? o.etol : (o.etol < 0 ? 0.0 : 1e-7);
         // a multigrid-preconditioned inner solve takes tens of iterations:
         // one that stops improving, or hits max_iter, has a bad preconditioner
-        sp.stall = sp.amg ? env_int("MOF_PCG_STALL", 64) : 0;
+        sp.stall = sp.amg ? mof::kPcgStall : 0;
         sp.fail_at_max_iter = sp.amg;
-        sp.adaptive_inner = env_int("MOF_FIXED_INNER_RTOL", 0) == 0;
         sp.fused = (o.flags & MOF_SOLVE_EAGER) ? 0 : ((o.flags & MOF_SOLVE_FUSED) ? 1 : -1);
         const bool recovery = !(o.flags & MOF_NO_RECOVERY);
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;

@@ -146,13 +146,8 @@ struct AmgDevice {
     // level 1 visits the coarser levels twice per cycle (S C S C S at level
     // 1, a palindrome of symmetric steps: the preconditioner stays SPD)
     bool wcycle = false;
-    // block-Jacobi sweeps per side on the separate coarse levels (1 .. the
-    // first fused one); MOF_AMG_NU1. 2 (one box, profiles/r05_ab/nu1/): PCG
-    // its per timestep S1 44.8 -> 43.1, R3 41.8 -> 40.9, C3 17.0 -> 15.7,
-    // F3 26.2 -> 23.0; timesteps/s 1076 -> 1018, 944 -> 842, 3688 -> 3542,
-    // 2488 -> 2515 (the CPU prototype's 17 % fewer S1 its to 1e-4 did not
-    // carry over to the refinement's inner solves): 1
-    int32_t nu1 = 1;
+    // (one block-Jacobi sweep per side on the coarse levels; 2 measured in
+    // round 5, profiles/r05_ab/nu1/: fewer its, fewer timesteps/s but on F3)
     // open surfaces: extra level-0 sweeps on the boundary rows and their
     // neighbour ring (k_bsweep); bsw_n rows (0: none), bsw_pos[N] = the row's
     // index in bsw_rows or -1

@@ -1775,13 +1775,17 @@ bool amg_build(mof_mesh *m) {
         prm.omega = 0.7f;
         prm.smooth = 1;
     }
-    if (const char *v = std::getenv("MOF_AMG_OMEGA")) prm.omega = (float)std::atof(v);  // tuning knobs
-    if (const char *v = std::getenv("MOF_AMG_OMEGA1")) prm.omega1 = (float)std::atof(v);
-    if (const char *v = std::getenv("MOF_AMG_SMOOTH")) prm.smooth = std::atoi(v);  // 1 / 0 force, unset auto
-    // level 1's smoothed prolongator: -1 auto (below: folded closed
-    // surfaces), MOF_AMG_SMOOTH1=1 / 0 forces
+    // MOF_AMG_OMEGA = w0[,w1]: the fine [and coarse] smoother damping
+    float omega1_set = 0.f;
+    if (const char *v = knob(Knob::AmgOmega)) {
+        char *end = nullptr;
+        prm.omega = std::strtof(v, &end);
+        if (end && *end == ',') omega1_set = prm.omega1 = std::strtof(end + 1, nullptr);
+    }
+    if (knob(Knob::AmgSmooth)) prm.smooth = knob_int(Knob::AmgSmooth, 0) != 0;  // 1 / 0 force, unset auto
+    // level 1's smoothed prolongator: auto (below: where level 0 is smoothed,
+    // and folded closed surfaces)
     prm.smooth1 = -1;
-    if (const char *v = std::getenv("MOF_AMG_SMOOTH1")) prm.smooth1 = std::atoi(v);
     if (m->n_own < m->N) prm.nown = m->n_own;
     if (m->amg && m->amg->built) return m->amg->lv.size() >= 2;
     if (!m->amg) m->amg = new AmgDevice();
@@ -1861,8 +1865,7 @@ bool amg_build(mof_mesh *m) {
     G.omega1 = prm.omega1;
     // level 0's corrected iterate x0 + Q y: bf16 in place on meshes with the
     // tentative prolongator (C3 +3.8 %, C2 mixed +3.3 %, same iterations),
-    // fp32 with the smoothed one (R3: bf16 costs 54.5 vs 50 its, -5 %);
-    // MOF_X_BF16=0/1 forces either
+    // fp32 with the smoothed one (R3: bf16 costs 54.5 vs 50 its, -5 %)
     G.xm = 2;
     G.lv.clear();
     G.built = true;
@@ -1879,8 +1882,7 @@ bool amg_build(mof_mesh *m) {
     // coarse-level damping: 1.1 on regular meshes (round 2, C3 17.2 -> 17.0
     // its, +1.8 %; C2 mixed +2 %), 1.05 otherwise (R3 as measured; 1.2
     // diverges there with the tentative P)
-    if (!std::getenv("MOF_AMG_OMEGA1")) G.omega1 = G.regular ? 1.1f : 1.05f;
-    if (const char *v = std::getenv("MOF_X_BF16")) G.xm = std::atoi(v) ? 1 : 2;
+    if (omega1_set <= 0.f) G.omega1 = G.regular ? 1.1f : 1.05f;
     // level 1 visiting the levels below twice (W): measured, not the default.
     // Round 5, same box (profiles/r05_ab/wcycle/): S1 (open) 858 -> 905
     // timesteps/s (59.5 -> 47.2 PCG its), F3 (folded) 1727 -> 1934 (40.5 ->
@@ -1889,8 +1891,6 @@ bool amg_build(mof_mesh *m) {
     // MOF_AMG_W=1 forces it.
     G.wcycle = false;
     if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
-    G.nu1 = 1;
-    if (const char *v = std::getenv("MOF_AMG_NU1")) G.nu1 = std::max(1, std::min(4, std::atoi(v)));
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
@@ -1911,11 +1911,13 @@ bool amg_build(mof_mesh *m) {
     // launches more per cycle on a launch-bound mesh); S1 (ring 2 %) 44.8 ->
     // 42.9 its, 1151-1154 -> 1142-1147 (the CPU prototype's 10 -> 9 its to
     // 1e-4, tools/amg_proto.py bsw=2). MOF_AMG_BSW = sweeps per side (0 off)
-    // forces it on any open surface.
+    // forces it on any open surface whose ring fits the sweep kernel's LDS
+    // (kBswMax rows; a larger ring keeps no boundary sweeps, said under
+    // MOF_VERBOSE).
     G.bsw_n = 0;
     G.bsw_sweeps = 0;
     int32_t bsw = -1;
-    if (const char *v = std::getenv("MOF_AMG_BSW")) bsw = std::max(0, std::min(8, std::atoi(v)));
+    if (knob(Knob::AmgBsw)) bsw = std::max(0, std::min(8, knob_int(Knob::AmgBsw, 0)));
     if (open_surface && bsw != 0) {
         const Pattern &P = m->pat;
         std::vector<uint8_t> mark(m->N, 0);
@@ -1935,6 +1937,9 @@ bool amg_build(mof_mesh *m) {
                 rows.push_back(i);
             }
         const bool want = bsw > 0 || 20 * (int64_t)rows.size() >= m->N;
+        if (want && rows.size() > (size_t)kBswMax && knob(Knob::Verbose))
+            std::fprintf(stderr, "mof amg: boundary ring of %zu rows exceeds the sweep kernel's %d: no boundary sweeps\n",
+                         rows.size(), kBswMax);
         if (want && !rows.empty() && rows.size() <= (size_t)kBswMax) {
             put_i(G.bsw_rows, rows);
             put_i(G.bsw_pos, pos);
@@ -1985,9 +1990,8 @@ bool amg_build(mof_mesh *m) {
             D.ngrp = (int32_t)grp.size() - 1;
             put_i(D.rgrp, grp);
             // smoothed P: each group's list entries by fine node (stable), for
-            // k_restrict0_sa's gathers; MOF_RESTR_SORT=0: list order
-            const char *rs = std::getenv("MOF_RESTR_SORT");
-            if (L.smoothed && !(rs && *rs && std::atoi(rs) == 0)) {
+            // k_restrict0_sa's gathers (same bits as list order)
+            if (L.smoothed) {
                 std::vector<int32_t> perm(L.rent.size() / 2);
                 for (int32_t g = 0; g + 1 < (int32_t)grp.size(); ++g) {
                     const int32_t e0 = L.rptr[grp[g]], e1 = L.rptr[grp[g + 1]];
@@ -1999,18 +2003,11 @@ bool amg_build(mof_mesh *m) {
             }
             // tentative P (every level but a smoothed level 0): coarse position
             // ranges of <= kWG gather entries and positions for the products by
-            // entry, k_galerkin0_ent / k_galerkin3_ent (unless a single
-            // position has more, or MOF_GAL_ENT=0)
-            // MOF_GAL_ENT=0: no product by entry; MOF_GAL3_ENT=0: level 0 only
-            const char *ge = std::getenv("MOF_GAL_ENT");
-            const char *ge3 = std::getenv("MOF_GAL3_ENT");
-            const bool ent_here = l == 0 || !(ge3 && *ge3 && std::atoi(ge3) == 0);
-            // Levels >= 1: positions past kGalBig entries (MOF_GAL_BIG: the
-            // threshold, 0 = none, i.e. a level with a position past kWG
-            // keeps the per-position product) go to k_galerkin3_big.
-            if ((!L.smoothed || l >= 1) && ent_here && !(ge && *ge && std::atoi(ge) == 0)) {
-                const char *gb = std::getenv("MOF_GAL_BIG");
-                const int32_t big = l == 0 ? 0 : std::min<int32_t>(kWG, gb && *gb ? std::atoi(gb) : kGalBig);
+            // entry, k_galerkin0_ent / k_galerkin3_ent (unless a level-0
+            // position has more). Levels >= 1: positions past kGalBig entries
+            // go to k_galerkin3_big.
+            if (!L.smoothed || l >= 1) {
+                const int32_t big = l == 0 ? 0 : std::min<int32_t>(kWG, kGalBig);
                 const std::vector<int32_t> &gq = L.gptr;
                 const int32_t npos = (int32_t)gq.size() - 1;
                 bool ok = true;
@@ -2046,7 +2043,7 @@ bool amg_build(mof_mesh *m) {
     }
     G.nc = H.coarse_dofs;
     G.cap = 0;
-    if (std::getenv("MOF_AMG_VERBOSE")) {
+    if (knob(Knob::Verbose)) {
         for (size_t l = 0; l < H.levels.size(); ++l)
             std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld%s curl %.3f%s\n", l,
                          H.levels[l].n, H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb(),
@@ -2055,13 +2052,6 @@ bool amg_build(mof_mesh *m) {
     }
     MOF_HIP(hipStreamSynchronize(s));
     return true;
-}
-
-// the smoothed level-0 Galerkin product by system slab (k_a_slab, k_galerkin_sys);
-// MOF_GAL0_SYS=0 or MOF_SA_GAL_BF16: the per-position k_galerkin0_ns
-static bool gal0_sys() {
-    const char *e = std::getenv("MOF_GAL0_SYS");
-    return !(e && *e && std::atoi(e) == 0) && !std::getenv("MOF_SA_GAL_BF16");
 }
 
 void amg_ensure(mof_mesh *m, int32_t B) {
@@ -2077,15 +2067,15 @@ void amg_ensure(mof_mesh *m, int32_t B) {
             D.r.alloc(n * B);  // bf16 pairs (ldr<2>)
             G.A0h.alloc((size_t)(2 * m->pat.sell_nb() * B));  // 8 B per block
             G.A0h.zero(s);  // SELL padding: never written by the assembly, read as 0
-            if (D.smoothed && gal0_sys() && G.aslab.n == 0) G.aslab.alloc((size_t)4 * kSlab * m->pat.sell_nb());
+            // the smoothed level-0 Galerkin product by system slab (k_a_slab,
+            // k_galerkin_sys)
+            if (D.smoothed && G.aslab.n == 0) G.aslab.alloc((size_t)4 * kSlab * m->pat.sell_nb());
         } else {
             D.A.alloc((size_t)kB3 * D.sell_nb * B);
             D.A.zero(s);
-            const char *g1 = std::getenv("MOF_GAL1_SYS");
             // (a level 1 of the fused tiny levels keeps its product by entry:
             // S1s, 400 nodes, 25050 -> 26450 timesteps/s without the chain)
-            if (l == 1 && G.aslab.n > 0 && G.lv.size() >= 3 && D.n > kSubNodes && D.slab.n == 0 &&
-                !(g1 && *g1 && std::atoi(g1) == 0))
+            if (l == 1 && G.aslab.n > 0 && G.lv.size() >= 3 && D.n > kSubNodes && D.slab.n == 0)
                 D.slab.alloc((size_t)kB3 * kSlab * D.sell_nb);
             if (l + 1 < G.lv.size()) {  // sweep copy, st_a9 (the coarsest stays fp32)
                 D.Ah.alloc(kAhWords * D.sell_nb * B);
@@ -2191,9 +2181,7 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                                            kGrpGal)),
                              kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p,
                                           F.Q.p, w.A32.p, m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
-                                          F.smoothed && !std::getenv("MOF_SA_GAL_BF16")
-                                              ? nullptr
-                                              : reinterpret_cast<const uint2 *>(G.A0h.p));
+                                          F.smoothed ? nullptr : reinterpret_cast<const uint2 *>(G.A0h.p));
         else if (ent) {
             if (F.nggrp > 0)
                 k_galerkin3_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
@@ -2268,19 +2256,9 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     // the cycle below level 0 from level 1's restricted b and pre-smoothed
     // x: down (residual, restriction + next pre-smooth), the fused tiny
     // levels, up (prolongation, post-smoothing into y)
-    // G.nu1 sweeps per side on the separate levels >= 1: the extra ones are
-    // k_post3 sweeps (y = x + w D^-1 (b - A x)) with x and y swapped after
-    // each, so the level's view always names its latest iterate x / result y
-    // (nu1 pre- and nu1 post-sweeps of the symmetric smoother: the cycle
-    // stays symmetric)
-    const int32_t nu1 = G.wcycle ? 1 : G.nu1;
     auto coarse = [&](Lvl (&u)[kMaxLevels]) {
         for (int32_t l = 1; l < S; ++l) {
             const int32_t smooth = l + 1 < L - 1;
-            for (int32_t k = 1; k < nu1; ++k) {
-                k_post3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], om1, sysi);
-                std::swap(u[l].x, u[l].y);
-            }
             k_res3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], sysi);
             if (G.lv[l].smoothed)
                 k_restrict0_sa<3><<<dim3(xcd_grid(G.lv[l].ngrp, (nL + kNSR - 1) / kNSR, kGrpRestr)), kWG, 0, s>>>(
@@ -2306,10 +2284,6 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
             else
                 k_prolong<3><<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], u[l + 1], sysi);
             k_post3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], om1, sysi);
-            for (int32_t k = 1; k < nu1; ++k) {
-                std::swap(u[l].x, u[l].y);
-                k_post3<<<grid2(u[l].n, nL), kWG, 0, s>>>(u[l], om1, sysi);
-            }
         }
     };
     // down at level 0: residual of the pre-smoothed x, restriction (+ level

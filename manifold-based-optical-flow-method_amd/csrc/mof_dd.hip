@@ -58,7 +58,7 @@ RcclApi *rccl_open() {
     if (api.h) return &api;
     MOF_REQUIRE(!tried, "librccl could not be loaded");
     tried = true;
-    const char *env = getenv("MOF_RCCL_LIB");
+    const char *env = knob(Knob::RcclLib);
     const char *names[] = {env, "librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
     for (const char *n : names) {
         if (!n) continue;
@@ -732,11 +732,6 @@ int mof_dd_get_info(const mof_dd *d, mof_dd_info *info) {
     });
 }
 
-static int env_int_dd(const char *name, int dflt) {
-    const char *v = std::getenv(name);
-    return (v && *v) ? std::atoi(v) : dflt;
-}
-
 int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const double *t_k, int32_t T, int32_t k0,
                        int32_t k1, double lambda, const mof_opts *opts, double *V_out, mof_stats *stats) {
     return mof_io_guard([&] {
@@ -765,7 +760,7 @@ int mof_dd_solve_range(mof_dd *d, const double *I, const double *I2, const doubl
         sp.inner_rtol = o.inner_rtol > 0 ? o.inner_rtol : 1e-4;
         // error control: etol 0 -> 1e-7 of max|V|, < 0 -> off
         sp.etol = o.etol > 0 ? o.etol : (o.etol < 0 ? 0.0 : 1e-7);
-        sp.stall = sp.amg ? env_int_dd("MOF_PCG_STALL", 64) : 0;
+        sp.stall = sp.amg ? kPcgStall : 0;
         sp.fail_at_max_iter = sp.amg;
         const bool recovery = !(o.flags & MOF_NO_RECOVERY);
         const bool dev_io = (o.flags & MOF_IO_DEVICE) != 0;

@@ -78,10 +78,7 @@ void CopyPool::copy(void *dst, const void *src, size_t bytes) {
 }
 
 int32_t stage_threads() {
-    for (const char *var : {"MOF_IO_THREADS", "OMP_NUM_THREADS"}) {
-        const char *v = std::getenv(var);
-        if (v && std::atoi(v) > 0) return std::min(std::atoi(v), 16);
-    }
+    if (const int32_t t = knob_threads(16)) return t;
     const unsigned hc = std::thread::hardware_concurrency();
     return (int32_t)std::min(16u, std::max(1u, hc));
 }

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/mof.h"
+#include "mof_knobs.h"
 
 namespace mof {
 
@@ -169,10 +170,13 @@ struct Workspace {
 //  the refinement steps taken (the eager path counts these on the host)
 //  SD_EST / SD_XMAX: the error estimate after the last refinement step,
 //  max|d| |r_{k+1}| / |r_k| (k_outer_check), and max|x64| (error control)
+//  SI_MET: the last outer check found rel <= rtol (the system only stayed
+//  active for the error estimate): a later inner solve that fails leaves
+//  x64 at that iterate, and the system retires instead of failing
 enum SysD { SD_TOL2 = 0, SD_RR = 1, SD_FF = 2, SD_REL = 3, SD_RR0 = 4, SD_BEST = 5, SD_OUTER = 6, SD_EST = 7,
             SD_XMAX = 8 };
 enum SysI { SI_CONV = 0, SI_ACTIVE = 1, SI_FAILED = 2, SI_ITSUM = 3, SI_BEST_IT = 4, SI_FAIL_IT = 5, SI_FAIL_WHY = 6,
-            SI_ITMAX = 7 };
+            SI_ITMAX = 7, SI_MET = 8 };
 enum FailWhy { FW_BREAKDOWN = 1, FW_DIVERGED = 2, FW_STALLED = 3, FW_MAXITER = 4, FW_RESIDUAL = 5 };
 constexpr int kSysStride = 12;
 
@@ -214,8 +218,12 @@ struct mof_mesh {
     int32_t N = 0, M = 0, device = 0;
     // mof_mesh_prepare's per-mesh solver setup running on a host thread;
     // every call that may use what it builds waits for it first
-    // (mof::mesh_join_prep)
+    // (mof::mesh_join_prep). prep_mu guards prep and prep_err: a handle may
+    // be cloned from several host threads while it is solved on; the
+    // setup's error is kept for the calls that need the hierarchy
+    std::mutex prep_mu;
     std::future<void> prep;
+    std::exception_ptr prep_err;
     // rows [n_own, N) are a decomposed part's ghosts (mof_dd.h): the
     // multigrid preconditioner decouples them (identity rows); N otherwise
     int32_t n_own = 0;
@@ -322,6 +330,11 @@ struct SpmvTiming {
 // (Roofline).
 double spmv_launch_bytes(const mof_mesh *m, uint32_t precision, int32_t active);
 
+// a multigrid-preconditioned inner solve takes tens of iterations: one whose
+// |r|^2 sets no new minimum for this many fails (its system goes to the
+// recovery solves)
+constexpr int32_t kPcgStall = 64;
+
 struct SolveParams {
     uint32_t precision;
     bool block_jacobi;
@@ -334,24 +347,26 @@ struct SolveParams {
     // kErrSafety) is at most etol max|x64|; 0: the residual alone
     double etol = 0.0;
     // stagnation window: an inner solve whose |r|^2 sets no new minimum for
-    // this many iterations fails (0: off)
+    // this many iterations fails (0: off; kPcgStall with the multigrid)
     int32_t stall = 0;
     // an inner solve that ends at max_iter unconverged fails the system
     // (instead of handing the partial correction to the next refinement step)
     bool fail_at_max_iter = false;
     // refinement steps after the first: per-system inner tolerance from the
-    // outer residual still missing (k_pcg_tol); MOF_FIXED_INNER_RTOL=1: off
+    // outer residual still missing (k_pcg_tol)
     bool adaptive_inner = true;
     // the whole fp64 solve of a batch in one launch, one workgroup per system
     // (k_solve_fused): 0 never, 1 when the batch is eligible, -1 auto (small
-    // meshes: row blocks <= MOF_FUSED_MAX_BLK)
+    // meshes: row blocks <= kFusedMaxBlk)
     int32_t fused = -1;
     // > 0: the multigrid's fine-level smoother damping for this solve instead
     // of the hierarchy's (the recovery's damped multigrid pass)
     float amg_omega = 0.f;
 };
-// Wait for a pending mof_mesh_prepare on the handle (rethrows its error).
-void mesh_join_prep(mof_mesh *m);
+// Wait for a pending mof_mesh_prepare on the handle (thread-safe). Its error
+// stays on the handle; take_error rethrows (and clears) it -- the calls that
+// need the multigrid hierarchy (the multigrid solve, mof_mesh_sync).
+void mesh_join_prep(mof_mesh *m, bool take_error = false);
 // The largest batch whose launch grids all stay within 2^32 - 1 work-items
 // (xcd_grid refuses a larger one): the block-level assembly pass over the
 // SELL slots of every system is the widest grid of a solve.

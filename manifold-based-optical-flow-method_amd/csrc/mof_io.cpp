@@ -48,10 +48,7 @@ namespace {
 // process's CPU share on shared hosts), else all cores; at most 64.
 int32_t pool_size(int32_t threads) {
     if (threads > 0) return std::min(threads, 256);
-    for (const char *var : {"MOF_IO_THREADS", "OMP_NUM_THREADS"}) {
-        const char *v = std::getenv(var);
-        if (v && std::atoi(v) > 0) return std::min(std::atoi(v), 64);
-    }
+    if (const int32_t t = knob_threads(64)) return t;
     const unsigned hc = std::thread::hardware_concurrency();
     return (int32_t)std::min(64u, std::max(1u, hc));
 }

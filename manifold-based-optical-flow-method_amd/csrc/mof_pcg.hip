@@ -1031,8 +1031,9 @@ __device__ __forceinline__ void outer_check_sys(const RedArgs &rd, int32_t B, co
             si[SI_FAILED] = 1;
             si[SI_ACTIVE] = 0;
             si[SI_FAIL_WHY] = FW_RESIDUAL;
-        } else if (rel <= rtol && (etol <= 0.0 || kErrSafety * est <= etol * dx[1])) {
-            si[SI_ACTIVE] = 0;
+        } else {
+            si[SI_MET] = rel <= rtol;
+            if (rel <= rtol && (etol <= 0.0 || kErrSafety * est <= etol * dx[1])) si[SI_ACTIVE] = 0;
         }
     }
 }
@@ -1056,11 +1057,21 @@ __global__ void k_sys_reset(int32_t B, int32_t *__restrict__ sysi, double *__res
 
 // Systems still active after the last refinement step fail -- except one
 // whose residual met rtol and only the error estimate did not (kept; its
-// estimate is reported through mof_stats.max_err_est).
+// estimate is reported through mof_stats.max_err_est). Likewise a system
+// whose inner solve failed in a step after its residual had met rtol
+// (SI_MET): the failed solve's correction was never added, x64 is the
+// iterate that met rtol, and the system retires with it.
+__device__ __forceinline__ void keep_met(int32_t *si) {
+    if (si[SI_FAILED] && si[SI_MET] && si[SI_FAIL_WHY] != FW_RESIDUAL) {
+        si[SI_FAILED] = 0;
+        si[SI_FAIL_WHY] = 0;
+    }
+}
 __global__ void k_mark_unconverged(int32_t B, double rtol, const double *__restrict__ sysd,
                                    int32_t *__restrict__ sysi) {
     const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
+    keep_met(sysi + b * kSysStride);
     if (sysi[b * kSysStride + SI_ACTIVE] && sysd[b * kSysStride + SD_REL] <= rtol) {
         sysi[b * kSysStride + SI_ACTIVE] = 0;
     } else if (sysi[b * kSysStride + SI_ACTIVE]) {
@@ -1253,9 +1264,9 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         }
     }
     const int64_t ps = (int64_t)B * m->ws.nblk * 2;  // part_rzrr slot stride
-    // MOF_CONV_EARLY=0: converged systems run their last V-cycle
-    const char *ce = std::getenv("MOF_CONV_EARLY");
-    const bool early = amg && !(ce && *ce && std::atoi(ce) == 0);
+    // a system converged after the update skips that iteration's V-cycle
+    // (k_pcg_conv_early; same bits: its z was never used)
+    const bool early = amg;
     // z = M^-1 r for the external preconditioner, r.z into slot `slot`
     auto precond = [&](int32_t slot) {
         if constexpr (sizeof(V) == 4)
@@ -1274,12 +1285,9 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     running_at = was_active;
     // launches over the running systems only when they are at most
     // kCompactFrac of the batch (SysMap): a later refinement step's few
-    // systems from the start, a long tail from its chunk boundary;
-    // MOF_COMPACT=0: all B
-    const char *ec = std::getenv("MOF_COMPACT");
-    const bool compact = !(ec && *ec && std::atoi(ec) == 0);
+    // systems from the start, a long tail from its chunk boundary (same bits)
     std::vector<int32_t> h_map(B);  // read by the async upload until the next fetch_flags
-    if (compact && solve_systems <= kCompactFrac * B) {
+    if (solve_systems <= kCompactFrac * B) {
         int32_t n = 0;
         for (int32_t b = 0; b < B; ++b)
             if (was_active[b]) h_map[n++] = b;
@@ -1289,9 +1297,8 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         }
     }
     // a mesh of at most kSelfRedBlk row blocks: the SpMV and the update
-    // reduce their scalars themselves (MOF_SELFRED=0: the k_red_* launches)
-    const char *esr = std::getenv("MOF_SELFRED");
-    a.selfred = a.red.P == 1 && m->ws.nblk <= kSelfRedBlk && !(esr && *esr && std::atoi(esr) == 0) ? 1 : 0;
+    // reduce their scalars themselves (same bits as the k_red_* launches)
+    a.selfred = a.red.P == 1 && m->ws.nblk <= kSelfRedBlk ? 1 : 0;
     k_pcg_init<V><<<g, kWG, 0, s>>>(a, rhs);
     k_pcg_tol<V><<<dim3((unsigned)B), kWG, 0, s>>>(a, rtol, outer_rtol, etol);
     if (amg) precond(0);
@@ -1305,7 +1312,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
     // the bulk of them, kBulkFrac) the first chunk stops at the bulk and the
     // rest runs compacted, straight to the previous slowest.
     int32_t it = 0;
-    const int32_t bulk = compact ? hint[kBulkHint] : 0;
+    const int32_t bulk = hint[kBulkHint];
     const bool split = bulk > 0 && *hint >= bulk + 2;
     int32_t chunk = split ? std::min(bulk, kMaxChunk) : (*hint > 0 ? std::min(*hint, kMaxChunk) : 8);
     bool done = false;
@@ -1359,7 +1366,7 @@ int64_t pcg(mof_mesh *m, int32_t B, const MatArgs<V> &mat, const V *dinv, const 
         chunk = split && it == std::min(bulk, kMaxChunk) && *hint > it ? std::min(*hint - it, kMaxChunk) : 8;
         // a tail chunk (at most kCompactFrac of the batch still running)
         // launches over those systems only; same bits (SysMap)
-        if (!done && compact && owe_or_run <= kCompactFrac * B) {
+        if (!done && owe_or_run <= kCompactFrac * B) {
             MOF_HIP(hipMemcpyAsync(m->ws.smap.p, h_map.data(), sizeof(int32_t) * owe_or_run, hipMemcpyHostToDevice, s));
             a.sm = SysMap{m->ws.smap.p, owe_or_run};
         }
@@ -1517,6 +1524,7 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
         }
     }
     if (threadIdx.x == 0) {
+        keep_met(si);
         if (si[SI_ACTIVE] && sd[SD_REL] <= f.rtol) {  // k_mark_unconverged
             si[SI_ACTIVE] = 0;
         } else if (si[SI_ACTIVE]) {
@@ -1534,8 +1542,21 @@ __global__ __launch_bounds__(NQ * kWG) void k_solve_fused(PcgArgs<double> a, OpA
 
 int32_t xcd_batch_cap_host(int64_t nblk, int32_t grp) { return xcd_batch_cap(nblk, grp); }
 
-void mesh_join_prep(mof_mesh *m) {
-    if (m && m->prep.valid()) m->prep.get();
+void mesh_join_prep(mof_mesh *m, bool take_error) {
+    if (!m) return;
+    std::lock_guard<std::mutex> lk(m->prep_mu);
+    if (m->prep.valid()) {
+        try {
+            m->prep.get();
+        } catch (...) {
+            m->prep_err = std::current_exception();
+        }
+    }
+    if (take_error && m->prep_err) {
+        std::exception_ptr e = m->prep_err;
+        m->prep_err = nullptr;
+        std::rethrow_exception(e);
+    }
 }
 
 int32_t grid_batch_cap(const mof_mesh *m) {
@@ -1618,27 +1639,19 @@ void ensure_workspace(mof_mesh *m, int32_t B, uint32_t precision) {
 
 // The fused solve covers the fp64 solve of a whole batch from x = 0 with a
 // stored u64 (the fp64 path's residual); auto (sp.fused < 0) on meshes of at
-// most MOF_FUSED_MAX_BLK row blocks (default 16: 4096 vertices), where the
-// eager path is launch-bound.
+// most kFusedMaxBlk row blocks (4096 vertices), where the eager path is
+// launch-bound.
+constexpr int32_t kFusedMaxBlk = 16;
 bool fused_eligible(const mof_mesh *m, const SolveParams &sp, const uint8_t *only) {
     if (sp.fused == 0 || only || sp.precision != MOF_PREC_F64 || sp.amg || sp.fail_at_max_iter) return false;
     if (m->ws.u64_stale || !m->ws.u64.p || m->n_own != m->N) return false;
     if (sp.fused > 0) return true;
-    static const int max_blk = [] {
-        const char *v = std::getenv("MOF_FUSED_MAX_BLK");
-        return v && *v ? std::atoi(v) : 16;
-    }();
-    return m->ws.nblk <= max_blk;
+    return m->ws.nblk <= kFusedMaxBlk;
 }
 
 // Row blocks the fused solve's workgroup runs side by side (groups of 256
-// threads; MOF_FUSED_NQ = 1 / 2 / 4 forces a width)
+// threads)
 int fused_quarters(int32_t nblk) {
-    static const int forced = [] {
-        const char *v = std::getenv("MOF_FUSED_NQ");
-        return v && *v ? std::atoi(v) : 0;
-    }();
-    if (forced == 1 || forced == 2 || forced == 4) return forced;
     return nblk >= 4 ? 4 : (nblk >= 2 ? 2 : 1);
 }
 
@@ -1737,8 +1750,8 @@ int64_t solve_batch(mof_mesh *m, int32_t B, const SolveParams &sp, hipStream_t s
     const RedArgs rdx{1, 0, (int32_t)gv.x, m->N};                 // k_outer_update's max records
     int64_t iters = 0, iters_before = 0;
     int32_t o = 0;
-    // MOF_SOLVE_VERBOSE: per refinement step iterations and residuals on stderr
-    static const bool verbose = std::getenv("MOF_SOLVE_VERBOSE") != nullptr;
+    // MOF_VERBOSE: per refinement step iterations and residuals on stderr
+    static const bool verbose = knob(Knob::Verbose) != nullptr;
     for (; o < sp.max_outer; ++o) {
         const double *rhs = (o == 0) ? w.rhs.p : w.r64.p;
         if (sp.precision == MOF_PREC_MIXED) {

@@ -57,14 +57,12 @@ def _digest(*parts) -> str:
     return h.hexdigest()
 
 
-# MOF_* switches that cannot change a saved V: logging, host staging sizes,
-# the fused solve's width and eligibility (bit-identical to the eager path),
-# the checkpoint's own settings, the RCCL library path
+# MOF_* switches that cannot change a saved V: logging, the host staging
+# size, host threads, the RCCL library path (csrc/mof_knobs.h), and the
+# checkpoint's own settings. The library's other switches (MOF_SYM_READS,
+# MOF_AMG_SMOOTH, MOF_AMG_OMEGA, MOF_AMG_BSW) change V bits and key the chunk.
 _KEY_NEUTRAL = frozenset((
-    "MOF_CHECKPOINT_DIR", "MOF_CHECKPOINT_CHUNK", "MOF_SOLVE_VERBOSE", "MOF_AMG_VERBOSE", "MOF_HOSTIO_VERBOSE",
-    "MOF_STAGE_MB", "MOF_STAGE_DIRECT_MB", "MOF_IO_THREADS", "MOF_FUSED_NQ", "MOF_FUSED_MAX_BLK", "MOF_RCCL_LIB",
-    # same bits either way (GPU tests): launch shapes and work skipping only
-    "MOF_CONV_EARLY", "MOF_COMPACT", "MOF_RESTR_SORT", "MOF_GAL_BIG", "MOF_SELFRED",
+    "MOF_CHECKPOINT_DIR", "MOF_CHECKPOINT_CHUNK", "MOF_VERBOSE", "MOF_STAGE_MB", "MOF_IO_THREADS", "MOF_RCCL_LIB",
 ))
 
 

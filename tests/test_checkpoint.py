@@ -114,11 +114,11 @@ def test_failed_chunks_are_solved_again(tmp_path):
 def test_environment_switches_invalidate_chunks(tmp_path, monkeypatch):
     I, tk = _inputs()
     m = _Mesh()
-    monkeypatch.delenv("MOF_PCG_STALL", raising=False)
+    monkeypatch.delenv("MOF_AMG_OMEGA", raising=False)
     velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
     velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
     assert len(m.calls) == 1
-    monkeypatch.setenv("MOF_PCG_STALL", "32")  # a solver switch: the chunk is stale
+    monkeypatch.setenv("MOF_AMG_OMEGA", "0.8")  # a solver switch: the chunk is stale
     velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
     assert len(m.calls) == 2
     m.reorder = False  # another device vertex order: stale as well
@@ -127,16 +127,15 @@ def test_environment_switches_invalidate_chunks(tmp_path, monkeypatch):
 
 
 def test_log_switches_keep_chunks(tmp_path, monkeypatch):
-    """Switches that cannot change V (logging, staging sizes, the fused
-    solve's width) leave the saved chunks valid (round-4 advisor)."""
+    """Switches that cannot change V (logging, staging sizes, host threads)
+    leave the saved chunks valid (round-4 advisor)."""
     I, tk = _inputs()
     m = _Mesh()
-    for k in ("MOF_SOLVE_VERBOSE", "MOF_HOSTIO_VERBOSE", "MOF_STAGE_MB", "MOF_FUSED_NQ"):
+    for k in ("MOF_VERBOSE", "MOF_STAGE_MB", "MOF_IO_THREADS"):
         monkeypatch.delenv(k, raising=False)
     velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
-    monkeypatch.setenv("MOF_SOLVE_VERBOSE", "1")
-    monkeypatch.setenv("MOF_HOSTIO_VERBOSE", "1")
+    monkeypatch.setenv("MOF_VERBOSE", "1")
     monkeypatch.setenv("MOF_STAGE_MB", "8")
-    monkeypatch.setenv("MOF_FUSED_NQ", "2")
+    monkeypatch.setenv("MOF_IO_THREADS", "3")
     velocity_field_sharded(m, I, tk, 0, 8, 0.5, checkpoint=str(tmp_path), chunk=8)
     assert len(m.calls) == 1

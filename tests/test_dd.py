@@ -192,7 +192,7 @@ def test_dd_amg_fewer_iterations_deterministic():
 def test_dd_amg_irregular_mesh_vs_smoothed_single_domain():
     """A random hull (valence 3-14) over 3 RCB parts: the parts keep the
     tentative prolongator (amg_build smooths only a whole mesh, nown < 0:
-    MOF_AMG_VERBOSE shows no "smoothed P" part level), the single domain
+    MOF_VERBOSE shows no "smoothed P" part level), the single domain
     smooths levels 0 and 1 (slab Galerkin, chunked coarse product, sorted
     restriction): two different preconditioners, V within 1e-6 of each
     other and of the oracle; the decomposed solve has the same bits for

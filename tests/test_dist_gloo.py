@@ -107,7 +107,7 @@ def test_bench_self_launch_weak_two_ranks():
                       "--no-cpu-baseline")
     assert line["dry_run"] and line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["timesteps_timed"] == 2 * 2 * 8
-    (a0, b0, n0), (a1, b1, n1) = line["rank_ranges"]
+    (a0, b0, n0, *_), (a1, b1, n1, *_) = line["rank_ranges"]
     assert (a0, b0, n0) == (0, 24, 16) and (a1, b1, n1) == (24, 48, 16)
 
 
@@ -119,6 +119,41 @@ def test_bench_fixed_timesteps_strong_split():
     assert line["scaling"] == "strong" and line["config"]["timesteps_timed"] == 5000
     assert [r[:2] for r in line["rank_ranges"]] == [[0, 2500], [2500, 5000]]
     assert sum(r[2] for r in line["rank_ranges"]) == 5000
+
+
+def test_bench_c4_eight_ranks_dry_run():
+    """C4 (BASELINE configs[3]) as the driver's 8-GPU run launches it:
+    bench.py --gpus 8 --fixed-timesteps 5000 --config C3 splits the job into
+    8 contiguous ranges of 625 timesteps; every rank sizes its batch against
+    its free HBM (288 GB: the default 1536 fits, so each rank runs its 625
+    timesteps as one batch). A rank with less free HBM (100 GB: 512) lowers
+    every rank's batch, so the batch rank 0 prints holds for all of them."""
+    argv = ("--gpus", "8", "--steps", "1", "--warmup", "1", "--config", "C3", "--fixed-timesteps", "5000",
+            "--no-cpu-baseline")
+    line = _bench_dry(*argv)
+    assert line["scaling"] == "strong" and line["n_gpus"] == 8 and line["config"]["timesteps_timed"] == 5000
+    assert [r[:2] for r in line["rank_ranges"]] == [[625 * i, 625 * (i + 1)] for i in range(8)]
+    assert all(r[2] == 625 and r[3] == 1536 and r[4] == 625 for r in line["rank_ranges"]), line["rank_ranges"]
+    assert line["config"]["batch"] == 1536 and line["config"]["batch_effective"] == 625
+    assert "batch_note" not in line["config"]
+    line = _bench_dry(*argv, env_extra={"MOF_BENCH_DRYRUN_FREE_GB": "288,288,288,100,288,288,288,288"})
+    own = [r[3] for r in line["rank_ranges"]]
+    assert own[3] == 512 and all(b == 1536 for i, b in enumerate(own) if i != 3), own
+    # every rank (rank 0 included) runs 512: 625 = 313 + 312
+    assert all(r[4] == 313 and r[2] == 625 for r in line["rank_ranges"]), line["rank_ranges"]
+    assert line["config"]["batch"] == 512 and line["config"]["batch_effective"] == 313
+    assert "smallest rank" in line["config"]["batch_note"]
+
+
+def test_bench_weak_eight_ranks_dry_run():
+    """The driver's scaling command at N = 8 (bench.py --gpus 8 --steps K
+    --warmup W, weak scaling at the default C3 / batch 1536): 8 contiguous
+    ranges of (W + K) x 1536 timesteps, K x 1536 timed per rank."""
+    line = _bench_dry("--gpus", "8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline")
+    assert line["scaling"] == "weak" and line["config"]["batch"] == 1536
+    assert [r[:2] for r in line["rank_ranges"]] == [[3 * 1536 * i, 3 * 1536 * (i + 1)] for i in range(8)]
+    assert all(r[2] == 2 * 1536 for r in line["rank_ranges"])
+    assert line["config"]["timesteps_timed"] == 8 * 2 * 1536 and line["legs"] is None
 
 
 def test_bench_gpus_must_match_world_size():

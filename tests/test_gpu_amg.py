@@ -216,108 +216,69 @@ def test_smoothed_aggregation_irregular_mesh(monkeypatch):
             assert np.abs(out[smooth][0][k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), (smooth, k)
 
 
-def test_slab_galerkin_vs_per_position(monkeypatch):
+def test_slab_galerkin_batch_split():
     """A smoothed level 0 (random hull, 20k vertices) takes its level-0 and
     level-1 Galerkin products by system slab (k_a_slab -> k_galerkin_sys,
     64 systems per wave): the same bits for batches that split the slabs
-    differently (70 = 64 + 6, 33 + 33 + 4), and against the per-position
-    products (MOF_GAL0_SYS=0; fused multiply-adds round differently) the
-    same iteration count within 5 % and V within 1e-6 of each other and of
-    the oracle."""
+    differently (70 = 64 + 6, 33 + 33 + 4), and V within 1e-6 of the
+    oracle's spsolve."""
     p, t, n, a = _hull(20000, seed=5)
     T = 71
     I = synth.travelling_wave(p, T)
     tk = np.arange(float(T))
-    monkeypatch.delenv("MOF_GAL0_SYS", raising=False)
     m = DeviceMesh(p, n, t, a)
     V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=70)
     V33, _ = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=33)
     m.close()
     assert st["failed"] == 0 and st["recovered"] == 0, st
     assert np.array_equal(V, V33)
-    monkeypatch.setenv("MOF_GAL0_SYS", "0")
-    m = DeviceMesh(p, n, t, a)
-    Vn, sn = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=70)
-    m.close()
-    assert sn["failed"] == 0 and sn["recovered"] == 0, sn
-    assert abs(st["iterations"] - sn["iterations"]) <= 0.05 * sn["iterations"], (st["iterations"], sn["iterations"])
-    scale = max(1.0, np.abs(Vn).max())
-    assert np.abs(V - Vn).max() < VTOL * scale
     a2, gw, e, iw = oracle.geometry(p, n, t, a)
     for k in (0, 69):
         Vo = oracle.worker(k, a2, gw, e, iw, t, list(tk), a, 0.01, I[k], I[k + 1])
         assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
 
 
-def test_restriction_entry_order_bit_identical(monkeypatch):
-    """The smoothed-P restriction forms its list entries' terms in fine-node
-    order (rperm) but sums each coarse node's terms in list order: the same
-    bits as the list-order pass (MOF_RESTR_SORT=0)."""
-    p, t, n, a = _hull(20000, seed=7)
-    T = 9
-    I = synth.travelling_wave(p, T)
-    tk = np.arange(float(T))
-    out = []
-    for srt in (None, "0"):
-        if srt is None:
-            monkeypatch.delenv("MOF_RESTR_SORT", raising=False)
-        else:
-            monkeypatch.setenv("MOF_RESTR_SORT", srt)
-        m = DeviceMesh(p, n, t, a)
-        V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=8)
-        m.close()
-        assert st["failed"] == 0 and st["recovered"] == 0, st
-        out.append((V, st["iterations"]))
-    assert out[0][1] == out[1][1]
-    assert np.array_equal(out[0][0], out[1][0])
-
-
 @pytest.mark.parametrize("case", ["G1_ico642", "G2_cap641"])
-def test_galerkin_by_entry_bit_identical(case, monkeypatch):
+def test_galerkin_by_entry_batch_split(case):
     """The level-0 Galerkin product by gather entry (k_galerkin0_ent, the
-    tentative prolongator's default) forms the same terms in the same order
-    as the per-position kernel (MOF_GAL_ENT=0): the same bits, batch split
-    into partial system quads."""
+    tentative prolongator's) puts two systems in a thread: the same bits for
+    a batch split into partial system pairs (7) as for the whole batch, and
+    V within 1e-6 of the reference's spsolve (golden V_k)."""
     g = load_golden(case)
     I, tk, lam = g["I"], g["t_k"], float(g["lambda_"])
+    m = mesh_of(g)
     out = []
-    for ent in ("1", "0"):
-        monkeypatch.setenv("MOF_GAL_ENT", ent)
-        m = mesh_of(g)
-        V, st = m.solve_range(I, tk, 0, len(I) - 2, lam, precision="mixed", precond="amg", batch=7)
+    for batch in (7, len(I) - 1):
+        V, st = m.solve_range(I, tk, 0, len(I) - 1, lam, precision="mixed", precond="amg", batch=batch)
         assert st["failed"] == 0 and st["recovered"] == 0
         out.append((V, st["iterations"]))
-        m.close()
+    m.close()
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][0], out[1][0])
+    assert np.abs(out[0][0] - g["V_k"]).max() < VTOL
 
 
-def test_coarse_galerkin_by_entry_bit_identical(monkeypatch):
-    """Levels >= 1 by gather entry (k_galerkin3_ent, round 4) against the
-    per-position product (MOF_GAL3_ENT=0, k_galerkin3_ns): the same terms in
-    the same order, the same bits, on a mesh with two coarse products
-    (10,242 -> ~1.3k -> ~170 nodes), ragged system groups. MOF_GAL_BIG=16
-    sends every position past 16 entries to k_galerkin3_big (chunked
-    lists, one summing lane per system and block entry): the same bits."""
+def test_coarse_galerkin_by_entry_batch_split():
+    """Levels >= 1 by gather entry (k_galerkin3_ent) and, for positions past
+    kGalBig entries, the chunked k_galerkin3_big, on a mesh with two coarse
+    products (10,242 -> ~1.3k -> ~170 nodes): the same bits for ragged system
+    groups (batch 7) as for the whole batch, V within 1e-6 of the oracle."""
     p, t = synth.icosphere(32, jitter=0.005)
     n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
     I = synth.travelling_wave(p, 12)
     tk = np.arange(12, dtype=np.float64)
+    m = DeviceMesh(p, n, t, a)
     out = []
-    for ent, big in (("1", None), ("1", "16"), ("0", None)):
-        monkeypatch.setenv("MOF_GAL3_ENT", ent)
-        if big is None:
-            monkeypatch.delenv("MOF_GAL_BIG", raising=False)
-        else:
-            monkeypatch.setenv("MOF_GAL_BIG", big)
-        m = DeviceMesh(p, n, t, a)
-        V, st = m.solve_range(I, tk, 0, 11, 0.01, precision="mixed", precond="amg", batch=7)
+    for batch in (7, 11):
+        V, st = m.solve_range(I, tk, 0, 11, 0.01, precision="mixed", precond="amg", batch=batch)
         assert st["failed"] == 0 and st["recovered"] == 0
         out.append((V, st["iterations"]))
-        m.close()
-    for o in out[1:]:
-        assert o[1] == out[0][1]
-        assert np.array_equal(o[0], out[0][0])
+    m.close()
+    assert out[0][1] == out[1][1]
+    assert np.array_equal(out[0][0], out[1][0])
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    Vo = oracle.worker(3, a2, gw, e, iw, t, list(tk), a, 0.01, I[3], I[4])
+    assert np.abs(out[0][0][3] - Vo).max() < VTOL
 
 
 def test_open_patch_batch_split_bit_identical():
@@ -345,19 +306,17 @@ def test_open_patch_boundary_sweeps(monkeypatch):
     takes two extra block-Jacobi sweeps per side on those rows (k_bsweep):
     fewer PCG iterations than without them (MOF_AMG_BSW=0: 28.6 vs 19.8 per
     timestep on the bench), V within 1e-6 of that solve and of the oracle, no
-    failed or recovered system; the bf16 corrected iterate (MOF_X_BF16=1,
-    k_bsweep on the x0 format after the prolongation) as well."""
+    failed or recovered system."""
     p, t, n, a = synth.mesh_for_config("S1s")
     T = 13
     I = synth.config_wave("S1s", p, T)
     tk = np.arange(float(T))
     res = {}
-    for env in ({}, {"MOF_AMG_BSW": "0"}, {"MOF_X_BF16": "1"}):
-        for k in ("MOF_AMG_BSW", "MOF_X_BF16"):
-            if k in env:
-                monkeypatch.setenv(k, env[k])
-            else:
-                monkeypatch.delenv(k, raising=False)
+    for env in ({}, {"MOF_AMG_BSW": "0"}):
+        if env:
+            monkeypatch.setenv("MOF_AMG_BSW", env["MOF_AMG_BSW"])
+        else:
+            monkeypatch.delenv("MOF_AMG_BSW", raising=False)
         m = DeviceMesh(p, n, t, a)
         V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", batch=T - 1)
         m.close()
@@ -368,7 +327,6 @@ def test_open_patch_boundary_sweeps(monkeypatch):
     assert its < 0.85 * its0, (its, its0)
     scale = max(1.0, np.abs(V0).max())
     assert np.abs(V - V0).max() < VTOL * scale
-    assert np.abs(res[(("MOF_X_BF16", "1"),)][0] - V0).max() < VTOL * scale
     a2, gw, e, iw = oracle.geometry(p, n, t, a)
     for k in (0, T - 2):
         Vo = oracle.worker(k, a2, gw, e, iw, t, list(tk), a, 0.01, I[k], I[k + 1])
@@ -376,15 +334,13 @@ def test_open_patch_boundary_sweeps(monkeypatch):
 
 
 @pytest.mark.parametrize("kind", ["golden", "hull"])
-def test_early_convergence_mark_bit_identical(kind, monkeypatch):
-    """Systems whose |r|^2 after the update already meets the tolerance are
-    marked converged before the V-cycle (k_pcg_conv_early) and skip it: the
-    z it would have made was never used, so V, the iteration counts and the
-    refinement are the same bits as with the last V-cycle run
-    (MOF_CONV_EARLY=0). Tail chunks launch over the running systems only
-    (SysMap): the same bits as launches over the whole batch (MOF_COMPACT=0).
-    On the 642-vertex mesh the SpMV and the update reduce their own scalars
-    (PcgArgs::selfred): the same bits as the k_red_* launches (MOF_SELFRED=0)."""
+def test_work_skipping_batch_split(kind):
+    """Systems whose |r|^2 after the update already meets the tolerance skip
+    that iteration's V-cycle (k_pcg_conv_early), tail chunks launch over the
+    running systems only (SysMap), and on the 642-vertex mesh the SpMV and the
+    update reduce their own scalars (PcgArgs::selfred). None of it may depend
+    on which systems share a launch: the same V bits, iteration counts and
+    residuals for batches of 5 and 3, and V within 1e-6 of spsolve."""
     if kind == "golden":
         g = load_golden("G1_ico642")
         p, n, t, a = g["coordinates"], g["normals"], g["triangles"], g["areas"]
@@ -394,18 +350,18 @@ def test_early_convergence_mark_bit_identical(kind, monkeypatch):
         I = synth.travelling_wave(p, 9)
         tk, lam = np.arange(9.0), 0.01
     T = len(I)
+    m = DeviceMesh(p, n, t, a)
     out = []
-    for env in ({}, {"MOF_CONV_EARLY": "0"}, {"MOF_COMPACT": "0"}, {"MOF_SELFRED": "0"}):
-        for k in ("MOF_CONV_EARLY", "MOF_COMPACT", "MOF_SELFRED"):
-            if k in env:
-                monkeypatch.setenv(k, env[k])
-            else:
-                monkeypatch.delenv(k, raising=False)
-        m = DeviceMesh(p, n, t, a)
-        V, st = m.solve_range(I, tk, 0, T - 1, lam, precision="mixed", precond="amg", batch=5)
-        m.close()
+    for batch in (5, 3):
+        V, st = m.solve_range(I, tk, 0, T - 1, lam, precision="mixed", precond="amg", batch=batch)
         assert st["failed"] == 0 and st["recovered"] == 0, st
         out.append((V, st["iterations"], st["max_rel_residual"]))
-    for o in out[1:]:
-        assert o[1] == out[0][1] and o[2] == out[0][2]
-        assert np.array_equal(o[0], out[0][0])
+    m.close()
+    assert out[1][1] == out[0][1] and out[1][2] == out[0][2]
+    assert np.array_equal(out[1][0], out[0][0])
+    if kind == "golden":
+        assert np.abs(out[0][0] - g["V_k"]).max() < VTOL
+    else:
+        a2, gw, e, iw = oracle.geometry(p, n, t, a)
+        Vo = oracle.worker(4, a2, gw, e, iw, t, list(tk), a, lam, I[4], I[5])
+        assert np.abs(out[0][0][4] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max())

@@ -41,8 +41,7 @@ def _oracle_V(p, t, n, a, I, ks, lam=0.01):
 def diverging_smoother(monkeypatch):
     # read when the hierarchy is built (first multigrid solve of a handle):
     # fine-level block-Jacobi damping far past its divergence edge (1.0 on R3)
-    monkeypatch.setenv("MOF_AMG_OMEGA", "2.5")
-    monkeypatch.setenv("MOF_AMG_OMEGA1", "2.5")
+    monkeypatch.setenv("MOF_AMG_OMEGA", "2.5,2.5")  # fine, coarse
     yield
 
 
@@ -175,9 +174,13 @@ def test_host_pipeline_matches_device_path(same_I2, direct, monkeypatch):
     I = synth.travelling_wave(p, T)
     I2 = I if same_I2 else np.ascontiguousarray(I[::-1] * 0.5 + 0.25)
     tk = np.arange(float(T))
-    # ring chunks (1 MB) far smaller than one batch's 4.4 / 8.3 MB transfers
-    monkeypatch.setenv("MOF_STAGE_DIRECT_MB", "16" if direct else "0")
-    monkeypatch.setenv("MOF_STAGE_MB", "1")
+    # staged: ring chunks (1 MB) far smaller than one batch's 4.4 / 8.3 MB
+    # transfers (direct copies only up to half a chunk); direct: the default
+    # 16 MB bound takes them straight from pageable memory
+    if direct:
+        monkeypatch.delenv("MOF_STAGE_MB", raising=False)
+    else:
+        monkeypatch.setenv("MOF_STAGE_MB", "1")
     m = DeviceMesh(p, n, t, a)
     Vh, sh = m.solve_range(I, tk, 2, T - 1, 0.01, I2=I2, precision="mixed", precond="amg", batch=16)
     dev = torch.device("cuda", 0)
@@ -320,7 +323,7 @@ def test_bench_marks_recovery_as_defect():
     import json
     import subprocess
     import sys
-    env = dict(os.environ, MOF_AMG_OMEGA="2.5", MOF_AMG_OMEGA1="2.5")
+    env = dict(os.environ, MOF_AMG_OMEGA="2.5,2.5")
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--config", "C2", "--precision", "mixed",
            "--precond", "amg", "--steps", "1", "--warmup", "0", "--batch", "4", "--no-cpu-baseline",
            "--parity-samples", "0", "--host-batches", "0"]
@@ -447,3 +450,45 @@ def test_large_irregular_mesh_default_schedule():
         scale = max(1.0, np.abs(Vo).max())
         assert np.abs(V[k] - Vo).max() < VTOL * scale, k
         assert np.abs(V4[k] - Vo).max() < VTOL * scale, k
+
+
+def test_clones_while_prepare_pending():
+    """mof_mesh_prepare's background setup joined from several host threads
+    at once (round-5 advisor): clones of a handle whose multigrid build is
+    still pending (no sync_solver in between) and a solve on the handle
+    itself race for the setup's result; every call succeeds, and the solve
+    gives the same bits as on a handle that was synchronised first."""
+    import ctypes
+    import threading
+    from mofhip import _lib as L
+    p, t, n, a = synth.mesh_for_config("S1s")
+    I = synth.config_wave("S1s", p, 9)
+    tk = np.arange(9.0)
+    opts = dict(precision="mixed", precond="amg")
+    ref = DeviceMesh(p, n, t, a)
+    ref.prepare_solver(**opts)
+    ref.sync_solver()
+    V0, _ = ref.solve_range(I, tk, 0, 8, 0.01, **opts)
+    ref.close()
+    m = DeviceMesh(p, n, t, a)
+    m.prepare_solver(**opts)  # no sync_solver: the build is pending
+    h = m.handle()
+    rcs, clones = [], []
+
+    def clone():
+        c = ctypes.c_void_p()
+        rcs.append(L.lib().mof_mesh_clone(h, 0, ctypes.byref(c)))
+        clones.append(c)
+
+    ths = [threading.Thread(target=clone) for _ in range(4)]
+    for th in ths:
+        th.start()
+    V, st = m.solve_range(I, tk, 0, 8, 0.01, **opts)
+    for th in ths:
+        th.join()
+    for c in clones:
+        L.lib().mof_mesh_destroy(c)
+    m.close()
+    assert rcs == [0] * 4, rcs
+    assert st["failed"] == st["recovered"] == 0
+    assert np.array_equal(V, V0)

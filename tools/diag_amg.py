@@ -2,10 +2,10 @@
 
     python tools/diag_amg.py CONFIG [K] [ENV=VAL ...]
 
-Solves K timesteps (mixed + multigrid) with recovery off and MOF_SOLVE_VERBOSE
+Solves K timesteps (mixed + multigrid) with recovery off and MOF_VERBOSE
 set, so the library prints per refinement step the inner iterations and why
 the first solve's failed systems failed; the environment assignments (e.g.
-MOF_AMG_SMOOTH=0, MOF_X_BF16=0, MOF_WINDOW_SORT=0) select the variant. The
+MOF_AMG_SMOOTH=0, MOF_AMG_OMEGA=...) select the variant. The
 signal is the bench's for CONFIG (synth.config_wave; DIAG_PINWHEEL=1: the
 atan2 pinwheel of synth.travelling_wave).
 """
@@ -26,8 +26,7 @@ def main():
         if "=" in kv:
             k, v = kv.split("=", 1)
             os.environ[k] = v
-    os.environ["MOF_SOLVE_VERBOSE"] = "1"
-    os.environ.setdefault("MOF_AMG_VERBOSE", "1")
+    os.environ["MOF_VERBOSE"] = "1"
     from mofhip import DeviceMesh, synth
     p, t, n, a = synth.mesh_for_config(cfg)
     m = DeviceMesh(p, n, t, a)
