@@ -57,6 +57,7 @@ CONFIG_NAMES = {
           "by a seeded band-limited field: gyral period 16-27 mm at 70 mm radius, sulcal amplitude 15 % of the "
           "radius; synth.folded_sphere)",
     "S1": "160,801-vertex S1-like reconstructed patch (51 x 51 electrode grid, Delaunay, butterfly x3, smoothed)",
+    "S1m": "40,401-vertex S1-like reconstructed patch (26 x 26 electrode grid at 3 mm)",
     "S1s": "3,249-vertex S1-like reconstructed patch (8 x 8 electrode grid), T=98 (97 solves), the reference's "
            "real workload size (config.yaml:5, find_singularity_point.py:19-20)",
 }

@@ -382,7 +382,7 @@ def wave_phase(name: str, points: np.ndarray):
     across the electrode grid (about 3 wavelengths over it) instead of a
     pinwheel whose unbounded gradient would sit at the patch centre."""
     p = np.asarray(points, dtype=np.float64)
-    if name in ("S1", "S1s"):
+    if name in ("S1", "S1s", "S1m"):
         return np.arctan2(p[:, 2] + 70.0, p[:, 1]), 30.0
     return np.arctan2(p[:, 1], p[:, 0]), 3.0
 
@@ -407,13 +407,16 @@ def mesh_for_config(name: str):
     if name == "R3":
         p, t = random_sphere(163842, 10.0, seed=0)
         return p, t, vertex_normals(p, t), triangle_areas(p, t)
-    if name in ("S1", "S1s"):
+    if name in ("S1", "S1s", "S1m"):
         # S1-like surfaces (electrode_surface): S1s = an 8 x 8 grid at 10 mm
         # (a clinical ECoG grid, 70 mm across; 3,249 vertices, the size of the
         # reference's real surfaces, find_singularity_point.py:19-20), S1 = a
         # 51 x 51 high-density grid at 1.5 mm over the same 75 mm (160,801
-        # vertices, the 160k class)
-        p, t = electrode_surface(51, spacing=1.5) if name == "S1" else electrode_surface(8, spacing=10.0)
+        # vertices, the 160k class), S1m = a 26 x 26 grid at 3 mm (40,401
+        # vertices: the smallest of the class whose multigrid level 1 is a
+        # separate level, for tests of the coarse-level cycle)
+        p, t = {"S1": lambda: electrode_surface(51, spacing=1.5), "S1s": lambda: electrode_surface(8, spacing=10.0),
+                "S1m": lambda: electrode_surface(26, spacing=3.0)}[name]()
         return p, t, vertex_normals(p, t), triangle_areas(p, t)
     if name == "P3":
         p, t, _, _ = mesh_for_config("C3")

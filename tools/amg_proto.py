@@ -47,6 +47,8 @@ mixed solve -- for aggregation-multigrid variants:
               the pre- and before the post-smoothing (the library's k_bsweep)
   exact=L     an exact (sparse LU) solve from level L down: the two-grid
               bound at L = 1
+  f32gal=1    the Galerkin products in fp32 (fp32 operands and sums, as the
+              GPU's k_galerkin* kernels)
   s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
               (from the copy's diagonal blocks) and the level-0 Galerkin
               product all on the stored copy in format F (1 = bf16, today)
@@ -323,7 +325,11 @@ def build(A, a2m, e, opts):
         pc = np.diff(Pb.indptr)
         rows = np.repeat(np.arange(Ab.shape[0] // bs), np.diff(Ab.indptr))
         L.gal_terms = int((pc[rows] * pc[Ab.indices]).sum())
-        Ac = (P.T @ (L.Aq if hasattr(L, "Aq") else Acur) @ P).tocsr()
+        if opts.get("f32gal"):  # the GPU's fp32 Galerkin product: fp32 operands, fp32 sums
+            P32 = P.astype(np.float32)
+            Ac = (P32.T @ (L.Aq if hasattr(L, "Aq") else Acur).astype(np.float32) @ P32).astype(np.float64).tocsr()
+        else:
+            Ac = (P.T @ (L.Aq if hasattr(L, "Aq") else Acur) @ P).tocsr()
         a2cur = (P.T @ (a2m if lvl == 0 else a2cur) @ P).tocsr()
         dead = np.abs(Ac).sum(1).A1 == 0
         Ac = (Ac + sp.diags(dead * 1.0)).tocsr()
