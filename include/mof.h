@@ -327,7 +327,8 @@ int mof_cell_areas(const float *points, const int64_t *triangles, int64_t N, int
  * each level (at most 16 levels); qtq_err the largest |Q^T Q - I| entry over
  * the level-0 aggregates (orthonormal prolongator columns); max_curl (ABI 4,
  * optional) the largest per-level median sigma_3 / sigma_1 of the aggregates'
- * near-null blocks -- the multigrid's W-cycle criterion (>= 0.35). */
+ * near-null blocks -- the multigrid's criterion for smoothing level 1's
+ * prolongator on a closed surface (>= 0.35: folds). */
 int mof_amg_probe(const int32_t *tri, const double *e, int32_t N, int32_t M, int32_t *n_levels,
                   int32_t *level_nodes, double *qtq_err, double *max_curl);
 

@@ -90,7 +90,8 @@ struct AmgHierarchy {
     // per transition l -> l+1: the median over the aggregates of
     // sigma_3 / sigma_1 of the stacked near-null block (how much the tangent
     // planes turn inside an aggregate; 0 on a flat one), and the largest of
-    // these over transitions with >= 64 aggregates (amg_build's W-cycle choice)
+    // these over transitions with >= 64 aggregates (amg_build's level-1
+    // smoothing choice, kFoldCurl)
     std::vector<double> curl;
     double max_curl = 0.0;
     bool folded = false;  // amg_build's auto choice rebuilt it with level 1 smoothed
@@ -143,9 +144,6 @@ struct AmgDevice {
     float omega = 0.85f, omega1 = 1.05f;
     int32_t xm = 2;  // level 0's corrected iterate: 1 in the x0 format in place, 2 fp32 in lv[0].y
     bool regular = false;  // tentative prolongator on a regular mesh: the bf16 iterates and omega1 1.1
-    // level 1 visits the coarser levels twice per cycle (S C S C S at level
-    // 1, a palindrome of symmetric steps: the preconditioner stays SPD)
-    bool wcycle = false;
     // (one block-Jacobi sweep per side on the coarse levels; 2 measured in
     // round 5, profiles/r05_ab/nu1/: fewer its, fewer timesteps/s but on F3)
     // open surfaces: extra level-0 sweeps on the boundary rows and their

@@ -1883,14 +1883,14 @@ bool amg_build(mof_mesh *m) {
     // its, +1.8 %; C2 mixed +2 %), 1.05 otherwise (R3 as measured; 1.2
     // diverges there with the tentative P)
     if (omega1_set <= 0.f) G.omega1 = G.regular ? 1.1f : 1.05f;
-    // level 1 visiting the levels below twice (W): measured, not the default.
-    // Round 5, same box (profiles/r05_ab/wcycle/): S1 (open) 858 -> 905
-    // timesteps/s (59.5 -> 47.2 PCG its), F3 (folded) 1727 -> 1934 (40.5 ->
-    // 30.1) -- level 1's smoothed prolongator does better on both (995,
-    // 2292) -- and the spheres lose (C3 3652 -> 3370, R3 748 -> 657).
-    // MOF_AMG_W=1 forces it.
-    G.wcycle = false;
-    if (const char *v = std::getenv("MOF_AMG_W")) G.wcycle = std::atoi(v) != 0;
+    // (a W-cycle at level 1 -- the levels below visited twice -- was
+    // measured in rounds 5-6 and removed: slower than level 1's smoothed
+    // prolongator on every mesh (S1 905 vs 995, F3 1934 vs 2292, C3 3370 vs
+    // 3652 timesteps/s, profiles/r05_ab/wcycle/), and together with it it
+    // broke 15 of 4608 S1 solves down: the cycle below level 1 over-corrects
+    // there (lambda(B2 A2) up to 2.2 with the coarse damping 1.05,
+    // tools/wcycle_study.py), which a V-cycle tolerates and the second
+    // coarse correction of a W-cycle does not)
     MOF_REQUIRE(H.coarse_dofs <= kMaxCoarse, "coarsest multigrid level too large");
     MOF_REQUIRE(H.levels.size() <= (size_t)kMaxLevels, "too many multigrid levels");
     G.lv.resize(H.levels.size());
@@ -2048,7 +2048,7 @@ bool amg_build(mof_mesh *m) {
             std::fprintf(stderr, "mof amg level %zu: n=%d bs=%d blocks=%zu sell=%lld%s curl %.3f%s\n", l,
                          H.levels[l].n, H.levels[l].bs, H.levels[l].vcol.size(), (long long)H.levels[l].sell_nb(),
                          H.levels[l].smoothed ? " (smoothed P)" : "", l < H.curl.size() ? H.curl[l] : 0.0,
-                         l == 0 && G.wcycle ? " (W-cycle at level 1)" : (l == 0 && H.folded ? " (folded)" : ""));
+                         l == 0 && H.folded ? " (folded)" : "");
     }
     MOF_HIP(hipStreamSynchronize(s));
     return true;
@@ -2113,7 +2113,6 @@ AmgFine amg_fine(mof_mesh *m) {
     f.omega = G.omega;
     f.smoothed = G.lv[0].smoothed;
     f.regular = G.regular;
-    f.wcycle = G.wcycle;
     return f;
 }
 
@@ -2318,12 +2317,6 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
         k_subcycle<<<dim3((unsigned)nL), kSubWG, 0, s>>>(sa);
     } else {
         coarse(v);
-        if (G.wcycle) {
-            // the second visit from level 1's post-smoothed y: x and y swap
-            // roles, and level 0's prolongation reads the new result
-            std::swap(v[1].x, v[1].y);
-            coarse(v);
-        }
     }
     // up at level 0: coarse correction, post-smooth
     for (int32_t l = 0; l >= 0; --l) {

@@ -411,7 +411,6 @@ struct AmgFine {
     float omega;
     bool smoothed;    // level 0 has the smoothed prolongator (irregular mesh)
     bool regular;     // tentative prolongator on a regular mesh (bf16 z is tuned for it)
-    bool wcycle;      // level 1 visits the coarser levels twice (folded or open surfaces)
 };
 AmgFine amg_fine(mof_mesh *m);
 // bf16 level-0 A of the next batch, written by the assembly (marks it

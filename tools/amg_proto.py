@@ -28,6 +28,8 @@ mixed solve -- for aggregation-multigrid variants:
   sa1a2=X     the same with the coarse levels' Galerkin image of lambda*a2 (per mesh)
   sa1only=1   sa1 / sa1a2 at level 1 only (the transition 1 -> 2)
   w2          two coarse-grid visits per level-1 cycle (W-cycle at level 1)
+  kcyc=K      K-cycle at level 1: level 2's problem by K flexible-CG steps
+              preconditioned by level 2's cycle (the outer PCG turns flexible)
   nu1=K       K pre- and K post-smoothing sweeps at the coarse levels (V(K,K))
   q1=F        the sweeps at levels >= 1 on a stored copy of the operator: 1 bf16,
               2 int8 + one scale per block, 3 fp8 e4m3 + one scale per block,
@@ -47,6 +49,7 @@ mixed solve -- for aggregation-multigrid variants:
               the pre- and before the post-smoothing (the library's k_bsweep)
   exact=L     an exact (sparse LU) solve from level L down: the two-grid
               bound at L = 1
+  galq=1      with q1: the coarse Galerkin products from the stored copy
   f32gal=1    the Galerkin products in fp32 (fp32 operands and sums, as the
               GPU's k_galerkin* kernels)
   s0=F        level 0 as the GPU runs it: the sweeps, the smoother's D
@@ -269,6 +272,10 @@ def build(A, a2m, e, opts):
             if lvl == 0 and "omb" in opts:  # per-row damping: boundary rows omb
                 om = np.where(system.boundary, opts["omb"], L.om)
                 L.om = np.repeat(om, bs)
+        if lvl >= 1 and opts.get("galq") and opts.get("q1"):
+            # the coarse Galerkin products from the sweeps' stored copy (the
+            # operator the level's residual applies), not the exact one
+            L.Aq = quantize(Acur, bs, int(opts["q1"]))
         levels.append(L)
         n = Acur.shape[0] // bs
         if n * bs <= 128 or n * 3 <= 128:
@@ -425,10 +432,35 @@ def vcycle(levels, l, b, opts):
     cyc = 2 if (opts.get("w2") and l == 1) else 1
     for _ in range(cyc):
         r = b - Aw @ x
-        y = vcycle(levels, l + 1, L.P.T @ r, opts)
+        if opts.get("kcyc") and l == 1:  # K-cycle: the level-2 problem by kcyc FCG steps
+            y = _kcycle(levels, l + 1, L.P.T @ r, opts, int(opts["kcyc"]))
+        else:
+            y = vcycle(levels, l + 1, L.P.T @ r, opts)
         x = x + L.P @ y
         for _ in range(nu):
             x = x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
+    return x
+
+
+def _kcycle(levels, l, b, opts, steps):
+    """Notay's K-cycle at level l: `steps` flexible-CG iterations on the
+    level's operator (the copy its cycle applies), preconditioned by the
+    level's own cycle, from x = 0."""
+    L = levels[l]
+    Aw = getattr(L, "Aq", L.A)
+    x = np.zeros_like(b)
+    r = b.copy()
+    d_prev = q_prev = None
+    for _ in range(steps):
+        z = vcycle(levels, l, r, opts)
+        d = z
+        if d_prev is not None:  # A-orthogonal to the previous direction
+            d = z - (z @ q_prev) / (d_prev @ q_prev) * d_prev
+        q = Aw @ d
+        a = (d @ r) / (d @ q)
+        x = x + a * d
+        r = r - a * q
+        d_prev, q_prev = d, q
     return x
 
 
@@ -548,7 +580,9 @@ def _bsw_vcycle(levels, L, Aw, b, opts):
     return x + L.om * bsr_apply(L.Dinv, b - Aw @ x, L.bs)
 
 
-def pcg(A, f, M, tol=1e-4, maxit=2000):
+def pcg(A, f, M, tol=1e-4, maxit=2000, flexible=False):
+    """PCG; flexible: Polak-Ribiere beta (flexible CG, for a nonlinear
+    preconditioner such as the K-cycle)."""
     x = np.zeros_like(f)
     r = f.copy()
     z = M(r)
@@ -559,13 +593,15 @@ def pcg(A, f, M, tol=1e-4, maxit=2000):
         q = A @ p
         a = rz / (p @ q)
         x += a * p
+        r_old = r.copy() if flexible else None
         r -= a * q
         if np.linalg.norm(r) <= tol * nf:
             pcg.rho = (np.linalg.norm(r) / nf) ** (1.0 / it)
             return it
         z = M(r)
         rz2 = r @ z
-        p = z + (rz2 / rz) * p
+        beta = (z @ (r - r_old)) / rz if flexible else rz2 / rz
+        p = z + beta * p
         rz = rz2
     return maxit
 
@@ -593,7 +629,7 @@ def main():
         levels = build(A, a2m, e, opts)
         sizes = [lv.A.shape[0] // lv.bs for lv in levels]
         nnz = sum(lv.A.nnz for lv in levels)
-        its = pcg(A, f, lambda r: vcycle(levels, 0, r, opts))
+        its = pcg(A, f, lambda r: vcycle(levels, 0, r, opts), flexible=bool(opts.get("kcyc")))
         blk = [round(lv.A.nnz / lv.bs ** 2 / (lv.A.shape[0] / lv.bs), 1) for lv in levels]
         pb = [round(lv.p_blocks, 2) for lv in levels if hasattr(lv, "p_blocks")]
         gal = [getattr(lv, "gal_terms", 0) for lv in levels]

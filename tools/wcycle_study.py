@@ -112,6 +112,22 @@ def main():
             live = np.abs(A2).sum(1).A1 > 0
             lo2, hi2 = lanczos_extremes(A2, lambda r: P.vcycle(levels, 2, r, o), n2, steps=80)
             b2 = "  B2 A2 in [%.4f, %.4f] (%d dofs, %d live)" % (lo2, hi2, n2, live.sum())
+        # dense: the level-2 cycle B2 against level 2's Galerkin operator A2
+        # and against the operator level 1's coarse correction actually
+        # inverts, P1^T A1q P1 (A1q: the level-1 residual's stored copy)
+        if len(levels) > 2 and not hasattr(levels[2], "coarse") and levels[2].A.shape[0] <= 6000:
+            n2 = levels[2].A.shape[0]
+            B2 = np.column_stack([P.vcycle(levels, 2, col, o) for col in np.eye(n2)])
+            B2 = 0.5 * (B2 + B2.T)
+            A1w = getattr(levels[1], "Aq", levels[1].A)
+            A2e = (levels[1].P.T @ A1w @ levels[1].P).toarray()
+            A2e += np.diag((np.abs(A2e).sum(1) == 0) * 1.0)
+            import scipy.linalg as sl
+            Lb = np.linalg.cholesky(B2)
+            for nm, Am in (("A2", levels[2].A.toarray()), ("P1'A1q P1", A2e)):
+                ev = np.linalg.eigvalsh(Lb.T @ Am @ Lb)
+                print("   eig(B2 %s) in [%.4f, %.4f]  (lambda_min(%s) %.3e)" %
+                      (nm, ev[0], ev[-1], nm, np.linalg.eigvalsh(Am)[0]), flush=True)
         # smallest eigenvalues of the coarse operators (the Galerkin products
         # the cycle inverts): dense below 4k dofs, else shift-invert near 0
         lmin = []
@@ -124,9 +140,10 @@ def main():
                 ev = sla.eigsh(Al.tocsc(), k=2, sigma=0.0, which="LM", return_eigenvectors=False)
                 lmin.append("%.2e" % ev.min())
         print("   coarse lambda_min[/max]: %s" % " ".join(lmin), flush=True)
-        its = P.pcg(A, f, M)
-        print("%-14s levels %s  asym %.2e  M A in [%.4f, %.4f]%s  its(1e-4) %d" %
-              (spec, sizes, asym, lo, hi, b2, its), flush=True)
+        its = P.pcg(A, f, M, flexible=bool(o.get("kcyc")))
+        its_tight = P.pcg(A, f, M, tol=1e-8, flexible=bool(o.get("kcyc")))
+        print("%-14s levels %s  asym %.2e  M A in [%.4f, %.4f]%s  its(1e-4) %d  its(1e-8) %d" %
+              (spec, sizes, asym, lo, hi, b2, its, its_tight), flush=True)
 
 
 if __name__ == "__main__":
