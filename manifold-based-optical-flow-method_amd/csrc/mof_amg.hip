@@ -1829,24 +1829,27 @@ bool amg_build(mof_mesh *m) {
         // level 1 smoothed at once where level 0 is (irregular or open
         // surfaces): round 5, same box (profiles/r05_ab/sa1/): R3 742 ->
         // 842 timesteps/s (53.6 -> 41.8 PCG its), S1 905 (with the level-1
-        // W-cycle) -> 995 (44.8 its; with both, 5 of 1536 solves broke down)
+        // W-cycle, since removed) -> 995 (44.8 its)
         const bool l0_smooth = prm.nown < 0 && prm.a2 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat));
         p1.smooth1 = prm.smooth1 > 0 ? prm.smooth1 : (prm.smooth1 < 0 && l0_smooth ? 1 : 0);
         build_amg(m->pat, e.data(), p1, *built);
         // auto: a closed surface whose coarse aggregates turn strongly (the
         // median sigma_3 / sigma_1 of their near-null blocks >= kFoldCurl at
         // some level: folds at the coarse levels' scale) is rebuilt with
-        // level 1's prolongator smoothed. Round 5, same box
-        // (profiles/r05_ab/sa1/): F3 (curl 0.46-0.51) 2003 -> 2292
-        // timesteps/s, 31.0 -> 26.2 PCG its, against the level-1 W-cycle's
-        // 2003 (23.0 its with both: 2131); C3 (curl <= 0.25) gains no
-        // iteration (17.0) and loses 12 % to the level-1 product; on the
-        // open S1 it breaks solves down (19 of 3072 recovered: the twice
-        // smoothed product cancels too much in fp32)
+        // the prolongators of levels 0 and 1 smoothed (unless MOF_AMG_SMOOTH
+        // = 0 keeps level 0 tentative). Round 5, same box
+        // (profiles/r05_ab/sa1/): level 1 alone, F3 (curl 0.46-0.51) 2003 ->
+        // 2292 timesteps/s, 31.0 -> 26.2 PCG its; C3 (curl <= 0.25) gains no
+        // iteration (17.0) and loses 12 % to the level-1 product. Round 6,
+        // same box (profiles/r06/f3_fold/): level 0 as well, with the
+        // regular mesh's storage formats kept (below), F3 2548 / 2584 ->
+        // 2794 / 2797 timesteps/s, 26.2 -> 17.5 its (level 0 smoothed with
+        // the irregular meshes' fp32 iterates: 19.0 its, 2546)
         if (prm.smooth1 < 0 && p1.smooth1 == 0 && prm.nown < 0 && prm.a2 && !built->levels.empty() &&
             !built->levels[0].smoothed && built->max_curl >= kFoldCurl) {
             const double curl = built->max_curl;
             p1.smooth1 = 1;
+            if (prm.smooth != 0) p1.smooth = 1;
             auto again = std::make_shared<AmgHierarchy>();
             build_amg(m->pat, e.data(), p1, *again);
             again->max_curl = curl;
@@ -1876,8 +1879,12 @@ bool amg_build(mof_mesh *m) {
     // prolongator it runs (round 3: R3 forced onto the tentative P took
     // 146.5 PCG its/timestep with the regular meshes' choices)
     // (round 4: and closed -- an open patch's near-null modes suffer from
-    // the bf16 iterates as from the stronger coarse damping)
-    G.regular = !H.levels[0].smoothed && !amg_auto_smooth(m->pat) && !open_surface;
+    // the bf16 iterates as from the stronger coarse damping). The choice
+    // follows the mesh, not the prolongator: a regular closed mesh keeps
+    // them with a smoothed level 0 too (round 6: F3 folded 17.5 its, +9 %;
+    // C3 forced smoothed, round 5: 3653-3730 vs 3253-3268 timesteps/s
+    // without them)
+    G.regular = !amg_auto_smooth(m->pat) && !open_surface;
     G.xm = G.regular ? 1 : 2;
     // coarse-level damping: 1.1 on regular meshes (round 2, C3 17.2 -> 17.0
     // its, +1.8 %; C2 mixed +2 %), 1.05 otherwise (R3 as measured; 1.2
