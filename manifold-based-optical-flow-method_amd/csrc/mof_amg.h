@@ -98,8 +98,12 @@ struct AmgHierarchy {
 };
 
 // the fold criterion on AmgHierarchy::max_curl (amg_build): F3 0.46-0.51, the
-// jittered spheres <= 0.25 at every resolution, R3 0.09, S1 0.03
+// jittered spheres 0.13 (C2) / 0.25 (C3) / 0.41 (C5: the 0.5 % jitter is
+// rough against a 640k mesh's edges), R3 0.09, S1 0.03
 constexpr double kFoldCurl = 0.35;
+// ... and level 0's too when the finest aggregates' median turn is below
+// this (folded, not rough: F3 0.07, C3 0.20, C5 0.34)
+constexpr double kFlatCurl = 0.15;
 
 void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &prm,
                AmgHierarchy &H);

@@ -1836,8 +1836,12 @@ bool amg_build(mof_mesh *m) {
         // auto: a closed surface whose coarse aggregates turn strongly (the
         // median sigma_3 / sigma_1 of their near-null blocks >= kFoldCurl at
         // some level: folds at the coarse levels' scale) is rebuilt with
-        // the prolongators of levels 0 and 1 smoothed (unless MOF_AMG_SMOOTH
-        // = 0 keeps level 0 tentative). Round 5, same box
+        // level 1's prolongator smoothed, and level 0's too where the finest
+        // aggregates stay flat (curl[0] < kFlatCurl: a folded surface, not a
+        // rough one -- the 640k jittered sphere C5 turns 0.34 at level 0 and
+        // loses 9 % with level 0 smoothed, 945 -> 859 timesteps/s at 15.2 ->
+        // 13.0 its, profiles/r06/sweep/C5.json; F3 turns 0.07 there;
+        // MOF_AMG_SMOOTH = 0 keeps level 0 tentative). Round 5, same box
         // (profiles/r05_ab/sa1/): level 1 alone, F3 (curl 0.46-0.51) 2003 ->
         // 2292 timesteps/s, 31.0 -> 26.2 PCG its; C3 (curl <= 0.25) gains no
         // iteration (17.0) and loses 12 % to the level-1 product. Round 6,
@@ -1849,7 +1853,7 @@ bool amg_build(mof_mesh *m) {
             !built->levels[0].smoothed && built->max_curl >= kFoldCurl) {
             const double curl = built->max_curl;
             p1.smooth1 = 1;
-            if (prm.smooth != 0) p1.smooth = 1;
+            if (prm.smooth != 0 && !built->curl.empty() && built->curl[0] < kFlatCurl) p1.smooth = 1;
             auto again = std::make_shared<AmgHierarchy>();
             build_amg(m->pat, e.data(), p1, *again);
             again->max_curl = curl;
