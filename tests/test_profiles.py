@@ -71,8 +71,8 @@ def test_roofline_reproduces_from_trace_b1536_final():
 
 def test_pmc_summary_reproduces_committed_entry_b1536(tmp_path):
     dst = tmp_path / "pmc.json"
-    _run("profiles/pmc_summary.py", "profiles/r05_pmc_fetch_c3_mixed_amg_b1536.csv",
-         "profiles/r05_pmc_write_c3_mixed_amg_b1536.csv", str(dst), "C3/mixed/amg/B1536", "6144")
+    _run("profiles/pmc_summary.py", "profiles/r06/pmc_fetch_c3_mixed_amg_b1536.csv",
+         "profiles/r06/pmc_write_c3_mixed_amg_b1536.csv", str(dst), "C3/mixed/amg/B1536", "6144")
     mine = json.load(open(dst))["C3/mixed/amg/B1536"]
     ref = json.load(open(os.path.join(P, "pmc_traffic.json")))["C3/mixed/amg/B1536"]
     assert mine["kernels"].keys() == ref["kernels"].keys()
@@ -103,6 +103,37 @@ def test_pmc_summary_reproduces_committed_entry(tmp_path):
     for k, v in ref["kernels"].items():
         assert mine["kernels"][k]["hbm_bytes_per_launch"] == pytest.approx(v["hbm_bytes_per_launch"])
     assert mine["run"]["hbm_bytes_per_timestep"] == pytest.approx(ref["run"]["hbm_bytes_per_timestep"])
+
+
+def test_roofline_check_reproduces_r06_line():
+    """The final build's default configuration: the line's SpMV roofline
+    from its own rocprof trace, within 1 %."""
+    out = json.loads(_run("profiles/roofline_check.py", "profiles/r06/c3_b1536_bench_under_rocprof.json",
+                          "profiles/r06/c3_mixed_amg_b1536_kernel_trace.csv", "C3/mixed/amg/B1536"))
+    assert abs(out["rel_diff"]) < 0.01 and out["rocprof_frac"] >= 0.65, out
+
+
+def test_kernel_rates_table():
+    out = _run("profiles/kernel_rates.py", "profiles/r06/c3_mixed_amg_b1536_kernel_trace.csv",
+               "profiles/r06/pmc_fetch_c3_mixed_amg_b1536.csv", "profiles/r06/pmc_write_c3_mixed_amg_b1536.csv")
+    rows = [r for r in out.splitlines() if r.startswith("| `k_pcg_spmv<float, false")]
+    assert rows and "31.36 GB" in rows[0]
+    assert out.strip() == open(os.path.join(P, "r06", "kernel_rates_c3_b1536.md")).read().strip()
+
+
+def test_r06_default_line_with_legs():
+    """The round-6 default line carries the reference's mesh class as legs
+    (F3, S1s), each with its parity, iterations and roofline, and no defect."""
+    lines = [l for l in open(os.path.join(P, "r06", "bench_default_c6.json")) if l.startswith("{")]
+    line = json.loads(lines[-1])
+    assert "defect" not in line and line["solver"]["recovered"] == 0
+    legs = {leg["config"]: leg for leg in line["legs"]}
+    assert set(legs) == {"F3", "S1s"}
+    for leg in legs.values():
+        assert leg["solver"]["recovered"] == leg["solver"]["failed"] == 0
+        assert leg["parity"]["max_abs_err"] < 1e-6 * max(1.0, leg["parity"]["max_abs_V"])
+        assert leg["roofline"]["frac"] > 0
+    assert legs["F3"]["solver"]["pcg_iterations_per_timestep"] <= 20
 
 
 def test_headline_line_contract():
