@@ -1898,7 +1898,7 @@ bool amg_build(mof_mesh *m) {
     // measured in rounds 5-6 and removed: slower than level 1's smoothed
     // prolongator on every mesh (S1 905 vs 995, F3 1934 vs 2292, C3 3370 vs
     // 3652 timesteps/s, profiles/r05_ab/wcycle/), and together with it it
-    // broke 15 of 4608 S1 solves down: the cycle below level 1 over-corrects
+    // broke 15 of 3072 S1 solves down: the cycle below level 1 over-corrects
     // there (lambda(B2 A2) up to 2.2 with the coarse damping 1.05,
     // tools/wcycle_study.py), which a V-cycle tolerates and the second
     // coarse correction of a W-cycle does not)
