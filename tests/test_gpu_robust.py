@@ -498,3 +498,30 @@ def test_clones_while_prepare_pending():
     assert rcs == [0] * 4, rcs
     assert st["failed"] == st["recovered"] == 0
     assert np.array_equal(V, V0)
+
+
+def test_met_residual_never_fails_under_an_unreachable_error_bar():
+    """A system whose residual has met rtol and that only keeps refining for
+    the error estimate must not end failed, whatever its later inner solves
+    do (round-5 advisor): with an error bar no estimate can reach (etol
+    1e-18; the refinement reaches ~1e-16) every system refines to
+    max_outer, its later inner solves run on
+    residuals at the rounding level (where a stagnation or breakdown would
+    otherwise NaN-fill it, recovery off), and every system still retires
+    with the iterate that met rtol -- V within the bar of spsolve."""
+    from scipy.sparse.linalg import spsolve
+    p, t, n, a = synth.mesh_for_config("S1s")
+    T = 9
+    I = synth.config_wave("S1s", p, T)
+    tk = np.arange(float(T))
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, tk, 0, T - 1, 0.01, precision="mixed", precond="amg", etol=1e-18, max_outer=6,
+                          recovery=False)
+    m.close()
+    assert st["failed"] == 0 and st["max_rel_residual"] <= 1e-8, st
+    assert st["outer_steps"] == 6 and st["max_err_est"] > 1e-18, st
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    for k in (0, T - 2):
+        Ao, fo = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[k], I[k + 1], 1.0)
+        Vo = spsolve(Ao.tocsc(), fo)
+        assert np.abs(V[k] - Vo).max() < VTOL * max(1.0, np.abs(Vo).max()), k
