@@ -153,8 +153,10 @@ struct AmgDevice {
     // open surfaces: extra level-0 sweeps on the boundary rows and their
     // neighbour ring (k_bsweep); bsw_n rows (0: none), bsw_pos[N] = the row's
     // index in bsw_rows or -1
-    int32_t bsw_n = 0, bsw_sweeps = 0;
-    DevArray<int32_t> bsw_rows, bsw_pos;
+    // (k_bsweep: the ring as its own SELL-64 matrix, mof_amg.hip)
+    int32_t bsw_n = 0, bsw_sweeps = 0, bsw_N = 0, bsw_nout = 0, bsw_nslot = 0;
+    DevArray<int32_t> bsw_rows, bsw_roff, bsw_wrow, bsw_xsrc, bsw_bsrc, bsw_ocol;
+    DevArray<uint32_t> bsw_A;  // [cap][bsw_nslot] bf16 blocks (uint2), per batch
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)

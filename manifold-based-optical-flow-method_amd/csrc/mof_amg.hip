@@ -1672,61 +1672,131 @@ __global__ __launch_bounds__(kWG) MOF_ROW_OCC void k_post0_ns(int32_t N, int32_t
 // on the boundary rows and their neighbour ring only, after the fused
 // pre-smoothing and before the post-smoothing (the cycle stays symmetric).
 // At a Neumann boundary vertex the diagonal block lacks the missing
-// triangles, so one damped sweep leaves those rows least smoothed. One
-// workgroup per system; the subset's iterates live in LDS (two buffers: a
-// Jacobi sweep reads only the previous one), rows outside the subset are
-// read from x and do not change. F32X: x as fp32 pairs (the corrected
-// iterate with xm = 2), else the bf16 x0 format.
-constexpr int kBswWG = 1024, kBswMax = 4096;
+// triangles, so one damped sweep leaves those rows least smoothed.
+// The ring is its own small SELL-64 matrix (per mesh, host-built: ring
+// position p's slot t at bsw_roff[p/64] + 64 t + p%64, the same slots in the
+// same order as the row's level-0 SELL slots, padding included): per slot
+// the operand's source, a ring position (>= 0), an outside column (-1 - k:
+// bsw_ocol[k]) or none (kBswOff), and per batch the slot's bf16 block
+// gathered (transposed where the symmetric reads would) from the level-0
+// sweep copy by k_bsw_extract. One workgroup per system: the ring's iterates
+// (two buffers: a Jacobi sweep reads only the previous one) and the outside
+// operands, which do not change, live in LDS; the blocks stream coalesced.
+// The same products summed in the same order as spmv_row_hx_ns: the same
+// bits as the level-0 kernels' arithmetic. Round 6: the first version read
+// the ring rows' slots in place (three dependent trips per slot, one
+// scattered line per block): 705 us per 2-sweep launch on S1, 1536 systems.
+// F32X: x as fp32 pairs (the corrected iterate with xm = 2), else the bf16
+// x0 format.
+constexpr int kBswWG = 1024;
+constexpr int32_t kBswOff = INT32_MIN;
+constexpr int64_t kBswLdsMax = 160 * 1024;  // a workgroup may take the CU's whole LDS (gfx950)
+struct BswArgs {
+    int32_t N, nbr, nout, nslot;
+    const int32_t *rows, *roff, *wrow, *xsrc, *ocol;
+    const uint2 *A;  // [cap][nslot] blocks
+};
 template <bool F32X>
-__global__ __launch_bounds__(kBswWG) void k_bsweep(int32_t N, int32_t nbr, const int32_t *__restrict__ rows,
-                                                   const int32_t *__restrict__ pos, SysMap sm, MatH mat,
-                                                   const float *__restrict__ rv, float *__restrict__ xv, float omega,
-                                                   int32_t sweeps, const int32_t *__restrict__ sysi) {
+__device__ __forceinline__ float2 bsw_ldx(const float *xv, int64_t vj) {
+    if constexpr (F32X)
+        return reinterpret_cast<const float2 *>(xv)[vj];
+    else
+        return ld_x0(xv, vj);
+}
+// per batch: the ring slots' blocks of every system from the level-0 copy
+__global__ __launch_bounds__(kWG) void k_bsw_extract(int32_t nslot, int32_t B, const int32_t *__restrict__ bsrc,
+                                                     const uint2 *__restrict__ A0h, int64_t sell_nb,
+                                                     uint2 *__restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * kWG + threadIdx.x;
+    if (q >= (int64_t)nslot * B) return;
+    const int32_t b = (int32_t)(q / nslot), t = (int32_t)(q - (int64_t)b * nslot);
+    const int32_t src = bsrc[t];
+    uint2 h = make_uint2(0u, 0u);
+    if (src >= 0) {
+        h = h0_ld(A0h, (int64_t)b * sell_nb + (src & kMirPos));
+        if (src & kMirT) h = h0_tr(h);
+    }
+    out[q] = h;
+}
+template <bool F32X>
+__global__ __launch_bounds__(kBswWG) void k_bsweep(BswArgs a, SysMap sm, const float *__restrict__ rv,
+                                                   float *__restrict__ xv, float omega, int32_t sweeps,
+                                                   const int32_t *__restrict__ sysi) {
 #pragma clang fp contract(off)
-    __shared__ float2 xs[2][kBswMax];
+    extern __shared__ float2 bsw_lds[];  // [2][nbr] iterates, [nout] outside operands
     if ((int32_t)blockIdx.x >= sm.n) return;
     const int32_t b = sm_b(sm, blockIdx.x);
     if (retired(sysi, b)) return;
-    const int64_t vb = (int64_t)b * N;
-    auto ldg = [&](int32_t j) -> float2 {
-        if constexpr (F32X)
-            return reinterpret_cast<const float2 *>(xv)[vb + j];
-        else
-            return ld_x0(xv, vb + j);
-    };
-    for (int32_t p = threadIdx.x; p < nbr; p += kBswWG) xs[0][p] = ldg(rows[p]);
+    const int64_t vb = (int64_t)b * a.N;
+    float2 *xs[2] = {bsw_lds, bsw_lds + a.nbr};
+    float2 *xo = bsw_lds + 2 * a.nbr;
+    for (int32_t p = threadIdx.x; p < a.nbr; p += kBswWG) xs[0][p] = bsw_ldx<F32X>(xv, vb + a.rows[p]);
+    for (int32_t k = threadIdx.x; k < a.nout; k += kBswWG) xo[k] = bsw_ldx<F32X>(xv, vb + a.ocol[k]);
     __syncthreads();
+    const uint2 *Ab = a.A + (int64_t)b * a.nslot;
+    constexpr int U = kPost0U;
     int cur = 0;
     for (int32_t k = 0; k < sweeps; ++k) {
-        for (int32_t p = threadIdx.x; p < nbr; p += kBswWG) {
-            const int32_t i = rows[p];
-            const int32_t bs[1] = {b};
-            float y[1][2];
-            uint2 dg[1];
-            auto xl = [&](int, int32_t j) -> float2 {
-                const int32_t q = pos[j];
-                return q >= 0 ? xs[cur][q] : ldg(j);
-            };
-            if (mat.sell_mir)
-                spmv_row_hx_ns<true, 1, kPost0U>(mat, bs, i, xl, y, dg);
-            else
-                spmv_row_hx_ns<false, 1, kPost0U>(mat, bs, i, xl, y, dg);
-            const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + i];
-            const float2 ds = bf16_diag_solve(dg[0], ri.x - y[0][0], ri.y - y[0][1]);
+        for (int32_t p = threadIdx.x; p < a.nbr; p += kBswWG) {
+            const int32_t base = a.roff[p >> 6] + (p & 63), w = a.wrow[p];
+            const float2 ri = reinterpret_cast<const float2 *>(rv)[vb + a.rows[p]];
+            float acc0 = 0.f, acc1 = 0.f;
+            uint2 dg = make_uint2(0u, 0u);
+            for (int32_t t0 = 0; t0 < w; t0 += U) {
+                int32_t src[U];
+                uint2 blk[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int32_t q = base + min(t0 + u, w - 1) * kSlice;
+                    src[u] = a.xsrc[q];
+                    blk[u] = Ab[q];
+                }
+                if (t0 == 0) dg = blk[0];  // slot 0: the diagonal block
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const bool on = t0 + u < w && src[u] != kBswOff;
+                    float2 xj = make_float2(0.f, 0.f);
+                    if (on) xj = src[u] >= 0 ? xs[cur][src[u]] : xo[-1 - src[u]];
+                    float e00, e01, e10, e11;
+                    h0_dec(blk[u], e00, e01, e10, e11);
+                    acc0 += on ? e00 * xj.x + e01 * xj.y : 0.f;
+                    acc1 += on ? e10 * xj.x + e11 * xj.y : 0.f;
+                }
+            }
+            const float2 ds = bf16_diag_solve(dg, ri.x - acc0, ri.y - acc1);
             const float2 xi = xs[cur][p];
             xs[cur ^ 1][p] = make_float2(xi.x + omega * ds.x, xi.y + omega * ds.y);
         }
         __syncthreads();
         cur ^= 1;
     }
-    for (int32_t p = threadIdx.x; p < nbr; p += kBswWG) {
+    for (int32_t p = threadIdx.x; p < a.nbr; p += kBswWG) {
         const float2 v = xs[cur][p];
         if constexpr (F32X)
-            reinterpret_cast<float2 *>(xv)[vb + rows[p]] = v;
+            reinterpret_cast<float2 *>(xv)[vb + a.rows[p]] = v;
         else
-            st_x0(xv, vb + rows[p], v.x, v.y);
+            st_x0(xv, vb + a.rows[p], v.x, v.y);
     }
+}
+BswArgs bsw_args(const AmgDevice &G) {
+    BswArgs a;
+    a.N = G.bsw_N;
+    a.nbr = G.bsw_n;
+    a.nout = G.bsw_nout;
+    a.nslot = G.bsw_nslot;
+    a.rows = G.bsw_rows.p;
+    a.roff = G.bsw_roff.p;
+    a.wrow = G.bsw_wrow.p;
+    a.xsrc = G.bsw_xsrc.p;
+    a.ocol = G.bsw_ocol.p;
+    a.A = reinterpret_cast<const uint2 *>(G.bsw_A.p);
+    return a;
+}
+template <bool F32X>
+void launch_bsweep(const AmgDevice &G, SysMap sm, const float *rv, float *xv, float omega, const int32_t *sysi,
+                   hipStream_t s) {
+    const size_t lds = sizeof(float2) * (2 * (size_t)G.bsw_n + G.bsw_nout);
+    k_bsweep<F32X><<<dim3((unsigned)sm.n), kBswWG, lds, s>>>(bsw_args(G), sm, rv, xv, omega, G.bsw_sweeps, sysi);
 }
 
 template <int XM, bool ZH, typename... Args>
@@ -1832,6 +1902,13 @@ bool amg_build(mof_mesh *m) {
         // W-cycle, since removed) -> 995 (44.8 its)
         const bool l0_smooth = prm.nown < 0 && prm.a2 && prm.smooth != 0 && (prm.smooth > 0 || amg_auto_smooth(m->pat));
         p1.smooth1 = prm.smooth1 > 0 ? prm.smooth1 : (prm.smooth1 < 0 && l0_smooth ? 1 : 0);
+        // open surfaces: every explicit coarse level smoothed (with the
+        // boundary sweeps below; round 6, same box, profiles/r06/bsw/): S1
+        // 1,188 -> 1,377 timesteps/s, 42.9 -> 35.5 PCG its (alone, without the
+        // sweeps: 1,121 at 46.1 its -- the CPU prototype agrees, 36 -> 36
+        // its to 1e-8 alone, 30 with them, tools/amg_proto.py); S1m / S1s
+        // have no explicit level past 1 (the same hierarchy)
+        if (open_surface && p1.smooth1 == 1) p1.smooth1 = 2;
         build_amg(m->pat, e.data(), p1, *built);
         // auto: a closed surface whose coarse aggregates turn strongly (the
         // median sigma_3 / sigma_1 of their near-null blocks >= kFoldCurl at
@@ -1915,16 +1992,16 @@ bool amg_build(mof_mesh *m) {
     };
     // open surfaces: the boundary rows (fewer incident triangles than
     // neighbours: the diagonal block's contribution list has one entry per
-    // incident triangle) and one ring of their neighbours, for k_bsweep.
-    // Auto: 2 sweeps per side where that ring is >= 1/20 of the rows. Round
-    // 5, one box (profiles/r05_ab/bsw/): S1s (ring 14 % of 3,249 rows) 28.6
-    // -> 19.8 PCG its/timestep, 25.8-26.3k -> 26.9-27.5k timesteps/s (two
-    // launches more per cycle on a launch-bound mesh); S1 (ring 2 %) 44.8 ->
-    // 42.9 its, 1151-1154 -> 1142-1147 (the CPU prototype's 10 -> 9 its to
-    // 1e-4, tools/amg_proto.py bsw=2). MOF_AMG_BSW = sweeps per side (0 off)
-    // forces it on any open surface whose ring fits the sweep kernel's LDS
-    // (kBswMax rows; a larger ring keeps no boundary sweeps, said under
-    // MOF_VERBOSE).
+    // incident triangle) and one ring of their neighbours, for k_bsweep: 2
+    // sweeps per side on every open surface whose ring fits the sweep
+    // kernel's LDS (a larger ring keeps no boundary sweeps, said under
+    // MOF_VERBOSE); MOF_AMG_BSW = sweeps per side (0 off). Round 5 (one
+    // workgroup reading the ring rows in place, 705 us per launch on S1) ran
+    // them only where the ring is >= 1/20 of the rows (S1s, 14 %: 28.6 ->
+    // 19.8 PCG its/timestep); round 6, the ring as its own SELL matrix (180
+    // us), same box (profiles/r06/bsw/): S1s 27,458 -> 29,287 timesteps/s
+    // (same bits), S1m (ring 4 %) 4,646 -> 6,012 at 43.9 -> 30.9 its, S1
+    // (2 %, with its coarse levels smoothed, above) 1,148 -> 1,377.
     G.bsw_n = 0;
     G.bsw_sweeps = 0;
     int32_t bsw = -1;
@@ -1947,15 +2024,77 @@ bool amg_build(mof_mesh *m) {
                 pos[i] = (int32_t)rows.size();
                 rows.push_back(i);
             }
-        const bool want = bsw > 0 || 20 * (int64_t)rows.size() >= m->N;
-        if (want && rows.size() > (size_t)kBswMax && knob(Knob::Verbose))
-            std::fprintf(stderr, "mof amg: boundary ring of %zu rows exceeds the sweep kernel's %d: no boundary sweeps\n",
-                         rows.size(), kBswMax);
-        if (want && !rows.empty() && rows.size() <= (size_t)kBswMax) {
-            put_i(G.bsw_rows, rows);
-            put_i(G.bsw_pos, pos);
-            G.bsw_n = (int32_t)rows.size();
-            G.bsw_sweeps = bsw > 0 ? bsw : 2;
+        if (!rows.empty()) {
+            // the ring's SELL-64 matrix: ring position p's slots are row
+            // rows[p]'s level-0 slots (spmv_row_hx_ns's order and masks)
+            const int32_t nbr = (int32_t)rows.size(), nrs = (nbr + kSlice - 1) / kSlice;
+            std::vector<int32_t> mir;
+            if (m->sym_reads) mir = sell_mirror(P, m->n_own, 1, nullptr);
+            std::vector<int32_t> wrow(nbr), roff(nrs + 1, 0), ocol, opos(m->N, -1);
+            for (int32_t p = 0; p < nbr; ++p) {
+                const int32_t s0 = rows[p] / kSlice;
+                wrow[p] = (int32_t)((P.sell_off[s0 + 1] - P.sell_off[s0]) / kSlice);
+            }
+            for (int32_t r = 0; r < nrs; ++r) {
+                int32_t wmax = 0;
+                for (int32_t p = r * kSlice; p < std::min(nbr, (r + 1) * kSlice); ++p) wmax = std::max(wmax, wrow[p]);
+                roff[r + 1] = roff[r] + wmax * kSlice;
+            }
+            const int32_t nslot = roff[nrs];
+            std::vector<int32_t> xsrc(nslot, kBswOff), bsrc(nslot, -1);
+            for (int32_t p = 0; p < nbr; ++p) {
+                const int32_t i = rows[p], s0 = i / kSlice, l = i % kSlice;
+                const int64_t o = P.sell_off[s0];
+                const int32_t w = wrow[p];
+                const int32_t wl = m->sym_reads ? w : std::min(w, P.vptr[i + 1] - P.vptr[i]);
+                for (int32_t t = 0; t < w; ++t) {
+                    const int64_t pp = o + (int64_t)std::min(t, wl - 1) * kSlice + l;
+                    const int32_t j = P.sell_col[pp];
+                    int32_t src = (int32_t)pp;
+                    bool on = t < wl;
+                    if (m->sym_reads) {
+                        const int32_t mr = mir[pp];
+                        on = on && mr >= 0;
+                        src = mr < 0 ? (int32_t)(o + l) : mr;  // position | kMirT (transposed)
+                    }
+                    if (!on) continue;
+                    const int64_t q = roff[p / kSlice] + (int64_t)t * kSlice + p % kSlice;
+                    bsrc[q] = src;
+                    if (pos[j] >= 0) {
+                        xsrc[q] = pos[j];
+                    } else {
+                        if (opos[j] < 0) {
+                            opos[j] = (int32_t)ocol.size();
+                            ocol.push_back(j);
+                        }
+                        xsrc[q] = -1 - opos[j];
+                    }
+                }
+            }
+            const int64_t lds = (int64_t)sizeof(float2) * (2 * (int64_t)nbr + (int64_t)ocol.size());
+            if (lds > kBswLdsMax) {
+                if (knob(Knob::Verbose))
+                    std::fprintf(stderr, "mof amg: boundary ring of %d rows needs %lld B of LDS: no boundary sweeps\n",
+                                 nbr, (long long)lds);
+            } else {
+                put_i(G.bsw_rows, rows);
+                put_i(G.bsw_roff, roff);
+                put_i(G.bsw_wrow, wrow);
+                put_i(G.bsw_xsrc, xsrc);
+                put_i(G.bsw_bsrc, bsrc);
+                put_i(G.bsw_ocol, ocol);
+                G.bsw_N = m->N;
+                G.bsw_n = nbr;
+                G.bsw_nout = (int32_t)ocol.size();
+                G.bsw_nslot = nslot;
+                G.bsw_sweeps = bsw > 0 ? bsw : 2;
+                if (lds > 64 * 1024) {
+                    MOF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_bsweep<true>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                    MOF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_bsweep<false>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                }
+            }
         }
     }
     for (size_t l = 0; l < H.levels.size(); ++l) {
@@ -2103,6 +2242,7 @@ void amg_ensure(mof_mesh *m, int32_t B) {
         }
     }
     G.cinv.alloc((size_t)G.nc * G.nc * B);
+    if (G.bsw_n > 0) G.bsw_A.alloc((size_t)2 * G.bsw_nslot * B);  // the ring slots' blocks (uint2)
     G.cap = B;
     MOF_HIP(hipStreamSynchronize(s));
 }
@@ -2141,6 +2281,12 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
             nb0, reinterpret_cast<const float4 *>(w.A32.p), reinterpret_cast<uint2 *>(G.A0h.p));
     }
     G.bf16_fresh = false;
+    if (G.bsw_n > 0) {
+        const int64_t n = (int64_t)G.bsw_nslot * B;
+        k_bsw_extract<<<dim3((unsigned)((n + kWG - 1) / kWG)), kWG, 0, s>>>(
+            G.bsw_nslot, B, G.bsw_bsrc.p, reinterpret_cast<const uint2 *>(G.A0h.p), m->pat.sell_nb(),
+            reinterpret_cast<uint2 *>(G.bsw_A.p));
+    }
     // a dispatch's grid is at most 2^32 - 1 work-items: a by-entry product
     // whose (group, system pair) grid would pass it (a batch of 1024 over
     // more than ~32k entry groups) takes the per-position kernel -- the same
@@ -2301,9 +2447,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
     for (int32_t l = 0; l < 1; ++l) {
         const int32_t smooth = l + 1 < L - 1;
         if (l == 0) {
-            if (G.bsw_n > 0)
-                k_bsweep<false><<<dim3((unsigned)nL), kBswWG, 0, s>>>(v[0].n, G.bsw_n, G.bsw_rows.p, G.bsw_pos.p, sm,
-                                                                     mat0, r0, v[0].x, om, G.bsw_sweeps, sysi);
+            if (G.bsw_n > 0) launch_bsweep<false>(G, sm, r0, v[0].x, om, sysi, s);
             k_res0_ns<kRes0NS><<<dim3(xcd_grid(nblk, (nL + kRes0NS - 1) / kRes0NS,
                                                kGrpSmooth > kRes0NS ? kGrpSmooth / kRes0NS : 1)),
                                  kWG, 0, s>>>(v[0].n, nblk, B, sm, mat0, r0, v[0].x,
@@ -2340,9 +2484,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                     k_prolong0_sa<2><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<2><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
-                if (G.bsw_n > 0)
-                    k_bsweep<true><<<dim3((unsigned)nL), kBswWG, 0, s>>>(v[0].n, G.bsw_n, G.bsw_rows.p, G.bsw_pos.p,
-                                                                        sm, mat0, r0, v[0].y, om, G.bsw_sweeps, sysi);
+                if (G.bsw_n > 0) launch_bsweep<true>(G, sm, r0, v[0].y, om, sysi, s);
                 if (zh)
                     launch_post0<2, true>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].y, om, sysi, z0, part_slot, rd);
                 else
@@ -2352,9 +2494,7 @@ void amg_vcycle(mof_mesh *m, int32_t B, const float *r0, float *z0, double *part
                     k_prolong0_sa<1><<<gsa, kWG, 0, s>>>(v[0], v[1], nb0, B, sysi);
                 else
                     k_prolong0<1><<<gp, kWG, 0, s>>>(v[0], v[1], nb0p, B, sysi);
-                if (G.bsw_n > 0)
-                    k_bsweep<false><<<dim3((unsigned)nL), kBswWG, 0, s>>>(v[0].n, G.bsw_n, G.bsw_rows.p, G.bsw_pos.p,
-                                                                         sm, mat0, r0, v[0].x, om, G.bsw_sweeps, sysi);
+                if (G.bsw_n > 0) launch_bsweep<false>(G, sm, r0, v[0].x, om, sysi, s);
                 if (zh)
                     launch_post0<1, true>(nblk, nL, s, v[0].n, nblk, B, sm, mat0, r0, v[0].x, om, sysi, z0, part_slot, rd);
                 else

@@ -301,15 +301,17 @@ def test_open_patch_batch_split_bit_identical():
     assert s1["iterations"] == s41["iterations"]
 
 
-def test_open_patch_boundary_sweeps(monkeypatch):
-    """An open patch whose boundary ring is >= 1/20 of its rows (S1s: 14 %)
-    takes two extra block-Jacobi sweeps per side on those rows (k_bsweep):
-    fewer PCG iterations than without them (MOF_AMG_BSW=0: 28.6 vs 19.8 per
-    timestep on the bench), V within 1e-6 of that solve and of the oracle, no
+@pytest.mark.parametrize("cfg", ["S1s", "S1m"])
+def test_open_patch_boundary_sweeps(monkeypatch, cfg):
+    """An open patch takes two extra block-Jacobi sweeps per side on its
+    boundary rows and their neighbour ring (k_bsweep, the ring as its own
+    SELL matrix; S1s: ring 14 % of the rows, S1m 4 %): fewer PCG iterations
+    than without them (MOF_AMG_BSW=0; bench: S1s 28.6 vs 19.8, S1m 43.9 vs
+    30.9 per timestep), V within 1e-6 of that solve and of the oracle, no
     failed or recovered system."""
-    p, t, n, a = synth.mesh_for_config("S1s")
+    p, t, n, a = synth.mesh_for_config(cfg)
     T = 13
-    I = synth.config_wave("S1s", p, T)
+    I = synth.config_wave(cfg, p, T)
     tk = np.arange(float(T))
     res = {}
     for env in ({}, {"MOF_AMG_BSW": "0"}):
