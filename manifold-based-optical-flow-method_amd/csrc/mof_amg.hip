@@ -2088,6 +2088,9 @@ bool amg_build(mof_mesh *m) {
                 G.bsw_nout = (int32_t)ocol.size();
                 G.bsw_nslot = nslot;
                 G.bsw_sweeps = bsw > 0 ? bsw : 2;
+                if (knob(Knob::Verbose))
+                    std::fprintf(stderr, "mof amg: boundary sweeps x%d on a ring of %d rows (%d outside, %lld B of LDS)\n",
+                                 G.bsw_sweeps, nbr, G.bsw_nout, (long long)lds);
                 if (lds > 64 * 1024) {
                     MOF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_bsweep<true>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

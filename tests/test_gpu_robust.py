@@ -259,6 +259,33 @@ def test_s1_full_size_default_vs_spsolve():
         assert err < 2.5e-7 * max(1.0, np.abs(Vo).max()), (k, err)
 
 
+@pytest.mark.timeout(600)
+def test_wide_ring_boundary_sweeps_vs_spsolve(monkeypatch, capfd):
+    """An open patch whose boundary ring needs more than 64 KiB of the sweep
+    kernel's LDS (a 223,729-vertex S1-like patch: ~3,800 ring rows; the
+    launch raises the kernel's dynamic-LDS limit) at the shipped defaults:
+    the sweeps run (said under MOF_VERBOSE), no system needs the recovery,
+    V within 2.5e-7 of max|V| of the reference's spsolve."""
+    from scipy.sparse.linalg import spsolve
+    import re
+    monkeypatch.setenv("MOF_VERBOSE", "1")
+    p, t = synth.electrode_surface(60, spacing=1.2)
+    n, a = synth.vertex_normals(p, t), synth.triangle_areas(p, t)
+    T = 5
+    I = synth.config_wave("S1", p, T)  # the S1 patches' wave across the grid
+    m = DeviceMesh(p, n, t, a)
+    V, st = m.solve_range(I, np.arange(float(T)), 0, T - 1, 0.01, precision="mixed", precond="amg")
+    m.close()
+    log = capfd.readouterr().err
+    hit = re.search(r"boundary sweeps x2 on a ring of (\d+) rows \((\d+) outside, (\d+) B of LDS\)", log)
+    assert hit and int(hit.group(3)) > 65536, log[-2000:]
+    assert st["failed"] == st["recovered"] == 0 and st["max_rel_residual"] <= 1e-8, st
+    a2, gw, e, iw = oracle.geometry(p, n, t, a)
+    Ao, fo = oracle.step_system(a2, gw, e, iw, t, a, 0.01, I[0], I[1], 1.0)
+    Vo = spsolve(Ao.tocsc(), fo)
+    assert np.abs(V[0] - Vo).max() < 2.5e-7 * max(1.0, np.abs(Vo).max())
+
+
 def test_s1s_dropin_defaults_vs_spsolve():
     """The reference's real workload size (S1s: 3,249-vertex S1-like patch,
     98 timesteps, config.yaml:5) through the drop-in's default ("auto")
