@@ -108,8 +108,8 @@ def parse():
                          "1e-7, < 0: the residual test alone)")
     ap.add_argument("--legs", default="auto",
                     help="comma-separated extra configurations timed after the main line on the same GPU, "
-                         "each with its iterations, parity and SpMV roofline (auto: F3,S1s -- the reference's "
-                         "mesh class -- for a 1-GPU C3 line; none: no legs)")
+                         "each with its iterations, parity and SpMV roofline (auto: F3,S1s,S1 -- the "
+                         "reference's mesh class -- for a 1-GPU C3 line; none: no legs)")
     ap.add_argument("--host-batches", type=int, default=4,
                     help="--io device: batches of the host-to-host leg (SURVEY.md 8(d)'s metric) timed after "
                          "the device-resident region (0: none)")
@@ -641,10 +641,10 @@ def main():
         del Vh, I_h
 
     # extra configurations on this GPU (--legs; a 1-GPU C3 line by default:
-    # F3 and S1s, the reference's mesh class), after the main mesh is freed
+    # F3, S1s and S1, the reference's mesh class), after the main mesh is freed
     legs, leg_jobs = [], []
     leg_names = ([] if args.legs == "none" else
-                 (["F3", "S1s"] if args.config == "C3" else []) if args.legs == "auto" else
+                 (["F3", "S1s", "S1"] if args.config == "C3" else []) if args.legs == "auto" else
                  [x for x in args.legs.split(",") if x])
     if world > 1 or dry or host_io:
         leg_names = []

@@ -123,12 +123,14 @@ def test_kernel_rates_table():
 
 def test_r06_default_line_with_legs():
     """The round-6 default line carries the reference's mesh class as legs
-    (F3, S1s), each with its parity, iterations and roofline, and no defect."""
-    lines = [l for l in open(os.path.join(P, "r06", "bench_default_c6.json")) if l.startswith("{")]
+    (F3, S1s, S1), each with its parity, iterations and roofline, and no
+    defect."""
+    lines = [l for l in open(os.path.join(P, "r06", "bench_default_c22.json")) if l.startswith("{")]
     line = json.loads(lines[-1])
     assert "defect" not in line and line["solver"]["recovered"] == 0
     legs = {leg["config"]: leg for leg in line["legs"]}
-    assert set(legs) == {"F3", "S1s"}
+    assert set(legs) == {"F3", "S1s", "S1"}
+    assert legs["S1"]["solver"]["pcg_iterations_per_timestep"] <= 36
     for leg in legs.values():
         assert leg["solver"]["recovered"] == leg["solver"]["failed"] == 0
         assert leg["parity"]["max_abs_err"] < 1e-6 * max(1.0, leg["parity"]["max_abs_V"])
