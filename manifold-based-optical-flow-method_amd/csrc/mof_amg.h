@@ -72,6 +72,10 @@ struct AmgLevel {
     std::vector<float> Qm;                         // the same rows in member (mlist) order
     std::vector<int32_t> gptr;                     // (next sell_nb + 1) Galerkin gather ranges
     std::vector<int32_t> gent;                     // triples {fine SELL pos (| kMirT: transposed), P block of i, P block of j}
+    // as the target of a product (level >= 1): the lower blocks' SELL
+    // positions and their upper twins' (the products cover the diagonal and
+    // upper blocks and write each lower twin as the transpose, st_pair)
+    std::vector<int32_t> low, twin;
     // smoothed prolongator (level 0 with AmgParams::smooth): P rows as blocks
     // (bs x 3 floats each, in Q) with CSR pptr / pcol over the fine nodes, and
     // the restriction lists per coarse node: pairs {fine node, P block}. The
@@ -127,6 +131,7 @@ struct AmgDevLevel {
     bool smoothed = false;                          // level 0: smoothed prolongator
     DevArray<int32_t> pptr, pcol, rptr, rent;
     DevArray<int32_t> rperm;                        // smoothed P: restriction group entries by fine node
+    DevArray<int32_t> twin;                         // level >= 1: each upper block's lower twin position, or -1
     int32_t ngrp = 0, nggrp = 0;
     DevArray<float> Q, Qm;
     // per system, capacity AmgDevice::cap

@@ -168,6 +168,25 @@ __device__ __forceinline__ void st_a9(uint4 *H, uint16_t *H22, int64_t q, const 
         reinterpret_cast<uint32_t *>(H22)[q] = u[8] | (sb << 16);
     }
 }
+// A product's block C at position pos of system b and, for an upper block
+// (tw >= 0: its lower twin's position, AmgLevel::twin), C^T at the twin: the
+// products cover the diagonal and upper blocks only (round 6), and the
+// coarse operator is symmetric to the bit
+__device__ __forceinline__ void st_pair(float *__restrict__ Ac, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
+                                        int64_t b, int64_t c_sell_nb, int64_t pos, int32_t tw,
+                                        const float (&C)[3][3]) {
+    st3(Ac, b * c_sell_nb + pos, C);
+    if (Ah) st_a9(Ah, Ah22, b * c_sell_nb + pos, C);
+    if (tw >= 0) {
+        float T[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) T[r][c] = C[c][r];
+        st3(Ac, b * c_sell_nb + tw, T);
+        if (Ah) st_a9(Ah, Ah22, b * c_sell_nb + tw, T);
+    }
+}
 
 // ---- per-timestep setup --------------------------------------------------
 
@@ -195,7 +214,7 @@ __global__ __launch_bounds__(kWG) void k_to_h0(int64_t n, const float4 *__restri
 constexpr int kGalNS = 4;
 __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22,
@@ -213,6 +232,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
     const int32_t b0 = bq * kGalNS;
     float Cm[kGalNS][3][3] = {};
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
+    if (g0 == g1 && pos != c_diag[I]) return;  // a lower block (its upper twin writes it, st_pair) or padding
     // one gather entry per load batch (92 VGPRs, 5 waves per SIMD) instead
     // of 2 (140, 3 waves): 6.37 -> 5.92 ms per launch (round 3)
     constexpr int U = 1;
@@ -285,8 +305,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
             inv3(Cm[t], D);
             st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
         }
-        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm[t]);
-        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm[t]);
+        st_pair(Ac, Ah, Ah22, b, c_sell_nb, pos, c_twin[pos], Cm[t]);
     }
 }
 
@@ -306,7 +325,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ns(
 constexpr int kGalENS = 2;
 __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
     int32_t ngrp, const int32_t *__restrict__ ggrp, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin, const int32_t *__restrict__ gptr,
     const int32_t *__restrict__ gent, const float *__restrict__ Q, const uint2 *__restrict__ Afh,
     int64_t f_sell_nb, int64_t c_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
@@ -376,10 +395,12 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
         if (I >= nC || b >= B) continue;
         float Cm[3][3] = {};
         const int32_t q0 = first ? tq0 : gptr[pos], q1 = first ? tq1 : gptr[pos + 1];
+        const bool diag = pos == (first ? tdg : c_diag[I]);
+        if (q0 == q1 && !diag) continue;  // a lower block (its upper twin writes it, st_pair) or padding
         for (int32_t q = q0; q < q1; ++q)
 #pragma unroll
             for (int k = 0; k < 9; ++k) Cm[k / 3][k % 3] += con[t][k][q - e0];
-        if (pos == (first ? tdg : c_diag[I])) {
+        if (diag) {
 #pragma unroll
             for (int d = 0; d < 3; ++d)
                 if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
@@ -387,8 +408,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
             inv3(Cm, D);
             st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
         }
-        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
-        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+        st_pair(Ac, Ah, Ah22, b, c_sell_nb, pos, c_twin[pos], Cm);
     }
 }
 
@@ -438,7 +458,7 @@ constexpr int kGalSysPos = kWG / 64;  // coarse positions per workgroup, one per
 template <int BSF>
 __global__ __launch_bounds__(kWG) void k_galerkin_sys(
     int64_t c_sell_nb, int32_t nC, int32_t B, int32_t b0, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin, const int32_t *__restrict__ gptr,
     const int32_t *__restrict__ gent, const float *__restrict__ Q, const float4 *__restrict__ FS,
     float *__restrict__ Ac, uint4 *__restrict__ Dh, uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah,
     uint16_t *__restrict__ Ah22, float4 *__restrict__ CS) {
@@ -453,6 +473,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin_sys(
     const int32_t lane = (int32_t)threadIdx.x & 63;
     float Cm[3][3] = {};
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
+    if (g0 == g1 && pos != c_diag[I]) return;  // a lower block (its upper twin writes it, st_pair) or padding
     // U entries per load batch (the entries' scalar loads, then their fine
     // blocks, in flight together); a batch's tail entries past g1 are
     // clamped to the last one and skipped (wave-uniform)
@@ -525,12 +546,16 @@ __global__ __launch_bounds__(kWG) void k_galerkin_sys(
         inv3(Cm, D);
         st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
     }
-    st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
-    if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+    st_pair(Ac, Ah, Ah22, b, c_sell_nb, pos, c_twin[pos], Cm);
     if (CS) {
         float4 *p = CS + (pos * kSlab + lane) * 3;
 #pragma unroll
         for (int r = 0; r < 3; ++r) p[r] = make_float4(Cm[r][0], Cm[r][1], Cm[r][2], 0.f);
+        if (c_twin[pos] >= 0) {
+            float4 *q = CS + ((int64_t)c_twin[pos] * kSlab + lane) * 3;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) q[r] = make_float4(Cm[0][r], Cm[1][r], Cm[2][r], 0.f);
+        }
     }
 }
 
@@ -544,7 +569,7 @@ constexpr int kGal3NS = 4;
 template <int NS>
 __global__ __launch_bounds__(kWG) void k_galerkin3_ns(
     int64_t c_sell_nb, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin,
     const int32_t *__restrict__ gptr, const int32_t *__restrict__ gent, const float *__restrict__ Q,
     const float *__restrict__ Af, int64_t f_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh,
     uint16_t *__restrict__ Dh22, uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
@@ -558,6 +583,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ns(
     const int32_t b0 = bq * NS;
     float Cm[NS][3][3] = {};
     const int32_t g0 = gptr[pos], g1 = gptr[pos + 1];
+    if (g0 == g1 && pos != c_diag[I]) return;  // a lower block (its upper twin writes it, st_pair) or padding
     for (int32_t g = g0; g < g1; ++g) {
         const int32_t fp = gent[3 * g], ii = gent[3 * g + 1], jj = gent[3 * g + 2];
         float qi[3][3], qj[3][3];
@@ -614,8 +640,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ns(
             inv3(Cm[t], D);
             st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
         }
-        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm[t]);
-        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm[t]);
+        st_pair(Ac, Ah, Ah22, b, c_sell_nb, pos, c_twin[pos], Cm[t]);
     }
 }
 
@@ -625,7 +650,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ns(
 // same bits as k_galerkin3_ns.
 __global__ __launch_bounds__(kWG) void k_galerkin3_ent(
     int32_t ngrp, const int32_t *__restrict__ ggrp, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin, const int32_t *__restrict__ gptr,
     const int32_t *__restrict__ gent, const float *__restrict__ Q, const float *__restrict__ Af, int64_t f_sell_nb,
     int64_t c_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh, uint16_t *__restrict__ Dh22,
     uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
@@ -699,10 +724,12 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ent(
         if (I >= nC || b >= B) continue;
         float Cm[3][3] = {};
         const int32_t q0 = first ? tq0 : gptr[pos], q1 = first ? tq1 : gptr[pos + 1];
+        const bool diag = pos == (first ? tdg : c_diag[I]);
+        if (q0 == q1 && !diag) continue;  // a lower block (its upper twin writes it, st_pair) or padding
         for (int32_t q = q0; q < q1; ++q)
 #pragma unroll
             for (int k = 0; k < 9; ++k) Cm[k / 3][k % 3] += con[t][k][q - e0];
-        if (pos == (first ? tdg : c_diag[I])) {
+        if (diag) {
 #pragma unroll
             for (int d = 0; d < 3; ++d)
                 if (c_dead[3 * (int64_t)I + d]) Cm[d][d] += 1.f;
@@ -710,8 +737,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_ent(
             inv3(Cm, D);
             st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
         }
-        st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
-        if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+        st_pair(Ac, Ah, Ah22, b, c_sell_nb, pos, c_twin[pos], Cm);
     }
 }
 
@@ -730,7 +756,7 @@ constexpr int kGalBig = 128;
 template <int NSB>
 __global__ __launch_bounds__(kWG) void k_galerkin3_big(
     int32_t nbig, const int32_t *__restrict__ gbig, int32_t nC, int32_t B, const int32_t *__restrict__ c_sell_row,
-    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ gptr,
+    const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin, const int32_t *__restrict__ gptr,
     const int32_t *__restrict__ gent, const float *__restrict__ Q, const float *__restrict__ Af, int64_t f_sell_nb,
     int64_t c_sell_nb, float *__restrict__ Ac, uint4 *__restrict__ Dh, uint16_t *__restrict__ Dh22,
     uint4 *__restrict__ Ah, uint16_t *__restrict__ Ah22) {
@@ -825,8 +851,7 @@ __global__ __launch_bounds__(kWG) void k_galerkin3_big(
         inv3(Cm, D);
         st_h9(Dh, Dh22, (int64_t)b * nC + I, D);
     }
-    st3(Ac, (int64_t)b * c_sell_nb + pos, Cm);
-    if (Ah) st_a9(Ah, Ah22, (int64_t)b * c_sell_nb + pos, Cm);
+    st_pair(Ac, Ah, Ah22, b, c_sell_nb, pos, c_twin[pos], Cm);
 }
 constexpr int kGalBigNS = 2;
 
@@ -2107,6 +2132,11 @@ bool amg_build(mof_mesh *m) {
         D.bs = L.bs;
         D.sell_nb = L.sell_nb();
         if (l > 0) {
+            {  // each upper block's lower twin (st_pair), -1 elsewhere
+                std::vector<int32_t> tw((size_t)L.sell_nb(), -1);
+                for (size_t k = 0; k < L.low.size(); ++k) tw[L.twin[k]] = L.low[k];
+                put_i(D.twin, tw);
+            }
             put_i(D.sell_off, L.sell_off);
             put_i(D.sell_col, L.sell_col);
             put_i(D.sell_row, L.sell_row);
@@ -2315,13 +2345,13 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
                 fnb, b0, std::min(kSlab, B - b0), reinterpret_cast<const float4 *>(w.A32.p),
                 reinterpret_cast<float4 *>(G.aslab.p));
             k_galerkin_sys<2><<<sys_grid(C.sell_nb), kWG, 0, s>>>(
-                C.sell_nb, C.n, B, b0, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
+                C.sell_nb, C.n, B, b0, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p,
                 reinterpret_cast<const float4 *>(G.aslab.p), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
                 l1 ? reinterpret_cast<float4 *>(C.slab.p) : nullptr);
             if (l1) {
                 AmgDevLevel &C2 = G.lv[2];
                 k_galerkin_sys<3><<<sys_grid(C2.sell_nb), kWG, 0, s>>>(
-                    C2.sell_nb, C2.n, B, b0, C2.sell_row.p, C2.diag_pos.p, C2.dead.p, C.gptr.p, C.gent.p, C.Q.p,
+                    C2.sell_nb, C2.n, B, b0, C2.sell_row.p, C2.diag_pos.p, C2.dead.p, C2.twin.p, C.gptr.p, C.gent.p, C.Q.p,
                     reinterpret_cast<const float4 *>(C.slab.p), C2.A.p, dh(C2), C2.Dh22.p, ah(C2), ah22(C2), nullptr);
             }
         }
@@ -2332,29 +2362,29 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
         const bool ent = ent_fits(F);
         if (l == 0 && ent)
             k_galerkin0_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
-                F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
+                F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p,
                 reinterpret_cast<const uint2 *>(G.A0h.p), m->pat.sell_nb(), C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C),
                 ah22(C));
         else if (l == 0)
             k_galerkin0_ns<<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGalNS - 1) / kGalNS,
                                            kGrpGal)),
-                             kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p,
+                             kWG, 0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p,
                                           F.Q.p, w.A32.p, m->pat.sell_nb(), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
                                           F.smoothed ? nullptr : reinterpret_cast<const uint2 *>(G.A0h.p));
         else if (ent) {
             if (F.nggrp > 0)
                 k_galerkin3_ent<<<dim3(xcd_grid(F.nggrp, (B + kGalENS - 1) / kGalENS, kGrpGal)), kWG, 0, s>>>(
-                    F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
+                    F.nggrp, F.ggrp.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
                     F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
             if (F.nbig > 0)
                 k_galerkin3_big<kGalBigNS>
                     <<<dim3(xcd_grid(F.nbig, (B + kGalBigNS - 1) / kGalBigNS, kGrpGal)), kWG, 0, s>>>(
-                        F.nbig, F.gbig.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p,
+                        F.nbig, F.gbig.p, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p,
                         F.A.p, F.sell_nb, C.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
         } else
             k_galerkin3_ns<kGal3NS>
                 <<<dim3(xcd_grid((int32_t)((C.sell_nb + kWG - 1) / kWG), (B + kGal3NS - 1) / kGal3NS, kGrpGal)), kWG,
-                   0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
+                   0, s>>>(C.sell_nb, C.n, B, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p, F.A.p,
                            F.sell_nb, C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C));
     }
     AmgDevLevel &Lc = G.lv[L - 1];

@@ -560,12 +560,32 @@ void build_amg(const Pattern &fine, const double *e_internal, const AmgParams &p
                         }
                 }
         }
+        // the coarse operator is symmetric: only its diagonal and upper blocks
+        // get terms; each lower block is its upper twin transposed (C.low /
+        // C.twin, written by st_pair) -- half the product's terms, and the twins
+        // equal to the bit (round 6)
+        std::vector<int32_t> cpos(C.vcol.size(), -1);  // adjacency index -> SELL position
+        for (int64_t pos = 0; pos < (int64_t)C.sell_blk.size(); ++pos)
+            if (C.sell_blk[pos] >= 0) cpos[C.sell_blk[pos]] = (int32_t)pos;
+        C.low.clear();
+        C.twin.clear();
         F.gent.clear();
-        F.gent.reserve(by_block.size());
+        F.gent.reserve(by_block.size() / 2 + 3 * (size_t)C.n);
         for (int64_t pos = 0; pos < (int64_t)C.sell_blk.size(); ++pos) {
             const int32_t p = C.sell_blk[pos];
-            if (p >= 0)
-                F.gent.insert(F.gent.end(), by_block.begin() + 3 * (size_t)cnt[p], by_block.begin() + 3 * (size_t)cnt[p + 1]);
+            if (p >= 0) {
+                const int32_t I = C.sell_row[pos], J = C.sell_col[pos];
+                if (J < I) {
+                    const int32_t q = (int32_t)(std::lower_bound(C.vcol.begin() + C.vptr[J],
+                                                                 C.vcol.begin() + C.vptr[J + 1], I) -
+                                                C.vcol.begin());
+                    C.low.push_back((int32_t)pos);
+                    C.twin.push_back(cpos[q]);
+                } else {
+                    F.gent.insert(F.gent.end(), by_block.begin() + 3 * (size_t)cnt[p],
+                                  by_block.begin() + 3 * (size_t)cnt[p + 1]);
+                }
+            }
             F.gptr[pos + 1] = (int32_t)(F.gent.size() / 3);
         }
         B.swap(Bc);
