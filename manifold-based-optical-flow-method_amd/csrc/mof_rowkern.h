@@ -335,8 +335,12 @@ __device__ __forceinline__ void spmv_row(const MatArgs<V> &mt, int32_t b, int32_
 // (10.2 -> 8.8 ms per 512-system batch), the residual 32 -> 8 system pairs
 // (5.73 -> 5.55 ms per launch); the Galerkin products at 1 instead of 8:
 // -0.7 % timesteps/s.
-constexpr int32_t kGrpSpmv = 8, kGrpSmooth = 8, kGrpRes = 8, kGrpGal = 8, kGrpAsm = 8, kGrpProl = 0,
-                  kGrpRestr = 0;
+// Round 6, rocprof on one box (profiles/r06/xfer_grp/): the transfers from
+// G = B to 8 -- F3's smoothed restriction 1740 -> 1526 us, level 1's 645 ->
+// 402, the smoothed prolongation 1155 -> 1086; C3's tentative prolongation
+// 638 -> 609 (4 / 16 / 32 no better).
+constexpr int32_t kGrpSpmv = 8, kGrpSmooth = 8, kGrpRes = 8, kGrpGal = 8, kGrpAsm = 8, kGrpProl = 8,
+                  kGrpRestr = 8;
 __host__ __device__ __forceinline__ int32_t sys_group(int32_t B, int32_t G) { return G > 0 && G < B ? G : B; }
 
 __host__ __device__ __forceinline__ bool xcd_map_w(int32_t w, int32_t nblk, int32_t B, int32_t &rb, int32_t &sys,
