@@ -125,7 +125,7 @@ def test_r06_default_line_with_legs():
     """The round-6 default line carries the reference's mesh class as legs
     (F3, S1s, S1), each with its parity, iterations and roofline, and no
     defect."""
-    lines = [l for l in open(os.path.join(P, "r06", "bench_default_c22.json")) if l.startswith("{")]
+    lines = [l for l in open(os.path.join(P, "r06", "bench_default_final.json")) if l.startswith("{")]
     line = json.loads(lines[-1])
     assert "defect" not in line and line["solver"]["recovered"] == 0
     legs = {leg["config"]: leg for leg in line["legs"]}
