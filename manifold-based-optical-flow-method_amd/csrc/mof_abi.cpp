@@ -629,7 +629,7 @@ void mesh_build(mof_mesh *m, const double *xyz, const double *nrm, const int32_t
 
 extern "C" {
 
-const char *mof_version(void) { return "mofhip 0.6.2 (gfx950, abi 4)"; }
+const char *mof_version(void) { return "mofhip 0.6.3 (gfx950, abi 4)"; }
 
 int mof_abi_version(void) { return MOF_ABI_VERSION; }
 

@@ -165,8 +165,9 @@ struct AmgDevice {
     std::deque<AmgDevLevel> lv;  // deque: DevArray is not movable
     DevArray<float> cinv;  // [B][nc][nc] coarsest inverse
     DevArray<uint32_t> A0h;  // [B][sell_nb][2] level-0 A in bf16 (smoother sweeps)
-    // smoothed level 0: one slab of 64 systems' fp32 level-0 blocks as
-    // [sell_nb][64][4] (k_a_slab -> k_galerkin0_sys), reused slab by slab
+    // smoothed level 0: one slab of 64 systems' level-0 blocks as
+    // [sell_nb][64] float4 (fp32 A), or uint2 (the bf16 sweep copy's, on
+    // regular meshes) (k_a_slab -> k_galerkin_sys<2>), reused slab by slab
     DevArray<float> aslab;
     bool bf16_fresh = false;  // A0h written by the batch's assembly
 };

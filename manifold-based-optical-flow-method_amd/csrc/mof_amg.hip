@@ -429,20 +429,26 @@ __global__ __launch_bounds__(kWG) void k_galerkin0_ent(
 // (profiles/r05_ab/gal_slab/).
 constexpr int kSlab = 64;
 constexpr int kSlabPos = 64;  // fine positions per k_a_slab workgroup
+// T = float4: the fp32 A; T = uint2 (round 6, regular closed meshes -- F3):
+// the level-0 sweep copy's bf16 blocks, as the tentative product by entry
+// reads them, half the bytes for the transpose and for the product's ~7
+// reads of each block: F3 +4 %; on the open patch S1 the bf16 coarse
+// operator cost 14 of 3,072 solves a recovery (profiles/r06/slab_bf16/)
+template <typename T>
 __global__ __launch_bounds__(kWG) void k_a_slab(int64_t f_sell_nb, int32_t b0, int32_t nb,
-                                                const float4 *__restrict__ Af, float4 *__restrict__ AI) {
-    __shared__ float4 t[kSlabPos][kSlab + 1];
+                                                const T *__restrict__ Af, T *__restrict__ AI) {
+    __shared__ T t[kSlabPos][kSlab + 1];
     const int64_t q0 = (int64_t)blockIdx.x * kSlabPos;
     const int32_t lane = (int32_t)threadIdx.x & 63, w = (int32_t)threadIdx.x >> 6;
-    // read: a wave takes one system's 64 consecutive blocks (1 KB)
+    // read: a wave takes one system's 64 consecutive blocks
     for (int32_t s = w; s < kSlab; s += kWG / 64) {
         const int64_t q = q0 + lane;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        T v = {};
         if (s < nb && q < f_sell_nb) v = Af[(int64_t)(b0 + s) * f_sell_nb + q];
         t[lane][s] = v;
     }
     __syncthreads();
-    // write: a wave takes one fine position's 64 systems (1 KB)
+    // write: a wave takes one fine position's 64 systems
     for (int32_t k = w; k < kSlabPos; k += kWG / 64) {
         const int64_t q = q0 + k;
         if (q < f_sell_nb) AI[q * kSlab + lane] = t[k][lane];
@@ -451,11 +457,11 @@ __global__ __launch_bounds__(kWG) void k_a_slab(int64_t f_sell_nb, int32_t b0, i
 
 constexpr int kGalSysPos = kWG / 64;  // coarse positions per workgroup, one per wave
 // Level l's Galerkin product over one system slab: BSF = 2 reads the level-0
-// slab (k_a_slab, float4 blocks, mirror entries), BSF = 3 the slab a level
+// slab (k_a_slab, float4 blocks or, H, bf16 as uint2; mirror entries), BSF = 3 the slab a level
 // l >= 1 product wrote beside its level's A (CS: [sell_nb][kSlab][3] float4,
 // the stored rows). Gather entries per load batch: 4 at level 0, 2 on the
 // coarse levels (their P blocks are 18 scalar registers each).
-template <int BSF>
+template <int BSF, bool H = false>
 __global__ __launch_bounds__(kWG) void k_galerkin_sys(
     int64_t c_sell_nb, int32_t nC, int32_t B, int32_t b0, const int32_t *__restrict__ c_sell_row,
     const int32_t *__restrict__ c_diag, const uint8_t *__restrict__ c_dead, const int32_t *__restrict__ c_twin, const int32_t *__restrict__ gptr,
@@ -499,9 +505,14 @@ __global__ __launch_bounds__(kWG) void k_galerkin_sys(
 #pragma unroll
                     for (int c = 0; c < BSF; ++c) a[u][r][c] = (fp[u] == -1 && r == c) ? 1.f : 0.f;
             } else if constexpr (BSF == 2) {
-                const float4 v = FS[(int64_t)(fp[u] & kMirPos) * kSlab + lane];
                 const bool tr = fp[u] & kMirT;  // transposed upper block
-                a[u][0][0] = v.x; a[u][0][1] = tr ? v.z : v.y; a[u][1][0] = tr ? v.y : v.z; a[u][1][1] = v.w;
+                if constexpr (H) {
+                    const uint2 h = reinterpret_cast<const uint2 *>(FS)[(int64_t)(fp[u] & kMirPos) * kSlab + lane];
+                    h0_dec(tr ? h0_tr(h) : h, a[u][0][0], a[u][0][1], a[u][1][0], a[u][1][1]);
+                } else {
+                    const float4 v = FS[(int64_t)(fp[u] & kMirPos) * kSlab + lane];
+                    a[u][0][0] = v.x; a[u][0][1] = tr ? v.z : v.y; a[u][1][0] = tr ? v.y : v.z; a[u][1][1] = v.w;
+                }
             } else {
                 const float4 *p = FS + ((int64_t)fp[u] * kSlab + lane) * 3;
 #pragma unroll
@@ -2341,13 +2352,24 @@ void amg_setup_batch(mof_mesh *m, int32_t B, hipStream_t s) {
         const int64_t fnb = m->pat.sell_nb();
         auto sys_grid = [](int64_t nb) { return dim3(xcd_grid((int32_t)((nb + kGalSysPos - 1) / kGalSysPos), 1, 1)); };
         for (int32_t b0 = 0; b0 < B; b0 += kSlab) {
-            k_a_slab<<<dim3((unsigned)((fnb + kSlabPos - 1) / kSlabPos)), kWG, 0, s>>>(
-                fnb, b0, std::min(kSlab, B - b0), reinterpret_cast<const float4 *>(w.A32.p),
-                reinterpret_cast<float4 *>(G.aslab.p));
-            k_galerkin_sys<2><<<sys_grid(C.sell_nb), kWG, 0, s>>>(
-                C.sell_nb, C.n, B, b0, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p,
-                reinterpret_cast<const float4 *>(G.aslab.p), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C),
-                l1 ? reinterpret_cast<float4 *>(C.slab.p) : nullptr);
+            const dim3 gs((unsigned)((fnb + kSlabPos - 1) / kSlabPos));
+            if (G.regular)
+                k_a_slab<uint2><<<gs, kWG, 0, s>>>(fnb, b0, std::min(kSlab, B - b0),
+                                                   reinterpret_cast<const uint2 *>(G.A0h.p),
+                                                   reinterpret_cast<uint2 *>(G.aslab.p));
+            else
+                k_a_slab<float4><<<gs, kWG, 0, s>>>(fnb, b0, std::min(kSlab, B - b0),
+                                                    reinterpret_cast<const float4 *>(w.A32.p),
+                                                    reinterpret_cast<float4 *>(G.aslab.p));
+            auto *cs = l1 ? reinterpret_cast<float4 *>(C.slab.p) : nullptr;
+            if (G.regular)
+                k_galerkin_sys<2, true><<<sys_grid(C.sell_nb), kWG, 0, s>>>(
+                    C.sell_nb, C.n, B, b0, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p,
+                    reinterpret_cast<const float4 *>(G.aslab.p), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C), cs);
+            else
+                k_galerkin_sys<2><<<sys_grid(C.sell_nb), kWG, 0, s>>>(
+                    C.sell_nb, C.n, B, b0, C.sell_row.p, C.diag_pos.p, C.dead.p, C.twin.p, F.gptr.p, F.gent.p, F.Q.p,
+                    reinterpret_cast<const float4 *>(G.aslab.p), C.A.p, dh(C), C.Dh22.p, ah(C), ah22(C), cs);
             if (l1) {
                 AmgDevLevel &C2 = G.lv[2];
                 k_galerkin_sys<3><<<sys_grid(C2.sell_nb), kWG, 0, s>>>(
