@@ -151,7 +151,6 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
                    bool dev_io, hipStream_t s, double *V_out, mof_stats &st, mof::SpmvTiming &timing) {
     mof::SolveParams sp = sp_in;
     const int32_t K = k1 - k0;
-    const int32_t nbat = (K + B - 1) / B;
     // MOF_VERBOSE: helper-thread and wait times, and the call's setup steps,
     // on stderr
     const bool hostio_verbose = mof::knob(mof::Knob::Verbose) != nullptr;
@@ -194,8 +193,25 @@ void solve_batches(mof_mesh *m, const double *I, const double *I2, const double 
     if (hostio_verbose)
         fprintf(stderr, "[mof setup] workspace + operator %.2f ms, hierarchy %.2f ms, its storage %.2f ms, host staging %.2f ms\n",
                 tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3]);
-    auto bk = [&](int32_t q) { return k0 + q * B; };
-    auto bn = [&](int32_t q) { return std::min(B, k1 - bk(q)); };
+    // batch starts: B timesteps each; a host-pointer job of more than two
+    // batches starts and ends with a quarter batch, so the pipeline's fill
+    // (the first batch's I rows) and drain (the last batch's V) are short
+    // -- V does not depend on the split (round 6: C3's host-to-host rate
+    // over 4 batches, profiles/r06/taper/)
+    std::vector<int32_t> kst{k0};
+    if (!dev_io && !direct && K > 2 * B) {
+        const int32_t sm = std::max(1, B / 4);
+        int32_t k = k0 + sm;
+        kst.push_back(k);
+        while (k1 - k > B + sm) kst.push_back(k += B);
+        if (k1 - k > sm) kst.push_back(k1 - sm);
+    } else {
+        for (int32_t k = k0 + B; k < k1; k += B) kst.push_back(k);
+    }
+    kst.push_back(k1);
+    const int32_t nbat = (int32_t)kst.size() - 1;
+    auto bk = [&](int32_t q) { return kst[q]; };
+    auto bn = [&](int32_t q) { return kst[q + 1] - kst[q]; };
     // helper-thread steps of the host pipeline (copy stream): batch q's I rows
     // into slot q&1 once batch q-2's assembly has read it, and batch q's V
     // out of slot q&1 into V_out
