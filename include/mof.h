@@ -109,7 +109,11 @@ typedef struct mof_opts {
     uint32_t precision;    /* MOF_PREC_* */
     uint32_t flags;        /* MOF_IO_DEVICE | MOF_NO_BLOCK_JACOBI | MOF_TIME_SPMV | MOF_PRECOND_AMG */
     int32_t batch;         /* timesteps solved together per launch (0: auto =
-                              512, fewer if device memory is short) */
+                              1024, fewer if device memory is short); a
+                              host-pointer job of more than two batches runs
+                              its first and last at a quarter of it (short
+                              copy-pipeline fill and drain; V is the same for
+                              any split) */
     int32_t max_iter;      /* PCG iterations per inner solve (0: 10000; 1000
                               with MOF_PRECOND_AMG, whose inner solves take
                               tens: more means a bad preconditioner, and
